@@ -1,0 +1,49 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of the in-process engine.
+//
+// Everything here is written for 64-lane wavefronts and the CDNA4 MFMA
+// register layouts (see /opt/skills/guides/cdna_hip_programming.md §3).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define P2P_API extern "C" __attribute__((visibility("default")))
+
+static constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ bf16x8 zero_bf16x8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.0f;
+  return z;
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+// Non-temporal 16-byte load for once-read weight streams (decode GEMV).
+__device__ __forceinline__ bf16x8 load_nt(const bf16x8* p) {
+  return __builtin_nontemporal_load(p);
+}
+
+#define P2P_CHECK_LAUNCH() return (int)hipGetLastError()

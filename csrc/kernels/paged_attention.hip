@@ -1,0 +1,194 @@
+// Paged-KV attention for decode ("flash-decoding", split over the context).
+//
+// KV cache layout (engine/kv_cache.py): K and V are each
+//     [num_pages][n_kv_heads][PAGE=64][D=128] bf16
+// so one page of one kv head is a contiguous 16 KiB tile.  Every query row r
+// carries a block-table row (its sequence) and a context length; a query row
+// is either one decode token or one prefill token (causal: ctx = pos + 1).
+//
+// Grid: (chunk, kv_head, row); a chunk = 4 pages = 256 keys, one page per wave.
+// GQA packing: all G = Hq / Hkv query heads of a kv head are scored against the
+// same K/V bytes in one pass (K/V read once per group, not once per q head).
+// Within a wave each lane scores one key (full 256-B K row), softmax partials
+// are wave-reduced, then each lane owns 2 of the 128 output dims for P.V.
+// The 4 waves are merged through LDS; with one chunk the block writes the
+// final bf16 output, otherwise fp32 partials (m, l, o) for the combine kernel.
+#include "common.h"
+
+namespace {
+
+constexpr int PAGE = 64;
+constexpr int HD = 128;
+constexpr int CHUNK = 4 * PAGE;
+
+template <int G>
+__global__ __launch_bounds__(256) void paged_attn_kernel(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const int* __restrict__ bt, int bt_stride, const int* __restrict__ row_bt,
+    const int* __restrict__ ctx_lens, int Hkv, float scale, int n_chunks, bf16* __restrict__ out,
+    int ldo, float* __restrict__ part_o, float* __restrict__ part_ml) {
+  const int c = blockIdx.x, h = blockIdx.y, r = blockIdx.z;
+  const int ctx = ctx_lens[r];
+  if (c * CHUNK >= ctx) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+
+  __shared__ float qs[G][HD];
+  __shared__ float ps[4][G][PAGE];
+  __shared__ float sm[4][G], sl[4][G];
+  __shared__ float so[4][G][HD];
+
+  const bf16* qrow = q + (size_t)r * ldq + (size_t)h * G * HD;
+  for (int i = tid; i < G * HD; i += 256) qs[i / HD][i % HD] = (float)qrow[i] * scale;
+  __syncthreads();
+
+  const int pi = c * 4 + w;
+  const int n_valid = min(max(ctx - pi * PAGE, 0), PAGE);
+  float o[G][2];
+  float mg[G], lg[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    o[g][0] = o[g][1] = 0.f;
+    mg[g] = -INFINITY;
+    lg[g] = 0.f;
+  }
+  if (n_valid > 0) {
+    const int page = bt[(size_t)row_bt[r] * bt_stride + pi];
+    const size_t tile = ((size_t)page * Hkv + h) * PAGE * HD;
+    const bf16* kb = kc + tile;
+    const bf16* vb = vc + tile;
+    float s[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) s[g] = 0.f;
+    if (lane < n_valid) {
+      const bf16x8* krow = reinterpret_cast<const bf16x8*>(kb + lane * HD);
+#pragma unroll 4
+      for (int ch = 0; ch < HD / 8; ++ch) {
+        const bf16x8 kv = krow[ch];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float kf = (float)kv[j];
+#pragma unroll
+          for (int g = 0; g < G; ++g) s[g] = fmaf(qs[g][ch * 8 + j], kf, s[g]);
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float sv = lane < n_valid ? s[g] : -INFINITY;
+      mg[g] = wave_max(sv);
+      const float p = lane < n_valid ? __expf(sv - mg[g]) : 0.f;
+      lg[g] = wave_sum(p);
+      ps[w][g][lane] = p;
+    }
+    // P.V: lane owns output dims 2*lane, 2*lane+1.  ps is produced and consumed
+    // by the same wave; the LDS write->read order within a wave is preserved.
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    const bf16x2* vcol = reinterpret_cast<const bf16x2*>(vb) + lane;
+#pragma unroll 8
+    for (int t = 0; t < n_valid; ++t) {
+      const bf16x2 vv = vcol[t * (HD / 2)];
+      const float v0 = (float)vv[0], v1 = (float)vv[1];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float p = ps[w][g][t];
+        o[g][0] = fmaf(p, v0, o[g][0]);
+        o[g][1] = fmaf(p, v1, o[g][1]);
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    so[w][g][2 * lane] = o[g][0];
+    so[w][g][2 * lane + 1] = o[g][1];
+    if (lane == 0) {
+      sm[w][g] = mg[g];
+      sl[w][g] = lg[g];
+    }
+  }
+  __syncthreads();
+  const int Hq = Hkv * G;
+  for (int i = tid; i < G * HD; i += 256) {
+    const int g = i / HD, d = i % HD;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm[ww][g]);
+    float num = 0.f, den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const float e = __expf(sm[ww][g] - M);
+        num = fmaf(e, so[ww][g][d], num);
+        den = fmaf(e, sl[ww][g], den);
+      }
+    }
+    const int hq = h * G + g;
+    if (n_chunks == 1) {
+      out[(size_t)r * ldo + (size_t)hq * HD + d] = f2bf(num / den);
+    } else {
+      const size_t pidx = ((size_t)r * Hq + hq) * n_chunks + c;
+      part_o[pidx * HD + d] = num;
+      if (d == 0) {
+        part_ml[pidx * 2] = M;
+        part_ml[pidx * 2 + 1] = den;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(HD) void attn_combine_kernel(const float* __restrict__ part_o,
+                                                          const float* __restrict__ part_ml,
+                                                          const int* __restrict__ ctx_lens,
+                                                          int Hq, int n_chunks,
+                                                          bf16* __restrict__ out, int ldo) {
+  const int r = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
+  const int nc = min((ctx_lens[r] + CHUNK - 1) / CHUNK, n_chunks);
+  const size_t base = ((size_t)r * Hq + hq) * n_chunks;
+  float M = -INFINITY;
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, part_ml[(base + c) * 2]);
+  float num = 0.f, den = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    const float m = part_ml[(base + c) * 2];
+    if (m == -INFINITY) continue;
+    const float e = __expf(m - M);
+    num = fmaf(e, part_o[(base + c) * HD + d], num);
+    den = fmaf(e, part_ml[(base + c) * 2 + 1], den);
+  }
+  out[(size_t)r * ldo + (size_t)hq * HD + d] = f2bf(den > 0.f ? num / den : 0.f);
+}
+
+template <int G>
+int launch_attn(const void* q, int ldq, const void* kc, const void* vc, const int* bt,
+                int bt_stride, const int* row_bt, const int* ctx, int R, int Hkv, float scale,
+                int n_chunks, void* out, int ldo, float* part_o, float* part_ml, hipStream_t st) {
+  hipLaunchKernelGGL((paged_attn_kernel<G>), dim3(n_chunks, Hkv, R), dim3(256), 0, st,
+                     (const bf16*)q, ldq, (const bf16*)kc, (const bf16*)vc, bt, bt_stride, row_bt,
+                     ctx, Hkv, scale, n_chunks, (bf16*)out, ldo, part_o, part_ml);
+  int e = (int)hipGetLastError();
+  if (e || n_chunks == 1) return e;
+  hipLaunchKernelGGL(attn_combine_kernel, dim3(R, Hkv * G), dim3(HD), 0, st, part_o, part_ml, ctx,
+                     Hkv * G, n_chunks, (bf16*)out, ldo);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// max_ctx bounds the number of 256-key chunks (grid.x); rows whose context is
+// shorter exit early.  part_o / part_ml: workspace of R*Hq*n_chunks*(128 | 2) floats,
+// unused when max_ctx <= 256.
+P2P_API int p2p_paged_attention(const void* q, int ldq, const void* k_cache, const void* v_cache,
+                                const int* block_tables, int bt_stride, const int* row_bt,
+                                const int* ctx_lens, int R, int Hq, int Hkv, int head_dim,
+                                float scale, int max_ctx, void* out, int ldo, float* part_o,
+                                float* part_ml, hipStream_t stream) {
+  if (head_dim != HD || Hkv <= 0 || Hq % Hkv != 0 || R <= 0) return (int)hipErrorInvalidValue;
+  const int n_chunks = (max_ctx + CHUNK - 1) / CHUNK;
+  if (n_chunks > 1 && (!part_o || !part_ml)) return (int)hipErrorInvalidValue;
+  switch (Hq / Hkv) {
+    case 1: return launch_attn<1>(q, ldq, k_cache, v_cache, block_tables, bt_stride, row_bt, ctx_lens, R, Hkv, scale, n_chunks, out, ldo, part_o, part_ml, stream);
+    case 2: return launch_attn<2>(q, ldq, k_cache, v_cache, block_tables, bt_stride, row_bt, ctx_lens, R, Hkv, scale, n_chunks, out, ldo, part_o, part_ml, stream);
+    case 4: return launch_attn<4>(q, ldq, k_cache, v_cache, block_tables, bt_stride, row_bt, ctx_lens, R, Hkv, scale, n_chunks, out, ldo, part_o, part_ml, stream);
+    case 8: return launch_attn<8>(q, ldq, k_cache, v_cache, block_tables, bt_stride, row_bt, ctx_lens, R, Hkv, scale, n_chunks, out, ldo, part_o, part_ml, stream);
+  }
+  return (int)hipErrorInvalidValue;
+}

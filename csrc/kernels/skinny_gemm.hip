@@ -1,0 +1,315 @@
+// Skinny (M <= 64) bf16 GEMM on MFMA for decode / short-prefill projections.
+//
+//   out[m, n] = epilogue( rstd[m] * sum_k X[m, k] * W[n, k] )
+//
+// This is the hot loop of suggest-reply decode: at batch 1 every projection is
+// a pure weight stream (16 GB / token for Llama-3.1-8B), so the kernel is built
+// around one contiguous 1 KiB non-temporal load per wave per k-step.
+//
+// Weight layout ("fragment-major", produced once at load time by
+// ops.gemm.tile_weight):
+//     Wt[g][s][lane][j] = W[16*g + (lane & 15)][32*s + 8*(lane >> 4) + j]
+// i.e. every 16x32 (n x k) block is stored exactly as the 64 lanes hold the B
+// operand of v_mfma_f32_16x16x32_bf16.  The activation fragment (A operand,
+// lane l holds X[l & 15][8*(l >> 4) + j]) is read straight from global memory
+// (it is a few KiB and L2-resident).
+//
+// Fusions (epilogues), all replacing separate kernels of a naive decoder layer:
+//   NORM      : RMSNorm of the input row.  The RMSNorm gain is folded into the
+//               weight at load time, so only rstd[m] = rsqrt(mean(x^2)+eps)
+//               remains; the sum of squares is accumulated from the same A
+//               fragments the MFMA consumes and applied to the accumulator.
+//   EPI_RESID : residual add in place (o_proj / down_proj).
+//   EPI_SILU  : SwiGLU: the block owns gate rows g and up rows g+F/16 and
+//               writes silu(gate) * up (gate_up_proj -> act -> [M, F]).
+//   EPI_F32   : fp32 logits (LM head).
+// Split-K across the waves of a block (WAVES), reduced through LDS.
+#include "common.h"
+
+namespace {
+
+enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_F32 = 3 };
+
+template <int MT, int WAVES, int EPI, bool NORM, int U>
+__global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
+    const bf16x8* __restrict__ Wt, const bf16* __restrict__ X, int ldx, int M, int K,
+    int up_group_offset, void* __restrict__ out, int ldo, float eps) {
+  constexpr int NB = (EPI == EPI_SILU) ? 2 : 1;
+  const int S = K >> 5;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int g = blockIdx.x;
+  const int s0 = (S * w) / WAVES;
+  const int s1 = (S * (w + 1)) / WAVES;
+  const int r = lane & 15, q = lane >> 4;
+
+  const bf16x8* wp[NB];
+  wp[0] = Wt + (size_t)g * S * 64 + lane;
+  if constexpr (NB == 2) wp[NB - 1] = Wt + (size_t)(g + up_group_offset) * S * 64 + lane;
+
+  const bf16* xp[MT];
+  bool xv[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = mt * 16 + r;
+    xv[mt] = row < M;
+    xp[mt] = X + (size_t)(xv[mt] ? row : 0) * ldx + 8 * q;
+  }
+
+  f32x4 acc[NB][MT];
+  float ss[MT];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[b][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
+
+  auto load = [&](int s, bf16x8(&bw)[U][NB], bf16x8(&ax)[U][MT]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) bw[u][b] = load_nt(wp[b] + (size_t)(s + u) * 64);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        ax[u][mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + (s + u) * 32)
+                           : zero_bf16x8();
+    }
+  };
+  auto compute = [&](bf16x8(&bw)[U][NB], bf16x8(&ax)[U][MT]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[u][mt], bw[u][b], acc[b][mt], 0, 0, 0);
+        if constexpr (NORM) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xf = (float)ax[u][mt][j];
+            ss[mt] = fmaf(xf, xf, ss[mt]);
+          }
+        }
+      }
+    }
+  };
+
+  const int n = s1 - s0;
+  const int nb = n / U;
+  if (nb > 0) {
+    bf16x8 bA[U][NB], aA[U][MT], bB[U][NB], aB[U][MT];
+    load(s0, bA, aA);
+    int b = 0;
+    for (; b + 2 < nb; b += 2) {
+      load(s0 + (b + 1) * U, bB, aB);
+      compute(bA, aA);
+      load(s0 + (b + 2) * U, bA, aA);
+      compute(bB, aB);
+    }
+    if (b + 1 < nb) {
+      load(s0 + (b + 1) * U, bB, aB);
+      compute(bA, aA);
+      compute(bB, aB);
+    } else {
+      compute(bA, aA);
+    }
+  }
+  for (int s = s0 + nb * U; s < s1; ++s) {
+    bf16x8 b1[1][NB], a1[1][MT];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) b1[0][b] = load_nt(wp[b] + (size_t)s * 64);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      a1[0][mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + s * 32) : zero_bf16x8();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[0][mt], b1[0][b], acc[b][mt], 0, 0, 0);
+      if constexpr (NORM) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xf = (float)a1[0][mt][j];
+          ss[mt] = fmaf(xf, xf, ss[mt]);
+        }
+      }
+    }
+  }
+
+  // ---- split-K reduction across the block's waves ----
+  if constexpr (NORM) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      ss[mt] += __shfl_xor(ss[mt], 16, 64);
+      ss[mt] += __shfl_xor(ss[mt], 32, 64);
+    }
+  }
+  if constexpr (WAVES > 1) {
+    __shared__ float red[WAVES - 1][NB * MT * 4][64];
+    __shared__ float red_ss[WAVES][MT][16];
+    if (w > 0) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) red[w - 1][(b * MT + mt) * 4 + j][lane] = acc[b][mt][j];
+    }
+    if constexpr (NORM) {
+      if (q == 0) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) red_ss[w][mt][r] = ss[mt];
+      }
+    }
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int ww = 0; ww < WAVES - 1; ++ww)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[b][mt][j] += red[ww][(b * MT + mt) * 4 + j][lane];
+    if constexpr (NORM) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;  // recomputed per (mt, j) below
+    }
+    // epilogue with rstd from LDS
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mt * 16 + q * 4 + j;
+        if (m >= M) continue;
+        float scale = 1.f;
+        if constexpr (NORM) {
+          float t = 0.f;
+#pragma unroll
+          for (int ww = 0; ww < WAVES; ++ww) t += red_ss[ww][mt][q * 4 + j];
+          scale = rsqrtf(t / (float)K + eps);
+        }
+        const float v = acc[0][mt][j] * scale;
+        const size_t o = (size_t)m * ldo + g * 16 + r;
+        if constexpr (EPI == EPI_STORE) {
+          reinterpret_cast<bf16*>(out)[o] = f2bf(v);
+        } else if constexpr (EPI == EPI_RESID) {
+          bf16* p = reinterpret_cast<bf16*>(out) + o;
+          *p = f2bf((float)*p + v);
+        } else if constexpr (EPI == EPI_SILU) {
+          const float u = acc[NB - 1][mt][j] * scale;
+          reinterpret_cast<bf16*>(out)[o] = f2bf(silu(v) * u);
+        } else {
+          reinterpret_cast<float*>(out)[o] = v;
+        }
+      }
+    }
+  } else {
+    // single wave: rstd for row m lives in lane (m & 15) of the same m-tile.
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mt * 16 + q * 4 + j;
+        float scale = 1.f;
+        if constexpr (NORM) {
+          const float t = __shfl(ss[mt], q * 4 + j, 64);
+          scale = rsqrtf(t / (float)K + eps);
+        }
+        if (m >= M) continue;
+        const float v = acc[0][mt][j] * scale;
+        const size_t o = (size_t)m * ldo + g * 16 + r;
+        if constexpr (EPI == EPI_STORE) {
+          reinterpret_cast<bf16*>(out)[o] = f2bf(v);
+        } else if constexpr (EPI == EPI_RESID) {
+          bf16* p = reinterpret_cast<bf16*>(out) + o;
+          *p = f2bf((float)*p + v);
+        } else if constexpr (EPI == EPI_SILU) {
+          const float u = acc[NB - 1][mt][j] * scale;
+          reinterpret_cast<bf16*>(out)[o] = f2bf(silu(v) * u);
+        } else {
+          reinterpret_cast<float*>(out)[o] = v;
+        }
+      }
+    }
+  }
+}
+
+template <int MT, int WAVES, int EPI, bool NORM>
+int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
+              void* out, int ldo, float eps, hipStream_t st) {
+  constexpr int U = (MT == 1) ? 8 : 4;
+  hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>), dim3(groups), dim3(WAVES * 64), 0,
+                     st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, up_off, out, ldo, eps);
+  return (int)hipGetLastError();
+}
+
+template <int MT, int EPI, bool NORM>
+int launch_m(int waves, const void* Wt, const void* X, int ldx, int M, int K, int groups,
+             int up_off, void* out, int ldo, float eps, hipStream_t st) {
+  switch (waves) {
+    case 1: return launch_mw<MT, 1, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+    case 2: return launch_mw<MT, 2, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+    case 4: return launch_mw<MT, 4, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+    case 8: return launch_mw<MT, 8, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+template <int EPI, bool NORM>
+int launch_e(int mt, int waves, const void* Wt, const void* X, int ldx, int M, int K, int groups,
+             int up_off, void* out, int ldo, float eps, hipStream_t st) {
+  switch (mt) {
+    case 1: return launch_m<1, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+    case 2: return launch_m<2, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+    case 4: return launch_m<4, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// Picks the split-K factor so that the launch has >= ~2048 waves in flight
+// (256 CUs x 4 SIMDs x 2) while every wave still streams >= 8 k-steps.
+static int pick_waves(int groups, int K, int mt) {
+  const int S = K / 32;
+  int waves = 1;
+  while (waves < 8 && groups * waves < 2048 && S / (waves * 2) >= 8) waves *= 2;
+  // LDS budget for the reduction buffer at the largest tile (SiLU, MT=4): keep <= 64 KiB.
+  (void)mt;
+  return waves;
+}
+
+// epi: 0 store bf16, 1 residual add (bf16, in place), 2 silu(gate)*up, 3 fp32 store.
+// N: number of weight rows (for epi 2: 2*F, gate rows then up rows).
+// waves: 0 = heuristic.
+P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
+                            int norm, void* out, int ldo, float eps, int waves,
+                            hipStream_t stream) {
+  if (M <= 0 || M > 64 || (K % 32) != 0 || (N % 16) != 0) return (int)hipErrorInvalidValue;
+  const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  int groups = N / 16;
+  int up_off = 0;
+  if (epi == EPI_SILU) {
+    if ((N % 32) != 0) return (int)hipErrorInvalidValue;
+    groups = N / 32;
+    up_off = groups;
+  }
+  if (waves <= 0) waves = pick_waves(groups, K, mt);
+  if (epi == EPI_SILU && mt == 4 && waves > 4) waves = 4;
+  if (epi == EPI_STORE) {
+    return norm ? launch_e<EPI_STORE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream)
+                : launch_e<EPI_STORE, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream);
+  } else if (epi == EPI_RESID) {
+    if (norm) return (int)hipErrorInvalidValue;
+    return launch_e<EPI_RESID, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream);
+  } else if (epi == EPI_SILU) {
+    if (!norm) return (int)hipErrorInvalidValue;
+    return launch_e<EPI_SILU, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream);
+  } else if (epi == EPI_F32) {
+    return norm ? launch_e<EPI_F32, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream)
+                : launch_e<EPI_F32, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream);
+  }
+  return (int)hipErrorInvalidValue;
+}

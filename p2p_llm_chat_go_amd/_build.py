@@ -1,0 +1,167 @@
+"""In-tree native build: HIP kernels (gfx950) + C++ runtime / networking.
+
+Everything is compiled with the ROCm toolchain directly (hipcc / g++), no
+torch.utils.cpp_extension and no hipify step.  Artefacts land inside the
+package (``p2p_llm_chat_go_amd/_lib``) so that they travel with the repo
+snapshot to the GPU box.  Targets are rebuilt only when a source or header is
+newer than the artefact.
+
+Usage:  python -m p2p_llm_chat_go_amd._build [--force] [--jobs N] [--only kernels|net|...]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "p2p_llm_chat_go_amd")
+LIBDIR = os.path.join(PKG, "_lib")
+BINDIR = os.path.join(ROOT, "bin")
+BUILDDIR = os.path.join(ROOT, "build")
+CSRC = os.path.join(ROOT, "csrc")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("P2P_GPU_ARCH", "gfx950")
+
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+CXX = os.environ.get("CXX", "g++")
+
+KERNEL_LIB = os.path.join(LIBDIR, "libp2p_kernels.so")
+
+
+def _newest(paths):
+    return max((os.path.getmtime(p) for p in paths if os.path.exists(p)), default=0.0)
+
+
+def _stale(target, deps):
+    return (not os.path.exists(target)) or os.path.getmtime(target) < _newest(deps)
+
+
+def _run(cmd, cwd=None):
+    r = subprocess.run(cmd, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n  %s\n%s" % (" ".join(cmd), r.stdout[-8000:]))
+    return r.stdout
+
+
+def _headers(d):
+    return glob.glob(os.path.join(d, "*.h")) + glob.glob(os.path.join(CSRC, "include", "*.h"))
+
+
+def build_kernels(force=False, jobs=8):
+    """Compile csrc/kernels/*.hip for gfx950 into one shared library (C ABI, ctypes)."""
+    kdir = os.path.join(CSRC, "kernels")
+    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")))
+    hdrs = _headers(kdir)
+    odir = os.path.join(BUILDDIR, "kernels")
+    os.makedirs(odir, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    flags = [
+        "--offload-arch=%s" % ARCH, "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
+        "-Wno-unused-result", "-I", os.path.join(CSRC, "include"), "-I", kdir,
+    ]
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(odir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + hdrs):
+            todo.append((s, o))
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        futs = [ex.submit(_run, [HIPCC] + flags + ["-c", s, "-o", o]) for s, o in todo]
+        for f in futs:
+            f.result()
+    if force or todo or _stale(KERNEL_LIB, objs):
+        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=%s" % ARCH] + objs + ["-o", KERNEL_LIB])
+    return KERNEL_LIB
+
+
+def _py_ext_suffix():
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def build_native(force=False, jobs=8):
+    """C++ runtime + networking: static objects, pybind11 module, and daemons."""
+    import pybind11  # noqa: F401  (build dependency, present in the image)
+
+    subdirs = ["net", "runtime"]
+    odir = os.path.join(BUILDDIR, "native")
+    os.makedirs(odir, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(BINDIR, exist_ok=True)
+    inc = ["-I", os.path.join(CSRC, "include"), "-I", CSRC]
+    base = ["-O2", "-g", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-pthread"] + inc
+    srcs = []
+    for d in subdirs:
+        srcs += sorted(glob.glob(os.path.join(CSRC, d, "*.cc")))
+    hdrs = []
+    for d in subdirs + ["include"]:
+        hdrs += glob.glob(os.path.join(CSRC, d, "*.h"))
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(odir, os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + hdrs):
+            todo.append((s, o))
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(_run, [CXX] + base + ["-c", s, "-o", o]) for s, o in todo]:
+            f.result()
+    if not objs:
+        return []
+    libs = ["-lssl", "-lcrypto", "-pthread"]
+    outs = []
+    # static archive for the daemons
+    ar = os.path.join(odir, "libp2pnative.a")
+    if force or todo or _stale(ar, objs):
+        if os.path.exists(ar):
+            os.remove(ar)
+        _run(["ar", "rcs", ar] + objs)
+    # daemons
+    for app in sorted(glob.glob(os.path.join(CSRC, "apps", "*.cc"))):
+        name = os.path.splitext(os.path.basename(app))[0]
+        exe = os.path.join(BINDIR, name)
+        if force or _stale(exe, [app, ar] + hdrs):
+            _run([CXX] + base + [app, ar, "-o", exe] + libs)
+        outs.append(exe)
+    # pybind11 module
+    import pybind11
+
+    bind = sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cc")))
+    if bind:
+        mod = os.path.join(LIBDIR, "_native" + _py_ext_suffix())
+        pyinc = sysconfig.get_paths()["include"]
+        if force or _stale(mod, bind + [ar] + hdrs):
+            _run([CXX] + base + ["-shared", "-I", pybind11.get_include(), "-I", pyinc] + bind
+                 + [ar, "-o", mod] + libs)
+        outs.append(mod)
+    return outs
+
+
+def build(force=False, jobs=8, only=None):
+    outs = []
+    if only in (None, "kernels"):
+        if shutil.which(HIPCC) or os.path.exists(HIPCC):
+            outs.append(build_kernels(force, jobs))
+        else:
+            print("hipcc not found; skipping HIP kernels", file=sys.stderr)
+    if only in (None, "native"):
+        outs += build_native(force, jobs)
+    return outs
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--only", choices=["kernels", "native"], default=None)
+    a = ap.parse_args(argv)
+    for o in build(a.force, a.jobs, a.only):
+        print(o)
+
+
+if __name__ == "__main__":
+    main()

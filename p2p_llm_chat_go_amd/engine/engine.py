@@ -1,0 +1,211 @@
+"""In-process suggest-reply engine (replaces the reference's Ollama HTTP hop).
+
+The reference's only LLM call is ``POST {OLLAMA_URL}/api/generate`` with
+``stream: false`` (`web/streamlit_app.py:89-101`); Ollama answers with the
+text plus ``prompt_eval_count/_duration`` and ``eval_count/_duration``.  This
+engine produces the same record in-process:
+
+  prefill   : all prompt tokens of the batch as one flat row list (chunked at
+              ``max_prefill_tokens``), causal paged attention, LM head on the last
+              row of each sequence only, greedy argmax -> first token (TTFT).
+  decode    : hipGraph replay of the whole step (engine.graph), state advanced
+              on the device; EOS is checked every ``check_every`` steps.
+
+Continuous batching across peers lives in ``engine.scheduler``; this class is
+the execution backend it drives (``prefill`` / ``decode_graph``).
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+
+import torch
+
+from ..models.config import ModelConfig
+from ..models.llama import LlamaModel
+from ..models.weights import EngineWeights
+from ..ops import PAGE
+from .graph import DecodeGraph, DecodeState
+from .kv_cache import KVCache, pages_for
+
+BATCH_BUCKETS = (1, 2, 4, 8, 16, 32, 64)
+CTX_BUCKETS = (256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 131072)
+
+
+def bucket(x, buckets):
+    for b in buckets:
+        if x <= b:
+            return b
+    raise ValueError("%d exceeds the largest bucket %d" % (x, buckets[-1]))
+
+
+@dataclasses.dataclass
+class GenResult:
+    tokens: list
+    prompt_eval_count: int
+    prompt_eval_duration_ns: int
+    eval_count: int
+    eval_duration_ns: int
+    total_duration_ns: int
+    ttft_ns: int
+    done_reason: str = "length"
+
+
+class Engine:
+    def __init__(self, cfg: ModelConfig, weights: EngineWeights | None = None, device="cuda",
+                 seed: int = 0, kv_pages: int | None = None, max_prefill_tokens: int = 1024,
+                 max_batch: int = 64, use_graph: bool = True, comm=None, tp_rank: int = 0,
+                 tp_size: int = 1, kv_fraction: float = 0.85):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if weights is None:
+            weights = EngineWeights.random(cfg, self.device, seed=seed, tp_rank=tp_rank,
+                                           tp_size=tp_size)
+        self.weights = weights
+        if kv_pages is None:
+            self.kv = KVCache.from_free_memory(cfg, self.device, fraction=kv_fraction,
+                                               tp_size=tp_size)
+        else:
+            self.kv = KVCache(cfg, kv_pages, self.device, tp_size)
+        self.model = LlamaModel(weights, self.kv, comm)
+        self.max_prefill_tokens = max_prefill_tokens
+        self.max_batch = max_batch
+        self.use_graph = use_graph
+        self._prefill_ws = {}
+        self._graphs = {}
+
+    # -------------------------------------------------------------- helpers
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def prefill_workspace(self, max_ctx):
+        key = bucket(max_ctx, CTX_BUCKETS)
+        ws = self._prefill_ws.get(key)
+        if ws is None:
+            ws = self.model.new_workspace(self.max_prefill_tokens, key, max_out_rows=self.max_batch)
+            self._prefill_ws[key] = ws
+        return ws
+
+    def decode_graph(self, B: int, ctx: int) -> DecodeGraph:
+        key = (bucket(B, BATCH_BUCKETS), bucket(ctx, CTX_BUCKETS))
+        g = self._graphs.get(key)
+        if g is None:
+            st = DecodeState(self.model, key[0], key[1] // PAGE, key[1], key[1])
+            g = DecodeGraph(st, self.use_graph).capture()
+            self._graphs[key] = g
+        return g
+
+    def warmup(self, batch_sizes=(1,), ctx=256):
+        for b in batch_sizes:
+            self.decode_graph(b, ctx)
+
+    # -------------------------------------------------------------- prefill
+    def prefill(self, prompts: list, block_tables: list, return_logits: bool = False):
+        """Run all prompts (flat rows, chunked at max_prefill_tokens).
+
+        Returns int32 first tokens [B] on the device (and, with return_logits,
+        the fp32 last-position logits [B, V_local] of every sequence).
+        """
+        dev = self.device
+        B = len(prompts)
+        max_ctx = max(len(p) for p in prompts)
+        ws = self.prefill_workspace(max_ctx)
+        max_pages = bucket(max_ctx, CTX_BUCKETS) // PAGE
+        bt = torch.zeros(B, max(max_pages, max(len(b) for b in block_tables)), dtype=torch.int32)
+        for b, pages in enumerate(block_tables):
+            bt[b, :len(pages)] = torch.tensor(pages, dtype=torch.int32)
+        rows = []  # (seq, pos, token)
+        for b, p in enumerate(prompts):
+            rows += [(b, i, t) for i, t in enumerate(p)]
+        bt_d = bt.to(dev, non_blocking=True)
+        first = torch.zeros(B, dtype=torch.int32, device=dev)
+        all_logits = None
+        if return_logits:
+            all_logits = torch.zeros(B, ws.logits.shape[1], dtype=torch.float32, device=dev)
+        C = self.max_prefill_tokens
+        for c0 in range(0, len(rows), C):
+            chunk = rows[c0:c0 + C]
+            R = len(chunk)
+            seq = torch.tensor([r[0] for r in chunk], dtype=torch.int32)
+            pos = torch.tensor([r[1] for r in chunk], dtype=torch.int32)
+            ids = torch.tensor([r[2] for r in chunk], dtype=torch.int32)
+            slots = bt[seq.long(), (pos // PAGE).long()] * PAGE + pos % PAGE
+            # rows that end a sequence inside this chunk need logits
+            outs, out_seq = [], []
+            for j, (b, i, _t) in enumerate(chunk):
+                if i == len(prompts[b]) - 1:
+                    outs.append(j)
+                    out_seq.append(b)
+            host = torch.stack([seq, pos, ids, slots, pos + 1])
+            dev_t = host.to(dev, non_blocking=True)
+            seq_d, pos_d, ids_d, slots_d, ctx_d = dev_t[0], dev_t[1], dev_t[2], dev_t[3], dev_t[4]
+            out_rows = torch.tensor(outs or [0], dtype=torch.int32).to(dev, non_blocking=True)
+            logits = self.model.forward(ws, ids_d, pos_d, slots_d, bt_d, seq_d, ctx_d, R,
+                                        max_ctx, out_rows=out_rows, n_out=len(outs))
+            if not outs:
+                continue
+            toks = self.model.sample_greedy(ws, logits)
+            sel = torch.tensor(out_seq, dtype=torch.long).to(dev, non_blocking=True)
+            first.index_copy_(0, sel, toks)
+            if all_logits is not None:
+                all_logits.index_copy_(0, sel, logits)
+        return (first, all_logits) if return_logits else first
+
+    # ------------------------------------------------------------- generate
+    def generate(self, prompts: list, max_new_tokens: int = 64, stop_on_eos: bool = True,
+                 check_every: int = 8) -> list:
+        """Greedy suggest-reply for a static batch of prompts (token id lists)."""
+        t0 = time.perf_counter_ns()
+        B = len(prompts)
+        assert 0 < B <= self.max_batch
+        need = [len(p) + max_new_tokens for p in prompts]
+        pages = [self.kv.allocator.alloc(pages_for(n)) for n in need]
+        try:
+            first = self.prefill(prompts, pages)
+            first_h = first.cpu()  # sync: first token is on the host -> TTFT
+            t1 = time.perf_counter_ns()
+            out = [[int(first_h[b])] for b in range(B)]
+            done = [stop_on_eos and out[b][0] in self.cfg.eos_ids for b in range(B)]
+            n_dec = max_new_tokens - 1
+            steps_run = 0
+            if n_dec > 0 and not all(done):
+                g = self.decode_graph(B, max(need))
+                st = g.state
+                st.load([o[0] for o in out], [len(p) for p in prompts], pages)
+                while steps_run < n_dec:
+                    k = n_dec - steps_run if not stop_on_eos else min(check_every,
+                                                                      n_dec - steps_run)
+                    g.replay(k)
+                    steps_run += k
+                    if stop_on_eos:
+                        h = st.hist[:B, :steps_run].cpu()
+                        for b in range(B):
+                            if not done[b] and any(int(t) in self.cfg.eos_ids for t in h[b]):
+                                done[b] = True
+                        if all(done):
+                            break
+                hist = st.hist[:B, :steps_run].cpu()
+                for b in range(B):
+                    out[b] += [int(t) for t in hist[b]]
+            else:
+                self._sync()
+            t2 = time.perf_counter_ns()
+        finally:
+            for p in pages:
+                self.kv.allocator.free(p)
+        res = []
+        for b in range(B):
+            toks = out[b][:max_new_tokens]
+            reason = "length"
+            if stop_on_eos:
+                for j, t in enumerate(toks):
+                    if t in self.cfg.eos_ids:
+                        toks = toks[:j]
+                        reason = "stop"
+                        break
+            res.append(GenResult(tokens=toks, prompt_eval_count=len(prompts[b]),
+                                 prompt_eval_duration_ns=t1 - t0, eval_count=len(toks),
+                                 eval_duration_ns=t2 - t1, total_duration_ns=t2 - t0,
+                                 ttft_ns=t1 - t0, done_reason=reason))
+        return res

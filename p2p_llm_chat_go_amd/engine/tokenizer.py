@@ -1,0 +1,133 @@
+"""Tokenizers and the suggest-reply prompt.
+
+* ``HFTokenizer`` loads a real ``tokenizer.json`` (Llama-3 tiktoken-BPE or
+  Mixtral SentencePiece exported to HF format) through the ``tokenizers``
+  package when a file is supplied (``TOKENIZER_PATH`` or a checkpoint dir).
+* ``SyntheticTokenizer`` is the offline default (no tokenizer files on the
+  box): a deterministic word-level tokenizer whose token counts track BPE on
+  English chat text (one token per word / punctuation mark), which is all the
+  benchmark depends on.  Ids are stable hashes into the model vocabulary;
+  decoding returns words it has seen and ``<id>`` placeholders otherwise.
+
+``suggest_prompt`` reproduces the reference co-pilot template verbatim
+(`web/streamlit_app.py:93`) and ``chat_ids`` wraps it the way Ollama's
+llama3.1 template does (one user turn, assistant header open).
+"""
+from __future__ import annotations
+
+import os
+import re
+import zlib
+
+SUGGEST_TEMPLATE = ("You are a helpful assistant. Draft a concise, friendly reply to the following "
+                    "message:\n\n{prompt}\n\nReply:")
+
+LLAMA3_SPECIAL = {
+    "<|begin_of_text|>": 128000, "<|end_of_text|>": 128001, "<|start_header_id|>": 128006,
+    "<|end_header_id|>": 128007, "<|eom_id|>": 128008, "<|eot_id|>": 128009,
+}
+
+
+def suggest_prompt(message: str) -> str:
+    return SUGGEST_TEMPLATE.format(prompt=message)
+
+
+class SyntheticTokenizer:
+    _pat = re.compile(r"\s*\w+|\s*[^\w\s]|\s+")
+
+    def __init__(self, vocab: int = 128256, n_special: int = 256, bos_id=None, eos_ids=None,
+                 llama3: bool | None = None):
+        self.vocab = vocab
+        self.llama3 = vocab >= 128256 if llama3 is None else llama3
+        self.hi = vocab - n_special if not self.llama3 else 128000
+        self.lo = 3
+        self.bos_id = bos_id if bos_id is not None else (128000 if self.llama3 else 1)
+        self.eos_ids = tuple(eos_ids) if eos_ids else ((128009, 128001) if self.llama3 else (2,))
+        self._seen = {}
+
+    def _id(self, piece: str) -> int:
+        h = zlib.crc32(piece.encode("utf-8"))
+        i = self.lo + h % (self.hi - self.lo)
+        self._seen.setdefault(i, piece)
+        return i
+
+    def encode(self, text: str, bos: bool = False) -> list:
+        ids = [self.bos_id] if bos else []
+        ids += [self._id(m.group(0)) for m in self._pat.finditer(text) if m.group(0)]
+        return ids
+
+    def decode(self, ids) -> str:
+        out = []
+        inv = {v: k for k, v in LLAMA3_SPECIAL.items()} if self.llama3 else {}
+        for i in ids:
+            i = int(i)
+            if i in inv or i == self.bos_id or i in self.eos_ids:
+                continue
+            out.append(self._seen.get(i, " <%d>" % i))
+        return "".join(out).strip()
+
+    def chat_ids(self, user_text: str) -> list:
+        if self.llama3:
+            S = LLAMA3_SPECIAL
+            ids = [S["<|begin_of_text|>"], S["<|start_header_id|>"]] + self.encode("user") + [
+                S["<|end_header_id|>"]] + self.encode("\n\n" + user_text) + [S["<|eot_id|>"],
+                                                                           S["<|start_header_id|>"]]
+            return ids + self.encode("assistant") + [S["<|end_header_id|>"]] + self.encode("\n\n")
+        return [self.bos_id] + self.encode("[INST] " + user_text + " [/INST]")
+
+
+class HFTokenizer:
+    def __init__(self, path: str, eos_ids=None):
+        from tokenizers import Tokenizer
+
+        if os.path.isdir(path):
+            path = os.path.join(path, "tokenizer.json")
+        self.tok = Tokenizer.from_file(path)
+        self.vocab = self.tok.get_vocab_size()
+        self.llama3 = self.tok.token_to_id("<|begin_of_text|>") is not None
+        if self.llama3:
+            self.bos_id = self.tok.token_to_id("<|begin_of_text|>")
+        else:
+            self.bos_id = self.tok.token_to_id("<s>") or 1
+        self.eos_ids = tuple(eos_ids) if eos_ids else tuple(
+            i for i in (self.tok.token_to_id("<|eot_id|>"), self.tok.token_to_id("<|end_of_text|>"),
+                        self.tok.token_to_id("</s>")) if i is not None)
+
+    def encode(self, text: str, bos: bool = False) -> list:
+        ids = self.tok.encode(text, add_special_tokens=False).ids
+        return ([self.bos_id] if bos else []) + ids
+
+    def decode(self, ids) -> str:
+        return self.tok.decode([int(i) for i in ids], skip_special_tokens=True).strip()
+
+    def chat_ids(self, user_text: str) -> list:
+        if self.llama3:
+            t = self.tok.token_to_id
+            return ([self.bos_id, t("<|start_header_id|>")] + self.encode("user")
+                    + [t("<|end_header_id|>")] + self.encode("\n\n" + user_text)
+                    + [t("<|eot_id|>"), t("<|start_header_id|>")] + self.encode("assistant")
+                    + [t("<|end_header_id|>")] + self.encode("\n\n"))
+        return [self.bos_id] + self.encode("[INST] " + user_text + " [/INST]")
+
+
+def get_tokenizer(cfg=None, path: str | None = None):
+    path = path or os.environ.get("TOKENIZER_PATH")
+    if path and os.path.exists(path):
+        return HFTokenizer(path, eos_ids=getattr(cfg, "eos_ids", None))
+    if cfg is None:
+        return SyntheticTokenizer()
+    return SyntheticTokenizer(vocab=cfg.vocab, bos_id=cfg.bos_id, eos_ids=cfg.eos_ids,
+                              llama3=cfg.vocab >= 128256)
+
+
+# Synthetic incoming chat messages (the screenshot's kind of traffic).
+SAMPLE_MESSAGES = [
+    "Hey! How's it going?",
+    "Are we still on for lunch tomorrow at noon? I can book a table near the office.",
+    "Thanks for sending the slides yesterday, they looked great. Any chance you could add the Q3 numbers?",
+    "I just landed in Berlin, the flight was delayed by two hours. Can we move our call to 6pm?",
+    "Did you see the game last night? That last-minute goal was unbelievable!",
+    "Quick question: do you know where the spare keys for the storage room are?",
+    "Happy birthday!! Hope you have an amazing day and a great year ahead.",
+    "My laptop keeps freezing when I open the project, have you seen this before?",
+]

@@ -1,0 +1,128 @@
+"""Llama / Mixtral decoder forward on the engine's kernels.
+
+One ``forward`` serves prefill and decode: its input is a flat list of *query
+rows* (tokens) with per-row position, KV slot, sequence (block-table row) and
+context length.  Per layer (TP=1, dense):
+
+    qkv   = rstd(h) * h @ Wqkv'          skinny_gemm  NORM | STORE
+    q,k,v = rope(qkv); k,v -> KV pages   rope_cache
+    a     = paged_attention(q, pages)    paged_attention (GQA-packed)
+    h    += a @ Wo                       skinny_gemm  RESID
+    act   = silu(g) * u, [g|u] = rstd(h) * h @ Wgu'   skinny_gemm NORM | SILU
+    h    += act @ Wdown                  skinny_gemm  RESID
+
+i.e. 6 launches per layer, every RMSNorm / residual add / SwiGLU fused into
+a GEMM.  With TP>1 the row-parallel outputs (o_proj, down) go to a scratch
+buffer and ``comm.allreduce_add_(h, partial)`` sums them into the residual.
+MoE layers (Mixtral) route through ``models.moe``.
+
+Every buffer lives in a preallocated ``Workspace`` so the decode step can be
+captured in a hipGraph (``engine.graph``).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .config import ModelConfig, rope_table
+from .weights import EngineWeights
+
+
+class Workspace:
+    def __init__(self, cfg: ModelConfig, max_rows: int, max_ctx: int, device, tp_size: int = 1,
+                 max_out_rows: int | None = None):
+        dev = torch.device(device)
+        self.max_rows = max_rows
+        self.max_ctx = max_ctx
+        nq = cfg.n_heads // tp_size
+        nkv = cfg.n_kv_heads // tp_size
+        D = cfg.head_dim
+        bf = torch.bfloat16
+        self.h = torch.zeros(max_rows, cfg.hidden, device=dev, dtype=bf)
+        self.qkv = torch.zeros(max_rows, (nq + 2 * nkv) * D, device=dev, dtype=bf)
+        self.q = torch.zeros(max_rows, nq * D, device=dev, dtype=bf)
+        self.attn = torch.zeros(max_rows, nq * D, device=dev, dtype=bf)
+        self.act = torch.zeros(max_rows, cfg.ffn // tp_size, device=dev, dtype=bf)
+        self.partial = torch.zeros(max_rows, cfg.hidden, device=dev, dtype=bf) if tp_size > 1 or cfg.is_moe else None
+        mo = max_out_rows or max_rows
+        self.last = torch.zeros(mo, cfg.hidden, device=dev, dtype=bf)
+        self.logits = torch.zeros(mo, cfg.vocab // tp_size, device=dev, dtype=torch.float32)
+        self.ids_out = torch.zeros(mo, device=dev, dtype=torch.int32)
+        self.attn_ws = ops.attn_workspace(max_rows, nq, max_ctx, dev)
+        self.moe = None  # lazily sized by models.moe
+
+
+class LlamaModel:
+    def __init__(self, weights: EngineWeights, kv, comm=None):
+        self.w = weights
+        self.cfg = weights.cfg
+        self.kv = kv
+        self.comm = comm
+        self.tp = weights.tp_size
+        self.device = weights.device
+        self.nq = self.cfg.n_heads // self.tp
+        self.nkv = self.cfg.n_kv_heads // self.tp
+        max_pos = min(self.cfg.max_pos, 1 << 17)
+        self.rope = rope_table(self.cfg, max_pos=max_pos, device=self.device)
+
+    def new_workspace(self, max_rows, max_ctx, max_out_rows=None) -> Workspace:
+        return Workspace(self.cfg, max_rows, max_ctx, self.device, self.tp, max_out_rows)
+
+    # ----------------------------------------------------------------- layers
+    def _row_parallel(self, wt, x, h, ws, R):
+        """h += x @ W (row-parallel across TP ranks)."""
+        if self.tp == 1:
+            ops.skinny_gemm(wt, x, ops.EPI_RESID, out=h)
+        else:
+            part = ws.partial[:R]
+            ops.skinny_gemm(wt, x, ops.EPI_STORE, out=part)
+            self.comm.allreduce_add_(h, part)
+
+    def _mlp(self, lw, ws, R):
+        h = ws.h[:R]
+        if self.cfg.is_moe:
+            from . import moe
+
+            moe.moe_forward(self, lw, ws, R)
+            return
+        act = ws.act[:R]
+        ops.skinny_gemm(lw.gate_up, h, ops.EPI_SILU, norm=True, out=act, eps=self.cfg.eps)
+        self._row_parallel(lw.down, act, h, ws, R)
+
+    def forward(self, ws: Workspace, ids, pos, slots, block_tables, row_bt, ctx_lens, R: int,
+                max_ctx: int, out_rows=None, n_out: int | None = None):
+        """Run all layers on R query rows; return fp32 logits of the selected rows.
+
+        out_rows: int32 [n_out] indices of rows whose logits are needed (prefill:
+        the last token of each sequence); None = all R rows (decode).
+        """
+        cfg = self.cfg
+        h = ws.h[:R]
+        ops.gather_rows(self.w.embed, ids[:R], out=h)
+        q, qkv, attn = ws.q[:R], ws.qkv[:R], ws.attn[:R]
+        for i, lw in enumerate(self.w.layers):
+            kc, vc = self.kv.layer(i)
+            ops.skinny_gemm(lw.qkv, h, ops.EPI_STORE, norm=True, out=qkv, eps=cfg.eps)
+            ops.rope_cache(qkv, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc, vc)
+            ops.paged_attention(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R], self.nq,
+                                self.nkv, max_ctx, out=attn, workspace=ws.attn_ws)
+            self._row_parallel(lw.o, attn, h, ws, R)
+            self._mlp(lw, ws, R)
+        if n_out == 0:
+            return None
+        if out_rows is None:
+            x = h
+            n = R
+        else:
+            n = n_out if n_out is not None else out_rows.shape[0]
+            x = ops.gather_rows(h, out_rows[:n], out=ws.last[:n])
+        logits = ws.logits[:n]
+        ops.skinny_gemm(self.w.lm_head, x, ops.EPI_F32, norm=True, out=logits, eps=cfg.eps)
+        return logits
+
+    def sample_greedy(self, ws: Workspace, logits, out=None):
+        n = logits.shape[0]
+        out = ws.ids_out[:n] if out is None else out
+        if self.tp == 1:
+            return ops.argmax(logits, out=out)
+        return self.comm.vocab_parallel_argmax(logits, out, self.cfg.vocab // self.tp)

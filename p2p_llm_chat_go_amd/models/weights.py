@@ -1,0 +1,193 @@
+"""Engine weight store: HF checkpoint / random init -> folded, sharded, MFMA-tiled.
+
+Load-time transforms (all one-off, none on the hot path):
+  * RMSNorm gains are folded into the projection that consumes the normed
+    activations (input_layernorm -> qkv, post_attention_layernorm -> gate_up /
+    router / experts, model.norm -> lm_head); the kernels then only apply
+    rstd (``ops.gemm``).
+  * q|k|v rows are concatenated into one qkv projection; gate|up into one
+    gate_up projection (SwiGLU epilogue pairs row g with row g + F).
+  * Tensor-parallel sharding (Megatron): qkv / gate_up / lm_head split by
+    output rows (heads, ffn columns, vocab), o_proj / down split by input
+    columns; the row-parallel outputs are summed by ``parallel.comm``.
+  * Every projection is re-laid out fragment-major (``ops.tile_weight``).
+
+Random init (BASELINE: no checkpoints on the box) draws N(0, std) directly in
+the tiled layout -- statistically identical to tiling a random natural
+matrix, without the transient copy (a 70B model is ~140 GB).
+"""
+from __future__ import annotations
+
+import dataclasses
+import glob
+import json
+import os
+
+import torch
+
+from .. import ops
+from .config import ModelConfig
+
+
+@dataclasses.dataclass
+class LayerWeights:
+    qkv: torch.Tensor          # tiled [(nq+2nkv)/tp * D, H]
+    o: torch.Tensor            # tiled [H, nq/tp * D]
+    gate_up: torch.Tensor | None = None   # tiled [2F/tp, H]
+    down: torch.Tensor | None = None      # tiled [H, F/tp]
+    # MoE
+    router: torch.Tensor | None = None    # natural [E, H] bf16 (norm folded), replicated
+    w13: torch.Tensor | None = None       # tiled per local expert [E_local, 2F/16, H/32, 64, 8]
+    w2: torch.Tensor | None = None        # tiled per local expert [E_local, H/16, F/32, 64, 8]
+
+
+@dataclasses.dataclass
+class EngineWeights:
+    cfg: ModelConfig
+    embed: torch.Tensor        # [V, H] bf16 (full table, replicated)
+    lm_head: torch.Tensor      # tiled [V/tp, H] (final norm folded)
+    layers: list
+    tp_rank: int = 0
+    tp_size: int = 1
+    ep_rank: int = 0
+    ep_size: int = 1
+
+    @property
+    def device(self):
+        return self.embed.device
+
+    def nbytes(self) -> int:
+        n = self.embed.numel() + self.lm_head.numel()
+        for lw in self.layers:
+            for f in dataclasses.fields(lw):
+                t = getattr(lw, f.name)
+                if t is not None:
+                    n += t.numel()
+        return 2 * n
+
+    # ------------------------------------------------------------------ build
+    @classmethod
+    def from_state_dict(cls, sd: dict, cfg: ModelConfig, device="cpu", tp_rank=0, tp_size=1,
+                        ep_rank=0, ep_size=1) -> "EngineWeights":
+        D, nh, nkv, F = cfg.head_dim, cfg.n_heads, cfg.n_kv_heads, cfg.ffn
+        assert nh % tp_size == 0 and nkv % tp_size == 0, "heads must divide tp"
+        qs, ks = nh // tp_size * D, nkv // tp_size * D
+        dev = torch.device(device)
+
+        def get(name):
+            return sd[name].to(dev)
+
+        def tile(w):
+            return ops.tile_weight(w.to(torch.bfloat16).contiguous())
+
+        layers = []
+        for i in range(cfg.n_layers):
+            p = "model.layers.%d." % i
+            g_in = get(p + "input_layernorm.weight")
+            g_post = get(p + "post_attention_layernorm.weight")
+            q = get(p + "self_attn.q_proj.weight")[tp_rank * qs:(tp_rank + 1) * qs]
+            k = get(p + "self_attn.k_proj.weight")[tp_rank * ks:(tp_rank + 1) * ks]
+            v = get(p + "self_attn.v_proj.weight")[tp_rank * ks:(tp_rank + 1) * ks]
+            qkv = ops.fold_norm(torch.cat([q, k, v], 0), g_in)
+            o = get(p + "self_attn.o_proj.weight")[:, tp_rank * qs:(tp_rank + 1) * qs]
+            lw = LayerWeights(qkv=tile(qkv), o=tile(o))
+            if cfg.is_moe:
+                E = cfg.n_experts
+                assert E % ep_size == 0
+                el = E // ep_size
+                lw.router = ops.fold_norm(get(p + "block_sparse_moe.gate.weight"), g_post).contiguous()
+                w13, w2 = [], []
+                Fs = F // tp_size
+                for e in range(ep_rank * el, (ep_rank + 1) * el):
+                    q_ = p + "block_sparse_moe.experts.%d." % e
+                    w1 = get(q_ + "w1.weight")[tp_rank * Fs:(tp_rank + 1) * Fs]
+                    w3 = get(q_ + "w3.weight")[tp_rank * Fs:(tp_rank + 1) * Fs]
+                    w13.append(tile(ops.fold_norm(torch.cat([w1, w3], 0), g_post)))
+                    w2.append(tile(get(q_ + "w2.weight")[:, tp_rank * Fs:(tp_rank + 1) * Fs]))
+                lw.w13 = torch.stack(w13).contiguous()
+                lw.w2 = torch.stack(w2).contiguous()
+            else:
+                Fs = F // tp_size
+                gate = get(p + "mlp.gate_proj.weight")[tp_rank * Fs:(tp_rank + 1) * Fs]
+                up = get(p + "mlp.up_proj.weight")[tp_rank * Fs:(tp_rank + 1) * Fs]
+                lw.gate_up = tile(ops.fold_norm(torch.cat([gate, up], 0), g_post))
+                lw.down = tile(get(p + "mlp.down_proj.weight")[:, tp_rank * Fs:(tp_rank + 1) * Fs])
+            layers.append(lw)
+        embed = get("model.embed_tokens.weight").to(torch.bfloat16).contiguous()
+        head = embed if cfg.tie_embeddings else get("lm_head.weight")
+        Vs = cfg.vocab // tp_size
+        head = ops.fold_norm(head[tp_rank * Vs:(tp_rank + 1) * Vs], get("model.norm.weight"))
+        return cls(cfg, embed, tile(head), layers, tp_rank, tp_size, ep_rank, ep_size)
+
+    @classmethod
+    def random(cls, cfg: ModelConfig, device="cuda", seed=0, std=0.02, tp_rank=0, tp_size=1,
+               ep_rank=0, ep_size=1) -> "EngineWeights":
+        """Random-init weights generated directly in the tiled layout (see module doc)."""
+        dev = torch.device(device)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed * 1000003 + tp_rank * 7919 + ep_rank * 104729)
+        H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
+
+        def rnd_tiled(n, k, s=std, lead=()):
+            t = torch.empty(*lead, n // 16, k // 32, 64, 8, device=dev, dtype=torch.bfloat16)
+            t.normal_(0.0, s, generator=gen)
+            return t
+
+        qkv_rows = (cfg.n_heads + 2 * cfg.n_kv_heads) // tp_size * D
+        q_cols = cfg.n_heads // tp_size * D
+        Fs = F // tp_size
+        layers = []
+        for _ in range(cfg.n_layers):
+            lw = LayerWeights(qkv=rnd_tiled(qkv_rows, H), o=rnd_tiled(H, q_cols))
+            if cfg.is_moe:
+                el = cfg.n_experts // ep_size
+                lw.router = torch.empty(cfg.n_experts, H, device=dev, dtype=torch.bfloat16).normal_(
+                    0.0, 0.5, generator=gen)
+                lw.w13 = rnd_tiled(2 * Fs, H, lead=(el,))
+                lw.w2 = rnd_tiled(H, Fs, lead=(el,))
+            else:
+                lw.gate_up = rnd_tiled(2 * Fs, H)
+                lw.down = rnd_tiled(H, Fs)
+            layers.append(lw)
+        embed = torch.empty(cfg.vocab, H, device=dev, dtype=torch.bfloat16).normal_(0.0, 1.0,
+                                                                                    generator=gen)
+        head = rnd_tiled(cfg.vocab // tp_size, H)
+        return cls(cfg, embed, head, layers, tp_rank, tp_size, ep_rank, ep_size)
+
+
+def load_safetensors_dir(path: str, device="cpu") -> dict:
+    """Read every ``*.safetensors`` shard of an HF checkpoint directory (no pickle)."""
+    from safetensors.torch import load_file
+
+    sd = {}
+    files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+    if not files:
+        raise FileNotFoundError("no .safetensors files under %s" % path)
+    for f in files:
+        sd.update(load_file(f, device=str(device)))
+    return sd
+
+
+def config_from_hf(path: str, base: ModelConfig | None = None) -> ModelConfig:
+    """Build a ModelConfig from an HF ``config.json`` (Llama / Mixtral)."""
+    with open(os.path.join(path, "config.json")) as f:
+        c = json.load(f)
+    rs = c.get("rope_scaling") or None
+    llama3 = None
+    if rs and rs.get("rope_type", rs.get("type")) == "llama3":
+        llama3 = (float(rs["factor"]), float(rs["low_freq_factor"]), float(rs["high_freq_factor"]),
+                  int(rs["original_max_position_embeddings"]))
+    eos = c.get("eos_token_id", 2)
+    eos = tuple(eos) if isinstance(eos, list) else (eos,)
+    return ModelConfig(
+        name=c.get("_name_or_path", os.path.basename(path.rstrip("/"))) or "hf",
+        hidden=c["hidden_size"], n_layers=c["num_hidden_layers"],
+        n_heads=c["num_attention_heads"], n_kv_heads=c.get("num_key_value_heads",
+                                                           c["num_attention_heads"]),
+        ffn=c["intermediate_size"], vocab=c["vocab_size"],
+        head_dim=c.get("head_dim", c["hidden_size"] // c["num_attention_heads"]),
+        rope_theta=float(c.get("rope_theta", 10000.0)), rope_llama3=llama3,
+        eps=float(c.get("rms_norm_eps", 1e-5)), max_pos=int(c.get("max_position_embeddings", 8192)),
+        n_experts=int(c.get("num_local_experts", 0)), top_k=int(c.get("num_experts_per_tok", 0)),
+        tie_embeddings=bool(c.get("tie_word_embeddings", False)),
+        bos_id=int(c.get("bos_token_id", 1)), eos_ids=eos)

@@ -1,0 +1,97 @@
+"""ctypes binding of the gfx950 kernel library (``_lib/libp2p_kernels.so``).
+
+The kernels take raw device pointers and the caller's HIP stream, so every
+launch lands on ``torch.cuda.current_stream()`` and is captured by
+``torch.cuda.graph`` (hipGraph) like any other work on that stream.
+
+torch must be imported first: it brings its own ``libamdhip64.so.7`` and the
+kernel library resolves against that already-loaded runtime (same soname),
+so there is exactly one HIP runtime in the process.
+
+On a machine with a GPU the library is mandatory: ``lib()`` raises if it is
+missing or fails to load (no silent eager fallback).  CPU tensors never reach
+this module (ops dispatch CPU tensors to their PyTorch reference path).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib",
+                         "libp2p_kernels.so")
+_lock = threading.Lock()
+_lib = None
+
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_void_p = ctypes.c_void_p
+
+_SIGS = {
+    # name: argtypes (all return int hipError_t)
+    "p2p_skinny_gemm": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                        c_int, c_float, c_int, c_void_p],
+    "p2p_paged_attention": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                            c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int,
+                            c_void_p, c_void_p, c_void_p],
+    "p2p_gather_rows": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
+    "p2p_rope_cache": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                       c_void_p, c_int, c_void_p, c_void_p, c_void_p],
+    "p2p_argmax": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
+    "p2p_advance": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                    c_void_p, c_int, c_void_p],
+}
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def lib():
+    """Load (once) and return the kernel library; raise if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(_LIB_PATH):
+            raise KernelError(
+                "HIP kernel library missing at %s -- run `python -m p2p_llm_chat_go_amd._build` "
+                "(or __graft_entry__.build())" % _LIB_PATH)
+        L = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = args
+            fn.restype = c_int
+        _lib = L
+        return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(err: int, name: str):
+    if err != 0:
+        raise KernelError("%s failed with hipError %d" % (name, err))
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,115 @@
+"""Paged-KV attention (decode + per-token causal prefill) and RoPE/KV-cache write.
+
+KV cache layout: ``[num_pages, n_kv_heads, PAGE=64, head_dim=128]`` bf16 for K
+and for V (see ``engine/kv_cache.py``).  A *query row* is one token with its
+sequence's block-table row and a context length (number of keys it attends,
+positions ``0 .. ctx-1``), so decode (ctx = pos+1 of the new token) and causal
+prefill (one row per prompt token) share one kernel.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+PAGE = 64
+HEAD_DIM = 128
+CHUNK = 256
+
+
+def attn_workspace(rows: int, n_heads: int, max_ctx: int, device) -> tuple:
+    n_chunks = max(1, (max_ctx + CHUNK - 1) // CHUNK)
+    if n_chunks == 1:
+        return None, None
+    part_o = torch.empty(rows * n_heads * n_chunks * HEAD_DIM, device=device, dtype=torch.float32)
+    part_ml = torch.empty(rows * n_heads * n_chunks * 2, device=device, dtype=torch.float32)
+    return part_o, part_ml
+
+
+def _gather_kv(cache, bt_row, ctx, h):
+    pos = torch.arange(ctx, device=cache.device)
+    pages = bt_row[pos // PAGE].long()
+    return cache[pages, h, pos % PAGE].float()  # [ctx, D]
+
+
+def paged_attention_ref(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_kv,
+                        scale, out):
+    R = q.shape[0]
+    G = n_heads // n_kv
+    qv = q.view(R, n_heads, HEAD_DIM).float()
+    res = torch.empty(R, n_heads, HEAD_DIM, dtype=torch.float32, device=q.device)
+    for r in range(R):
+        ctx = int(ctx_lens[r])
+        bt_row = block_tables[int(row_bt[r])]
+        for h in range(n_kv):
+            K = _gather_kv(k_cache, bt_row, ctx, h)
+            V = _gather_kv(v_cache, bt_row, ctx, h)
+            qh = qv[r, h * G:(h + 1) * G]  # [G, D]
+            s = (qh @ K.t()) * scale
+            p = torch.softmax(s, dim=-1)
+            res[r, h * G:(h + 1) * G] = p @ V
+    out.view(R, n_heads, HEAD_DIM).copy_(res.to(out.dtype))
+    return out
+
+
+def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                    block_tables: torch.Tensor, row_bt: torch.Tensor, ctx_lens: torch.Tensor,
+                    n_heads: int, n_kv: int, max_ctx: int, out: torch.Tensor | None = None,
+                    workspace: tuple | None = None, scale: float | None = None) -> torch.Tensor:
+    """q: [R, n_heads*128] bf16 -> out [R, n_heads*128] bf16."""
+    R = q.shape[0]
+    if scale is None:
+        scale = 1.0 / math.sqrt(HEAD_DIM)
+    if out is None:
+        out = torch.empty(R, n_heads * HEAD_DIM, device=q.device, dtype=q.dtype)
+    if q.device.type != "cuda":
+        return paged_attention_ref(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads,
+                                   n_kv, scale, out)
+    if workspace is None:
+        workspace = attn_workspace(R, n_heads, max_ctx, q.device)
+    po, pml = workspace
+    L = _lib.lib()
+    _lib.check(L.p2p_paged_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(),
+                                     v_cache.data_ptr(), block_tables.data_ptr(),
+                                     block_tables.stride(0), row_bt.data_ptr(), ctx_lens.data_ptr(),
+                                     R, n_heads, n_kv, HEAD_DIM, float(scale), int(max_ctx),
+                                     out.data_ptr(), out.stride(0), _lib.ptr(po), _lib.ptr(pml),
+                                     _lib.stream_ptr(q.device)), "paged_attention")
+    return out
+
+
+def rope_cache_ref(qkv, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_cache):
+    T = qkv.shape[0]
+    D = HEAD_DIM
+    x = qkv.view(T, n_heads + 2 * n_kv, D).float()
+    cs = cos_sin[pos.long()]  # [T, 64, 2]
+    c, s = cs[..., 0][:, None, :], cs[..., 1][:, None, :]
+    qk = x[:, :n_heads + n_kv]
+    x1, x2 = qk[..., :D // 2], qk[..., D // 2:]
+    rot = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+    q_out.view(T, n_heads, D).copy_(rot[:, :n_heads].to(q_out.dtype))
+    for t in range(T):
+        slot = int(slots[t])
+        if slot < 0:
+            continue
+        page, off = slot // PAGE, slot % PAGE
+        k_cache[page, :, off] = rot[t, n_heads:].to(k_cache.dtype)
+        v_cache[page, :, off] = x[t, n_heads + n_kv:].to(v_cache.dtype)
+    return q_out
+
+
+def rope_cache(qkv: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor, cos_sin: torch.Tensor,
+               n_heads: int, n_kv: int, q_out: torch.Tensor, k_cache: torch.Tensor,
+               v_cache: torch.Tensor) -> torch.Tensor:
+    """Rotate q/k (HF rotate_half, llama3-scaled table), write k/v to the paged cache."""
+    T = qkv.shape[0]
+    if qkv.device.type != "cuda":
+        return rope_cache_ref(qkv, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_cache)
+    L = _lib.lib()
+    _lib.check(L.p2p_rope_cache(qkv.data_ptr(), qkv.stride(0), pos.data_ptr(), slots.data_ptr(),
+                                cos_sin.data_ptr(), T, n_heads, n_kv, HEAD_DIM, q_out.data_ptr(),
+                                q_out.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                _lib.stream_ptr(qkv.device)), "rope_cache")
+    return q_out

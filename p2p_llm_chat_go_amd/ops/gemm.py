@@ -1,0 +1,93 @@
+"""Projection GEMMs on the fragment-major weight layout.
+
+Weights are stored once, at load time, in the layout the MFMA B operand wants
+(``csrc/kernels/skinny_gemm.hip`` header): a ``[N/16, K/32, 64, 8]`` bf16
+tensor where tile ``[g, s]`` is exactly what the 64 lanes of a wave hold for
+``v_mfma_f32_16x16x32_bf16``.  The decode weight stream is then one contiguous
+1 KiB load per wave per k-step.
+
+GPU tensors run the HIP kernels (mandatory); CPU tensors run the PyTorch
+reference of the same math (used by the tiny-llama CPU config and as the
+numerics oracle in tests).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+EPI_STORE, EPI_RESID, EPI_SILU, EPI_F32 = 0, 1, 2, 3
+SKINNY_MAX_M = 64
+
+
+def tile_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] (nn.Linear layout) -> fragment-major [N/16, K/32, 64, 8]."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 32 == 0, (N, K)
+    # W_t[g, s, q, r, j] = W[16 g + r, 32 s + 8 q + j]
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(
+        N // 16, K // 32, 64, 8)
+
+
+def untile_weight(wt: torch.Tensor) -> torch.Tensor:
+    G, S = wt.shape[0], wt.shape[1]
+    return wt.reshape(G, S, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(G * 16, S * 32)
+
+
+def tiled_shape(wt: torch.Tensor):
+    return wt.shape[0] * 16, wt.shape[1] * 32  # (N, K)
+
+
+def fold_norm(w: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
+    """Fold an RMSNorm gain into the consuming projection: W' = W * diag(gain)."""
+    return (w.float() * gain.float()[None, :]).to(w.dtype)
+
+
+def _ref(wt, x, epi, norm, out, eps):
+    N, K = tiled_shape(wt)
+    W = untile_weight(wt).float()
+    xf = x.float()
+    acc = xf @ W.t()
+    if norm:
+        rstd = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+        acc = acc * rstd
+    if epi == EPI_STORE:
+        out.copy_(acc.to(out.dtype))
+    elif epi == EPI_RESID:
+        out.copy_((out.float() + acc).to(out.dtype))
+    elif epi == EPI_SILU:
+        F = N // 2
+        g, u = acc[:, :F], acc[:, F:]
+        out.copy_((torch.nn.functional.silu(g) * u).to(out.dtype))
+    elif epi == EPI_F32:
+        out.copy_(acc)
+    else:
+        raise ValueError(epi)
+    return out
+
+
+def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: bool = False,
+                out: torch.Tensor | None = None, eps: float = 1e-5, waves: int = 0) -> torch.Tensor:
+    """out = epi(rstd(x) * x @ W^T) for x [M, K] with M <= 64 (rows > 64 are chunked)."""
+    N, K = tiled_shape(wt)
+    M = x.shape[0]
+    assert x.shape[1] == K and x.dtype == torch.bfloat16, (x.shape, K, x.dtype)
+    n_out = N // 2 if epi == EPI_SILU else N
+    if out is None:
+        if epi == EPI_RESID:
+            raise ValueError("EPI_RESID needs the residual tensor as `out`")
+        out = torch.empty(M, n_out, device=x.device,
+                          dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
+    if x.device.type != "cuda":
+        return _ref(wt, x, epi, norm, out, eps)
+    assert x.stride(1) == 1 and out.stride(1) == 1
+    L = _lib.lib()
+    s = _lib.stream_ptr(x.device)
+    for m0 in range(0, M, SKINNY_MAX_M):
+        mc = min(SKINNY_MAX_M, M - m0)
+        xs = x[m0:m0 + mc]
+        os_ = out[m0:m0 + mc]
+        _lib.check(L.p2p_skinny_gemm(wt.data_ptr(), xs.data_ptr(), x.stride(0), mc, K, N, epi,
+                                     int(norm), os_.data_ptr(), out.stride(0), float(eps), waves, s),
+                   "skinny_gemm")
+    return out

@@ -1,0 +1,109 @@
+"""End-to-end engine numerics: tiny-llama (CPU plumbing config) and GPU paths.
+
+Greedy comparisons are teacher-forced: the engine's logits for the reference's
+token stream must match the fp32 oracle within bf16 tolerance, and the engine's
+argmax must equal the oracle's wherever the oracle's top-2 margin is not a
+near-tie (random-init models have many near-ties).
+"""
+import pytest
+import torch
+
+from p2p_llm_chat_go_amd.engine import Engine
+from p2p_llm_chat_go_amd.models import TINY_LLAMA
+from p2p_llm_chat_go_amd.models.reference import (random_state_dict, reference_forward,
+                                                  reference_greedy)
+from p2p_llm_chat_go_amd.models.weights import EngineWeights
+
+
+def _check_prefill_logits(eng, sd, cfg, prompts):
+    """Engine prefill logits of the last prompt token vs oracle."""
+    from p2p_llm_chat_go_amd.engine.kv_cache import pages_for
+
+    pages = [eng.kv.allocator.alloc(pages_for(len(p) + 1)) for p in prompts]
+    try:
+        _first, logits = eng.prefill(prompts, pages, return_logits=True)
+        logits = logits.float().cpu()
+    finally:
+        for p in pages:
+            eng.kv.allocator.free(p)
+    for b, p in enumerate(prompts):
+        ref = reference_forward(sd, cfg, torch.tensor(p))[-1]
+        rel = (logits[b] - ref).norm() / ref.norm()
+        assert rel < 3e-2, rel
+
+
+def _greedy_ok(sd, cfg, prompt, got, margin=2e-2):
+    toks = list(prompt)
+    for t in got:
+        ref = reference_forward(sd, cfg, torch.tensor(toks))[-1]
+        top = ref.topk(2)
+        if int(top.indices[0]) != t:
+            gap = float(top.values[0] - ref[t])
+            assert gap < margin * float(ref.abs().max()), (t, top, gap)
+        toks.append(t)
+
+
+@pytest.mark.parametrize("chunk", [16, 1024])
+def test_tiny_engine_cpu(chunk):
+    cfg = TINY_LLAMA
+    sd = random_state_dict(cfg, seed=1)
+    w = EngineWeights.from_state_dict(sd, cfg, "cpu")
+    eng = Engine(cfg, weights=w, device="cpu", kv_pages=64, max_prefill_tokens=chunk, max_batch=4)
+    prompts = [[1, 5, 9, 33, 100, 7], list(range(3, 40)), [4]]
+    _check_prefill_logits(eng, sd, cfg, prompts)
+    res = eng.generate(prompts, max_new_tokens=6, stop_on_eos=False)
+    for p, r in zip(prompts, res):
+        assert len(r.tokens) == 6
+        _greedy_ok(sd, cfg, p, r.tokens)
+    assert res[0].tokens == reference_greedy(sd, cfg, prompts[0], 6)
+
+
+def test_engine_stop_on_eos_cpu():
+    cfg = TINY_LLAMA.replace(eos_ids=tuple(range(0, 512)))  # every token is EOS
+    sd = random_state_dict(cfg, seed=2)
+    eng = Engine(cfg, weights=EngineWeights.from_state_dict(sd, cfg, "cpu"), device="cpu",
+                 kv_pages=16)
+    r = eng.generate([[3, 4, 5]], max_new_tokens=10)[0]
+    assert r.tokens == [] and r.done_reason == "stop"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_tiny_engine_gpu(use_graph):
+    cfg = TINY_LLAMA
+    sd = random_state_dict(cfg, seed=1)
+    w = EngineWeights.from_state_dict(sd, cfg, "cuda")
+    eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_prefill_tokens=16, max_batch=4,
+                 use_graph=use_graph)
+    prompts = [[1, 5, 9, 33, 100, 7], list(range(3, 40)), [4]]
+    _check_prefill_logits(eng, sd, cfg, prompts)
+    res = eng.generate(prompts, max_new_tokens=8, stop_on_eos=False)
+    for p, r in zip(prompts, res):
+        assert len(r.tokens) == 8
+        _greedy_ok(sd, cfg, p, r.tokens)
+
+
+@pytest.mark.gpu
+def test_graph_equals_eager_gpu():
+    cfg = TINY_LLAMA.replace(n_layers=3)
+    w = EngineWeights.random(cfg, "cuda", seed=3)
+    prompts = [[1, 2, 3, 4, 5], [9] * 70]
+    outs = []
+    for g in (False, True):
+        eng = Engine(cfg, weights=w, device="cuda", kv_pages=32, max_batch=2, use_graph=g)
+        outs.append([r.tokens for r in eng.generate(prompts, 20, stop_on_eos=False)])
+    assert outs[0] == outs[1]
+
+
+@pytest.mark.gpu
+def test_llama8b_two_layers_gpu():
+    from p2p_llm_chat_go_amd.models import LLAMA31_8B
+
+    cfg = LLAMA31_8B.replace(n_layers=2)
+    sd = random_state_dict(cfg, seed=4)
+    w = EngineWeights.from_state_dict(sd, cfg, "cuda")
+    eng = Engine(cfg, weights=w, device="cuda", kv_pages=16, max_batch=2)
+    prompts = [list(range(100, 150))]
+    _check_prefill_logits(eng, sd, cfg, prompts)
+    r = eng.generate(prompts, 4, stop_on_eos=False)[0]
+    _greedy_ok(sd, cfg, prompts[0], r.tokens)

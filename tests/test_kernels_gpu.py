@@ -1,0 +1,184 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (run on an MI355X)."""
+import math
+
+import pytest
+import torch
+
+from p2p_llm_chat_go_amd import ops
+from p2p_llm_chat_go_amd.ops import attention as A
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    ops.kernel_lib()  # native library must load on the GPU box
+
+
+# ----------------------------------------------------------------- skinny GEMM
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 33, 64, 100])
+@pytest.mark.parametrize("K,N", [(256, 128), (4096, 512), (1024, 4096)])
+@pytest.mark.parametrize("norm", [False, True])
+def test_skinny_gemm_store(M, K, N, norm):
+    torch.manual_seed(M * 7 + K + N)
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    Wt = ops.tile_weight(W)
+    ref = x.float() @ W.float().t()
+    if norm:
+        ref = ref * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    out = ops.skinny_gemm(Wt.to(DEV), x.to(DEV), ops.EPI_STORE, norm=norm)
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("waves", [1, 2, 4, 8])
+def test_skinny_gemm_waves_and_f32(waves):
+    torch.manual_seed(waves)
+    M, K, N = 5, 2048, 256
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    ref = (x.float() @ W.float().t()) * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    out = ops.skinny_gemm(ops.tile_weight(W).to(DEV), x.to(DEV), ops.EPI_F32, norm=True,
+                          waves=waves)
+    assert out.dtype == torch.float32
+    assert _rel(out.cpu(), ref) < 5e-3
+
+
+@pytest.mark.parametrize("M", [1, 7, 40])
+def test_skinny_gemm_resid(M):
+    torch.manual_seed(M)
+    K, N = 14336 // 4, 1024
+    W = (torch.randn(N, K) * 0.02).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    h = torch.randn(M, N).to(torch.bfloat16)
+    ref = h.float() + x.float() @ W.float().t()
+    hd = h.to(DEV)
+    ops.skinny_gemm(ops.tile_weight(W).to(DEV), x.to(DEV), ops.EPI_RESID, out=hd)
+    assert _rel(hd.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 9, 64])
+def test_skinny_gemm_silu(M):
+    torch.manual_seed(M + 1)
+    K, F = 1024, 768
+    W = (torch.randn(2 * F, K) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    acc = (x.float() @ W.float().t()) * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    ref = torch.nn.functional.silu(acc[:, :F]) * acc[:, F:]
+    out = ops.skinny_gemm(ops.tile_weight(W).to(DEV), x.to(DEV), ops.EPI_SILU, norm=True)
+    assert out.shape == (M, F)
+    assert _rel(out.cpu(), ref) < 1e-2
+
+
+def test_skinny_gemm_matches_cpu_path_bitwise_shape():
+    # the CPU reference path of the same op agrees with the kernel
+    torch.manual_seed(3)
+    W = (torch.randn(256, 512) * 0.05).to(torch.bfloat16)
+    x = torch.randn(4, 512).to(torch.bfloat16)
+    Wt = ops.tile_weight(W)
+    a = ops.skinny_gemm(Wt, x, ops.EPI_F32, norm=True)
+    b = ops.skinny_gemm(Wt.to(DEV), x.to(DEV), ops.EPI_F32, norm=True).cpu()
+    assert _rel(b, a) < 5e-3
+
+
+# ------------------------------------------------------------ paged attention
+def _make_cache(P, Hkv, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    k = torch.randn(P, Hkv, 64, 128, generator=g).to(torch.bfloat16)
+    v = torch.randn(P, Hkv, 64, 128, generator=g).to(torch.bfloat16)
+    return k, v
+
+
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("ctxs", [[1], [63, 64, 65], [300, 7], [1000, 257, 1]])
+def test_paged_attention(G, ctxs):
+    Hkv = 2
+    Hq = Hkv * G
+    B = len(ctxs)
+    max_ctx = max(ctxs)
+    npg = (max_ctx + 63) // 64
+    P = 1 + B * npg
+    k, v = _make_cache(P, Hkv, seed=G)
+    perm = torch.randperm(P - 1)[:B * npg] + 1  # scattered pages
+    bt = perm.view(B, npg).to(torch.int32)
+    q = torch.randn(B, Hq * 128).to(torch.bfloat16)
+    row_bt = torch.arange(B, dtype=torch.int32)
+    ctx = torch.tensor(ctxs, dtype=torch.int32)
+    ref = A.paged_attention_ref(q, k, v, bt, row_bt, ctx, Hq, Hkv, 1 / math.sqrt(128),
+                                torch.empty(B, Hq * 128, dtype=torch.float32))
+    out = ops.paged_attention(q.to(DEV), k.to(DEV), v.to(DEV), bt.to(DEV), row_bt.to(DEV),
+                              ctx.to(DEV), Hq, Hkv, max_ctx)
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref) < 1e-2
+
+
+def test_paged_attention_spike_forces_rescale():
+    # one key dominates: exercises the max/exp path across waves and chunks
+    Hkv, G = 1, 4
+    k, v = _make_cache(9, Hkv, seed=5)
+    q = torch.randn(1, G * 128).to(torch.bfloat16)
+    k[3, 0, 17] = (q.view(G, 128)[0] * 4).to(torch.bfloat16)
+    bt = torch.arange(1, 9, dtype=torch.int32)[None]
+    ctx = torch.tensor([500], dtype=torch.int32)
+    rb = torch.zeros(1, dtype=torch.int32)
+    ref = A.paged_attention_ref(q, k, v, bt, rb, ctx, G, Hkv, 1 / math.sqrt(128),
+                                torch.empty(1, G * 128))
+    out = ops.paged_attention(q.to(DEV), k.to(DEV), v.to(DEV), bt.to(DEV), rb.to(DEV),
+                              ctx.to(DEV), G, Hkv, 500)
+    assert _rel(out.cpu(), ref) < 1e-2
+
+
+# ------------------------------------------------------------ rope + cache
+def test_rope_cache():
+    from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
+
+    Hq, Hkv, T = 8, 2, 37
+    cs = rope_table(LLAMA31_8B, max_pos=4096)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * 128).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32)
+    slots = torch.randperm(8 * 64)[:T].to(torch.int32)
+    slots[3] = -1
+    kc = torch.zeros(8, Hkv, 64, 128, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    q = torch.zeros(T, Hq * 128, dtype=torch.bfloat16)
+    A.rope_cache_ref(qkv, pos, slots, cs, Hq, Hkv, q, kc, vc)
+    kd, vd, qd = kc.zero_().to(DEV), vc.zero_().to(DEV), torch.zeros_like(q).to(DEV)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    A.rope_cache_ref(qkv, pos, slots, cs, Hq, Hkv, q, kc2, vc2)
+    ops.rope_cache(qkv.to(DEV), pos.to(DEV), slots.to(DEV), cs.to(DEV), Hq, Hkv, qd, kd, vd)
+    torch.cuda.synchronize()
+    assert _rel(qd.cpu(), q) < 1e-2
+    assert _rel(kd.cpu(), kc2) < 1e-2
+    assert torch.equal(vd.cpu(), vc2)
+
+
+# ------------------------------------------------------------ small kernels
+def test_gather_argmax_advance():
+    src = torch.randn(1000, 256).to(torch.bfloat16)
+    idx = torch.tensor([5, 999, 0, 5], dtype=torch.int32)
+    out = ops.gather_rows(src.to(DEV), idx.to(DEV))
+    assert torch.equal(out.cpu(), src[idx.long()])
+    logits = torch.randn(3, 128256)
+    logits[1, 77777] = 100.0
+    am = ops.argmax(logits.to(DEV))
+    assert am.cpu().tolist() == logits.argmax(-1).tolist()
+    B = 3
+    ids = torch.tensor([7, 8, 9], dtype=torch.int32)
+    pos = torch.tensor([63, 0, 130], dtype=torch.int32)
+    bt = torch.tensor([[4, 5, 6], [7, 8, 9], [1, 2, 3]], dtype=torch.int32)
+    ctx = pos + 1
+    slots = torch.zeros(B, dtype=torch.int32)
+    hist = torch.zeros(B, 4, dtype=torch.int32)
+    step = torch.zeros(1, dtype=torch.int32)
+    d = [t.to(DEV) for t in (ids, pos, ctx, slots, bt, hist, step)]
+    ops.advance(*d)
+    ops.advance(ids, pos, ctx, slots, bt, hist, step)
+    for a, b in zip(d, (ids, pos, ctx, slots, bt, hist, step)):
+        assert torch.equal(a.cpu(), b)
+    assert slots.tolist() == [5 * 64 + 0, 7 * 64 + 1, 3 * 64 + 3]
