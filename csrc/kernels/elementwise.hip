@@ -99,13 +99,18 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ 
 // Graph-resident decode-state advance for B sequences (one thread each):
 //   hist[b, *step] = ids[b]; pos[b] += 1; ctx[b] = pos[b] + 1;
 //   slot[b] = bt[b][pos / 64] * 64 + pos % 64;  then (*step)++ by thread 0.
-__global__ void advance_kernel(const int* __restrict__ ids, int* __restrict__ pos,
-                               int* __restrict__ ctx, int* __restrict__ slots,
-                               const int* __restrict__ bt, int bt_stride, int* __restrict__ hist,
-                               int hist_stride, int* __restrict__ step, int B) {
+__global__ void advance_kernel(int* __restrict__ ids, unsigned long long* __restrict__ keys,
+                               int* __restrict__ pos, int* __restrict__ ctx,
+                               int* __restrict__ slots, const int* __restrict__ bt, int bt_stride,
+                               int* __restrict__ hist, int hist_stride, int* __restrict__ step,
+                               int B) {
   const int b = threadIdx.x;
   const int st = *step;
   if (b < B) {
+    if (keys) {  // greedy keys from the fused LM-head argmax -> token ids; reset for next step
+      ids[b] = (int)(0xFFFFFFFFu - (unsigned)(keys[b] & 0xFFFFFFFFull));
+      keys[b] = 0ull;
+    }
     if (hist) hist[(size_t)b * hist_stride + st] = ids[b];
     const int p = pos[b] + 1;
     pos[b] = p;
@@ -116,7 +121,22 @@ __global__ void advance_kernel(const int* __restrict__ ids, int* __restrict__ po
   if (b == 0) *step = st + 1;
 }
 
+__global__ void argmax_finalize_kernel(unsigned long long* __restrict__ keys, int* __restrict__ ids,
+                                       int M) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < M) {
+    ids[m] = (int)(0xFFFFFFFFu - (unsigned)(keys[m] & 0xFFFFFFFFull));
+    keys[m] = 0ull;
+  }
+}
+
 }  // namespace
+
+P2P_API int p2p_argmax_finalize(unsigned long long* keys, int* ids, int M, hipStream_t st) {
+  if (M <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(argmax_finalize_kernel, dim3((M + 255) / 256), dim3(256), 0, st, keys, ids, M);
+  return (int)hipGetLastError();
+}
 
 P2P_API int p2p_gather_rows(const void* src, const int* idx, int T, int H, void* out, int ldo,
                             hipStream_t st) {
@@ -142,11 +162,11 @@ P2P_API int p2p_argmax(const float* logits, int M, int V, int ld, int* out, hipS
   return (int)hipGetLastError();
 }
 
-P2P_API int p2p_advance(const int* ids, int* pos, int* ctx, int* slots, const int* bt,
-                        int bt_stride, int* hist, int hist_stride, int* step, int B,
+P2P_API int p2p_advance(int* ids, unsigned long long* keys, int* pos, int* ctx, int* slots,
+                        const int* bt, int bt_stride, int* hist, int hist_stride, int* step, int B,
                         hipStream_t st) {
   if (B <= 0 || B > 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(((B + 63) / 64) * 64), 0, st, ids, pos, ctx,
-                     slots, bt, bt_stride, hist, hist_stride, step, B);
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(((B + 63) / 64) * 64), 0, st, ids, keys, pos,
+                     ctx, slots, bt, bt_stride, hist, hist_stride, step, B);
   return (int)hipGetLastError();
 }

@@ -32,17 +32,35 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   if (c * CHUNK >= ctx) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 
+  // V rows are transposed through LDS: row stride 136 bf16 (272 B) keeps both
+  // the per-lane 16-B row writes and the per-lane 4-B column reads conflict-free.
+  constexpr int VS = HD + 8;
   __shared__ float qs[G][HD];
+  __shared__ __attribute__((aligned(16))) bf16 vs[4][PAGE][VS];
   __shared__ float ps[4][G][PAGE];
   __shared__ float sm[4][G], sl[4][G];
   __shared__ float so[4][G][HD];
 
+  const int pi = c * 4 + w;
+  const int n_valid = min(max(ctx - pi * PAGE, 0), PAGE);
+
+  // 1) issue every global load of this wave up front (one memory latency):
+  //    lane t holds K row t and V row t of its page (16 x 16 B each).
+  bf16x8 kr[HD / 8], vr[HD / 8];
+  if (lane < n_valid) {
+    const int page = bt[(size_t)row_bt[r] * bt_stride + pi];
+    const size_t tile = ((size_t)page * Hkv + h) * PAGE * HD + (size_t)lane * HD;
+    const bf16x8* kp = reinterpret_cast<const bf16x8*>(kc + tile);
+    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vc + tile);
+#pragma unroll
+    for (int ch = 0; ch < HD / 8; ++ch) kr[ch] = kp[ch];
+#pragma unroll
+    for (int ch = 0; ch < HD / 8; ++ch) vr[ch] = vp[ch];
+  }
   const bf16* qrow = q + (size_t)r * ldq + (size_t)h * G * HD;
   for (int i = tid; i < G * HD; i += 256) qs[i / HD][i % HD] = (float)qrow[i] * scale;
   __syncthreads();
 
-  const int pi = c * 4 + w;
-  const int n_valid = min(max(ctx - pi * PAGE, 0), PAGE);
   float o[G][2];
   float mg[G], lg[G];
 #pragma unroll
@@ -52,25 +70,23 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
     lg[g] = 0.f;
   }
   if (n_valid > 0) {
-    const int page = bt[(size_t)row_bt[r] * bt_stride + pi];
-    const size_t tile = ((size_t)page * Hkv + h) * PAGE * HD;
-    const bf16* kb = kc + tile;
-    const bf16* vb = vc + tile;
+    // 2) scores: lane t scores key t against the G query heads of this kv head.
     float s[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) s[g] = 0.f;
     if (lane < n_valid) {
-      const bf16x8* krow = reinterpret_cast<const bf16x8*>(kb + lane * HD);
-#pragma unroll 4
+#pragma unroll
       for (int ch = 0; ch < HD / 8; ++ch) {
-        const bf16x8 kv = krow[ch];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float kf = (float)kv[j];
+          const float kf = (float)kr[ch][j];
 #pragma unroll
           for (int g = 0; g < G; ++g) s[g] = fmaf(qs[g][ch * 8 + j], kf, s[g]);
         }
       }
+      bf16x8* vrow = reinterpret_cast<bf16x8*>(&vs[w][lane][0]);
+#pragma unroll
+      for (int ch = 0; ch < HD / 8; ++ch) vrow[ch] = vr[ch];
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -80,14 +96,13 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
       lg[g] = wave_sum(p);
       ps[w][g][lane] = p;
     }
-    // P.V: lane owns output dims 2*lane, 2*lane+1.  ps is produced and consumed
-    // by the same wave; the LDS write->read order within a wave is preserved.
+    // 3) P.V from the wave's own LDS rows (same-wave LDS ops stay in order):
+    //    lane owns output dims 2*lane, 2*lane+1.
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
-    const bf16x2* vcol = reinterpret_cast<const bf16x2*>(vb) + lane;
-#pragma unroll 8
+#pragma unroll 4
     for (int t = 0; t < n_valid; ++t) {
-      const bf16x2 vv = vcol[t * (HD / 2)];
+      const bf16x2 vv = *reinterpret_cast<const bf16x2*>(&vs[w][t][2 * lane]);
       const float v0 = (float)vv[0], v1 = (float)vv[1];
 #pragma unroll
       for (int g = 0; g < G; ++g) {

@@ -23,17 +23,100 @@
 //   EPI_SILU  : SwiGLU: the block owns gate rows g and up rows g+F/16 and
 //               writes silu(gate) * up (gate_up_proj -> act -> [M, F]).
 //   EPI_F32   : fp32 logits (LM head).
+//   EPI_QKV_ROPE : qkv projection + RoPE + paged KV-cache write.  Weight rows of
+//               every head are permuted at load time (ops.gemm.rope_row_perm) so
+//               that each 16-row group holds dims {8k..8k+7} and {64+8k..64+8k+7};
+//               the rotate_half partner of lane r is lane r^8 (one shuffle).  q goes
+//               to q_out, k (rotated) and v to their pages -- no qkv round trip.
+//   EPI_ARGMAX: greedy sampling fused into the LM head: per-row max over the
+//               block's 16 columns, then one 64-bit atomicMax of
+//               (ordered(value) << 32 | ~index) per row and block (ties -> lowest id).
 // Split-K across the waves of a block (WAVES), reduced through LDS.
 #include "common.h"
 
 namespace {
 
-enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_F32 = 3 };
+enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_F32 = 3, EPI_QKV_ROPE = 4,
+             EPI_ARGMAX = 5 };
+
+constexpr int PAGE = 64;
+constexpr int HD = 128;
+
+struct EpiArgs {
+  // EPI_QKV_ROPE
+  const int* pos;
+  const int* slots;
+  const float2* cs;  // [max_pos][64] (cos, sin)
+  bf16* q_out;
+  int ldq;
+  bf16* kc;
+  bf16* vc;
+  int Hq, Hkv;
+  // EPI_ARGMAX: global column offset of this shard (vocab-parallel LM head)
+  int col_offset;
+};
+
+__device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) {
+  unsigned u = __float_as_uint(v);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (unsigned long long)(0xFFFFFFFFu - idx);
+}
+
+// Stores one accumulator element (row m, local column r of group g).  Called by
+// all 64 lanes of the epilogue wave (the QKV/ARGMAX epilogues shuffle).
+template <int EPI>
+__device__ __forceinline__ void epi_store(int m, bool valid, int g, int r, float v, float u,
+                                          void* __restrict__ out, int ldo, const EpiArgs& ea) {
+  if constexpr (EPI == EPI_QKV_ROPE) {
+    const float vp = __shfl_xor(v, 8, 64);
+    if (!valid) return;
+    const int head = g >> 3, k = g & 7;
+    const int d = (r < 8) ? 8 * k + r : 64 + 8 * k + (r - 8);
+    if (head < ea.Hq + ea.Hkv) {
+      const float2 c = ea.cs[(size_t)ea.pos[m] * 64 + (d & 63)];
+      const float y = (r < 8) ? (v * c.x - vp * c.y) : (v * c.x + vp * c.y);
+      if (head < ea.Hq) {
+        ea.q_out[(size_t)m * ea.ldq + (size_t)head * HD + d] = f2bf(y);
+      } else {
+        const int slot = ea.slots[m];
+        if (slot >= 0)
+          ea.kc[(((size_t)(slot / PAGE) * ea.Hkv + (head - ea.Hq)) * PAGE + slot % PAGE) * HD + d] =
+              f2bf(y);
+      }
+    } else {
+      const int slot = ea.slots[m];
+      if (slot >= 0)
+        ea.vc[(((size_t)(slot / PAGE) * ea.Hkv + (head - ea.Hq - ea.Hkv)) * PAGE + slot % PAGE) *
+                  HD + d] = f2bf(v);
+    }
+  } else if constexpr (EPI == EPI_ARGMAX) {
+    unsigned long long key = argmax_key(v, (unsigned)(ea.col_offset + g * 16 + r));
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const unsigned long long ok = __shfl_xor(key, o, 64);
+      key = ok > key ? ok : key;
+    }
+    if (valid && r == 0) atomicMax(reinterpret_cast<unsigned long long*>(out) + m, key);
+  } else {
+    if (!valid) return;
+    const size_t o = (size_t)m * ldo + g * 16 + r;
+    if constexpr (EPI == EPI_STORE) {
+      reinterpret_cast<bf16*>(out)[o] = f2bf(v);
+    } else if constexpr (EPI == EPI_RESID) {
+      bf16* p = reinterpret_cast<bf16*>(out) + o;
+      *p = f2bf((float)*p + v);
+    } else if constexpr (EPI == EPI_SILU) {
+      reinterpret_cast<bf16*>(out)[o] = f2bf(silu(v) * u);
+    } else {
+      reinterpret_cast<float*>(out)[o] = v;
+    }
+  }
+}
 
 template <int MT, int WAVES, int EPI, bool NORM, int U>
 __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     const bf16x8* __restrict__ Wt, const bf16* __restrict__ X, int ldx, int M, int K,
-    int up_group_offset, void* __restrict__ out, int ldo, float eps) {
+    int up_group_offset, void* __restrict__ out, int ldo, float eps, EpiArgs ea) {
   constexpr int NB = (EPI == EPI_SILU) ? 2 : 1;
   const int S = K >> 5;
   const int lane = threadIdx.x & 63;
@@ -182,7 +265,6 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = mt * 16 + q * 4 + j;
-        if (m >= M) continue;
         float scale = 1.f;
         if constexpr (NORM) {
           float t = 0.f;
@@ -190,19 +272,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           for (int ww = 0; ww < WAVES; ++ww) t += red_ss[ww][mt][q * 4 + j];
           scale = rsqrtf(t / (float)K + eps);
         }
-        const float v = acc[0][mt][j] * scale;
-        const size_t o = (size_t)m * ldo + g * 16 + r;
-        if constexpr (EPI == EPI_STORE) {
-          reinterpret_cast<bf16*>(out)[o] = f2bf(v);
-        } else if constexpr (EPI == EPI_RESID) {
-          bf16* p = reinterpret_cast<bf16*>(out) + o;
-          *p = f2bf((float)*p + v);
-        } else if constexpr (EPI == EPI_SILU) {
-          const float u = acc[NB - 1][mt][j] * scale;
-          reinterpret_cast<bf16*>(out)[o] = f2bf(silu(v) * u);
-        } else {
-          reinterpret_cast<float*>(out)[o] = v;
-        }
+        epi_store<EPI>(m, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out, ldo,
+                       ea);
       }
     }
   } else {
@@ -217,20 +288,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           const float t = __shfl(ss[mt], q * 4 + j, 64);
           scale = rsqrtf(t / (float)K + eps);
         }
-        if (m >= M) continue;
-        const float v = acc[0][mt][j] * scale;
-        const size_t o = (size_t)m * ldo + g * 16 + r;
-        if constexpr (EPI == EPI_STORE) {
-          reinterpret_cast<bf16*>(out)[o] = f2bf(v);
-        } else if constexpr (EPI == EPI_RESID) {
-          bf16* p = reinterpret_cast<bf16*>(out) + o;
-          *p = f2bf((float)*p + v);
-        } else if constexpr (EPI == EPI_SILU) {
-          const float u = acc[NB - 1][mt][j] * scale;
-          reinterpret_cast<bf16*>(out)[o] = f2bf(silu(v) * u);
-        } else {
-          reinterpret_cast<float*>(out)[o] = v;
-        }
+        epi_store<EPI>(m, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out, ldo,
+                       ea);
       }
     }
   }
@@ -238,32 +297,32 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 
 template <int MT, int WAVES, int EPI, bool NORM>
 int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
-              void* out, int ldo, float eps, hipStream_t st) {
+              void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   constexpr int U = (MT == 1) ? 8 : 4;
   hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>), dim3(groups), dim3(WAVES * 64), 0,
-                     st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, up_off, out, ldo, eps);
+                     st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, up_off, out, ldo, eps, ea);
   return (int)hipGetLastError();
 }
 
 template <int MT, int EPI, bool NORM>
 int launch_m(int waves, const void* Wt, const void* X, int ldx, int M, int K, int groups,
-             int up_off, void* out, int ldo, float eps, hipStream_t st) {
+             int up_off, void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   switch (waves) {
-    case 1: return launch_mw<MT, 1, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
-    case 2: return launch_mw<MT, 2, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
-    case 4: return launch_mw<MT, 4, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
-    case 8: return launch_mw<MT, 8, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+    case 1: return launch_mw<MT, 1, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+    case 2: return launch_mw<MT, 2, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+    case 4: return launch_mw<MT, 4, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+    case 8: return launch_mw<MT, 8, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
   }
   return (int)hipErrorInvalidValue;
 }
 
 template <int EPI, bool NORM>
 int launch_e(int mt, int waves, const void* Wt, const void* X, int ldx, int M, int K, int groups,
-             int up_off, void* out, int ldo, float eps, hipStream_t st) {
+             int up_off, void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   switch (mt) {
-    case 1: return launch_m<1, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
-    case 2: return launch_m<2, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
-    case 4: return launch_m<4, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, st);
+    case 1: return launch_m<1, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+    case 2: return launch_m<2, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+    case 4: return launch_m<4, EPI, NORM>(waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -281,12 +340,13 @@ static int pick_waves(int groups, int K, int mt) {
   return waves;
 }
 
-// epi: 0 store bf16, 1 residual add (bf16, in place), 2 silu(gate)*up, 3 fp32 store.
+// epi: 0 store bf16, 1 residual add (bf16, in place), 2 silu(gate)*up, 3 fp32 store,
+//      4 qkv+rope+kv-cache (see p2p_skinny_gemm_qkv_rope), 5 greedy argmax keys (u64 [M]).
 // N: number of weight rows (for epi 2: 2*F, gate rows then up rows).
 // waves: 0 = heuristic.
-P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
-                            int norm, void* out, int ldo, float eps, int waves,
-                            hipStream_t stream) {
+static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
+                           int norm, void* out, int ldo, float eps, int waves, const EpiArgs& ea,
+                           hipStream_t stream) {
   if (M <= 0 || M > 64 || (K % 32) != 0 || (N % 16) != 0) return (int)hipErrorInvalidValue;
   const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   int groups = N / 16;
@@ -298,18 +358,62 @@ P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K
   }
   if (waves <= 0) waves = pick_waves(groups, K, mt);
   if (epi == EPI_SILU && mt == 4 && waves > 4) waves = 4;
-  if (epi == EPI_STORE) {
-    return norm ? launch_e<EPI_STORE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream)
-                : launch_e<EPI_STORE, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream);
-  } else if (epi == EPI_RESID) {
-    if (norm) return (int)hipErrorInvalidValue;
-    return launch_e<EPI_RESID, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream);
-  } else if (epi == EPI_SILU) {
-    if (!norm) return (int)hipErrorInvalidValue;
-    return launch_e<EPI_SILU, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream);
-  } else if (epi == EPI_F32) {
-    return norm ? launch_e<EPI_F32, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream)
-                : launch_e<EPI_F32, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, stream);
+  switch (epi) {
+    case EPI_STORE:
+      return norm ? launch_e<EPI_STORE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream)
+                  : launch_e<EPI_STORE, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+    case EPI_RESID:
+      if (norm) return (int)hipErrorInvalidValue;
+      return launch_e<EPI_RESID, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+    case EPI_SILU:
+      if (!norm) return (int)hipErrorInvalidValue;
+      return launch_e<EPI_SILU, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+    case EPI_F32:
+      return norm ? launch_e<EPI_F32, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream)
+                  : launch_e<EPI_F32, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+    case EPI_QKV_ROPE:
+      if (!norm) return (int)hipErrorInvalidValue;
+      return launch_e<EPI_QKV_ROPE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+    case EPI_ARGMAX:
+      if (!norm) return (int)hipErrorInvalidValue;
+      return launch_e<EPI_ARGMAX, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
   }
   return (int)hipErrorInvalidValue;
+}
+
+P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
+                            int norm, void* out, int ldo, float eps, int waves,
+                            hipStream_t stream) {
+  if (epi == EPI_QKV_ROPE) return (int)hipErrorInvalidValue;
+  EpiArgs ea = {};
+  return skinny_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, waves, ea, stream);
+}
+
+// Greedy LM head: keys[m] = atomicMax over columns of (ordered(logit) << 32 | ~(col+col_offset)).
+// keys must be zero before the call (p2p_argmax_finalize / p2p_advance reset them).
+P2P_API int p2p_skinny_gemm_argmax(const void* Wt, const void* X, int ldx, int M, int K, int N,
+                                   unsigned long long* keys, int col_offset, float eps, int waves,
+                                   hipStream_t stream) {
+  EpiArgs ea = {};
+  ea.col_offset = col_offset;
+  return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_ARGMAX, 1, keys, 0, eps, waves, ea, stream);
+}
+
+// Fused qkv projection (rows permuted per head, see header) + RoPE + KV-cache write.
+P2P_API int p2p_skinny_gemm_qkv_rope(const void* Wt, const void* X, int ldx, int M, int K,
+                                     int Hq, int Hkv, const int* pos, const int* slots,
+                                     const void* cos_sin, void* q_out, int ldq, void* k_cache,
+                                     void* v_cache, float eps, int waves, hipStream_t stream) {
+  EpiArgs ea = {};
+  ea.pos = pos;
+  ea.slots = slots;
+  ea.cs = (const float2*)cos_sin;
+  ea.q_out = (bf16*)q_out;
+  ea.ldq = ldq;
+  ea.kc = (bf16*)k_cache;
+  ea.vc = (bf16*)v_cache;
+  ea.Hq = Hq;
+  ea.Hkv = Hkv;
+  const int N = (Hq + 2 * Hkv) * HD;
+  return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_QKV_ROPE, 1, nullptr, 0, eps, waves, ea, stream);
 }

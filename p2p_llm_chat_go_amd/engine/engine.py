@@ -141,15 +141,19 @@ class Engine:
             dev_t = host.to(dev, non_blocking=True)
             seq_d, pos_d, ids_d, slots_d, ctx_d = dev_t[0], dev_t[1], dev_t[2], dev_t[3], dev_t[4]
             out_rows = torch.tensor(outs or [0], dtype=torch.int32).to(dev, non_blocking=True)
-            logits = self.model.forward(ws, ids_d, pos_d, slots_d, bt_d, seq_d, ctx_d, R,
-                                        max_ctx, out_rows=out_rows, n_out=len(outs))
+            greedy = all_logits is None
+            res = self.model.forward(ws, ids_d, pos_d, slots_d, bt_d, seq_d, ctx_d, R,
+                                     max_ctx, out_rows=out_rows, n_out=len(outs), greedy=greedy)
             if not outs:
                 continue
-            toks = self.model.sample_greedy(ws, logits)
+            if greedy:
+                toks = self.model.finalize_greedy(ws, len(outs))
+            else:
+                toks = self.model.sample_greedy(ws, res)
             sel = torch.tensor(out_seq, dtype=torch.long).to(dev, non_blocking=True)
             first.index_copy_(0, sel, toks)
             if all_logits is not None:
-                all_logits.index_copy_(0, sel, logits)
+                all_logits.index_copy_(0, sel, res)
         return (first, all_logits) if return_logits else first
 
     # ------------------------------------------------------------- generate

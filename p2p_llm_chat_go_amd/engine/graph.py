@@ -46,6 +46,7 @@ class DecodeState:
         self.slots.zero_()
         self.bt.zero_()
         self.step.zero_()
+        self.ws.keys.zero_()
 
     def load(self, ids, pos, block_tables):
         """ids/pos: int lists (n <= B); block_tables: list of page lists."""
@@ -68,10 +69,13 @@ class DecodeState:
 
     def body(self):
         m = self.model
-        logits = m.forward(self.ws, self.ids, self.pos, self.slots, self.bt, self.row_bt, self.ctx,
-                           self.B, self.max_ctx)
-        m.sample_greedy(self.ws, logits, out=self.ids)
-        ops.advance(self.ids, self.pos, self.ctx, self.slots, self.bt, self.hist, self.step)
+        keys = m.forward(self.ws, self.ids, self.pos, self.slots, self.bt, self.row_bt, self.ctx,
+                         self.B, self.max_ctx, greedy=True)
+        if m.tp > 1:
+            m.comm.allreduce_max_u64_(keys[:self.B])
+        # keys -> ids (+ reset) folded into the state advance: no extra launch
+        ops.advance(self.ids, self.pos, self.ctx, self.slots, self.bt, self.hist, self.step,
+                    keys=keys[:self.B])
 
 
 class DecodeGraph:

@@ -4,15 +4,16 @@ One ``forward`` serves prefill and decode: its input is a flat list of *query
 rows* (tokens) with per-row position, KV slot, sequence (block-table row) and
 context length.  Per layer (TP=1, dense):
 
-    qkv   = rstd(h) * h @ Wqkv'          skinny_gemm  NORM | STORE
-    q,k,v = rope(qkv); k,v -> KV pages   rope_cache
+    q,k,v = rope(rstd(h) * h @ Wqkv');   skinny_gemm  NORM | QKV_ROPE
+            k,v -> KV pages               (RoPE + cache write in the epilogue)
     a     = paged_attention(q, pages)    paged_attention (GQA-packed)
     h    += a @ Wo                       skinny_gemm  RESID
     act   = silu(g) * u, [g|u] = rstd(h) * h @ Wgu'   skinny_gemm NORM | SILU
     h    += act @ Wdown                  skinny_gemm  RESID
 
-i.e. 6 launches per layer, every RMSNorm / residual add / SwiGLU fused into
-a GEMM.  With TP>1 the row-parallel outputs (o_proj, down) go to a scratch
+i.e. 5 launches per layer, every RMSNorm / RoPE / KV write / residual add /
+SwiGLU fused into a GEMM; the LM head fuses greedy argmax (64-bit atomicMax
+keys) so no logits round trip on the greedy path.  With TP>1 the row-parallel outputs (o_proj, down) go to a scratch
 buffer and ``comm.allreduce_add_(h, partial)`` sums them into the residual.
 MoE layers (Mixtral) route through ``models.moe``.
 
@@ -48,6 +49,7 @@ class Workspace:
         self.last = torch.zeros(mo, cfg.hidden, device=dev, dtype=bf)
         self.logits = torch.zeros(mo, cfg.vocab // tp_size, device=dev, dtype=torch.float32)
         self.ids_out = torch.zeros(mo, device=dev, dtype=torch.int32)
+        self.keys = torch.zeros(mo, device=dev, dtype=torch.int64)
         self.attn_ws = ops.attn_workspace(max_rows, nq, max_ctx, dev)
         self.moe = None  # lazily sized by models.moe
 
@@ -90,20 +92,22 @@ class LlamaModel:
         self._row_parallel(lw.down, act, h, ws, R)
 
     def forward(self, ws: Workspace, ids, pos, slots, block_tables, row_bt, ctx_lens, R: int,
-                max_ctx: int, out_rows=None, n_out: int | None = None):
-        """Run all layers on R query rows; return fp32 logits of the selected rows.
+                max_ctx: int, out_rows=None, n_out: int | None = None, greedy: bool = False):
+        """Run all layers on R query rows.
 
         out_rows: int32 [n_out] indices of rows whose logits are needed (prefill:
         the last token of each sequence); None = all R rows (decode).
+        Returns fp32 logits of the selected rows, or with greedy=True the int64
+        argmax keys (ws.keys, see ops.lm_head_argmax).
         """
         cfg = self.cfg
         h = ws.h[:R]
         ops.gather_rows(self.w.embed, ids[:R], out=h)
-        q, qkv, attn = ws.q[:R], ws.qkv[:R], ws.attn[:R]
+        q, attn = ws.q[:R], ws.attn[:R]
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)
-            ops.skinny_gemm(lw.qkv, h, ops.EPI_STORE, norm=True, out=qkv, eps=cfg.eps)
-            ops.rope_cache(qkv, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc, vc)
+            ops.qkv_rope_gemm(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc,
+                              vc, eps=cfg.eps)
             ops.paged_attention(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R], self.nq,
                                 self.nkv, max_ctx, out=attn, workspace=ws.attn_ws)
             self._row_parallel(lw.o, attn, h, ws, R)
@@ -116,9 +120,19 @@ class LlamaModel:
         else:
             n = n_out if n_out is not None else out_rows.shape[0]
             x = ops.gather_rows(h, out_rows[:n], out=ws.last[:n])
+        if greedy:
+            off = self.w.tp_rank * (cfg.vocab // self.tp)
+            return ops.lm_head_argmax(self.w.lm_head, x, ws.keys, col_offset=off, eps=cfg.eps)
         logits = ws.logits[:n]
         ops.skinny_gemm(self.w.lm_head, x, ops.EPI_F32, norm=True, out=logits, eps=cfg.eps)
         return logits
+
+    def finalize_greedy(self, ws: Workspace, n: int, out=None):
+        """keys -> token ids (TP: all-reduce MAX of the keys across vocab shards first)."""
+        out = ws.ids_out[:n] if out is None else out
+        if self.tp > 1:
+            self.comm.allreduce_max_u64_(ws.keys[:n])
+        return ops.argmax_finalize(ws.keys[:n], out)
 
     def sample_greedy(self, ws: Workspace, logits, out=None):
         n = logits.shape[0]

@@ -10,6 +10,8 @@ Load-time transforms (all one-off, none on the hot path):
   * Tensor-parallel sharding (Megatron): qkv / gate_up / lm_head split by
     output rows (heads, ffn columns, vocab), o_proj / down split by input
     columns; the row-parallel outputs are summed by ``parallel.comm``.
+  * qkv rows are permuted per head (``ops.rope_row_perm``) so RoPE and the KV
+    cache write run in the projection's epilogue.
   * Every projection is re-laid out fragment-major (``ops.tile_weight``).
 
 Random init (BASELINE: no checkpoints on the box) draws N(0, std) directly in
@@ -89,6 +91,8 @@ class EngineWeights:
             k = get(p + "self_attn.k_proj.weight")[tp_rank * ks:(tp_rank + 1) * ks]
             v = get(p + "self_attn.v_proj.weight")[tp_rank * ks:(tp_rank + 1) * ks]
             qkv = ops.fold_norm(torch.cat([q, k, v], 0), g_in)
+            # fused qkv+RoPE epilogue row order (ops.rope_row_perm)
+            qkv = qkv[ops.rope_row_perm(qkv.shape[0] // D, D).to(qkv.device)]
             o = get(p + "self_attn.o_proj.weight")[:, tp_rank * qs:(tp_rank + 1) * qs]
             lw = LayerWeights(qkv=tile(qkv), o=tile(o))
             if cfg.is_moe:

@@ -40,8 +40,14 @@ _SIGS = {
     "p2p_rope_cache": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "p2p_argmax": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
-    "p2p_advance": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
-                    c_void_p, c_int, c_void_p],
+    "p2p_advance": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                    c_int, c_void_p, c_int, c_void_p],
+    "p2p_argmax_finalize": [c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_skinny_gemm_argmax": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                               c_float, c_int, c_void_p],
+    "p2p_skinny_gemm_qkv_rope": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float,
+                                 c_int, c_void_p],
 }
 
 

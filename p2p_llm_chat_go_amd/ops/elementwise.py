@@ -34,10 +34,17 @@ def argmax(logits: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tenso
     return out
 
 
-def advance(ids, pos, ctx, slots, block_tables, hist, step):
-    """Decode-state advance (all int32, device-resident): see elementwise.hip."""
+def advance(ids, pos, ctx, slots, block_tables, hist, step, keys=None):
+    """Decode-state advance (all int32, device-resident): see elementwise.hip.
+
+    keys: optional int64 greedy keys from ops.lm_head_argmax -> converted into ids
+    (and reset) before the advance.
+    """
     B = ids.shape[0]
     if ids.device.type != "cuda":
+        if keys is not None:
+            ids.copy_((0xFFFFFFFF - (keys[:B] & 0xFFFFFFFF)).to(torch.int32))
+            keys[:B] = 0
         st = int(step[0])
         if hist is not None:
             hist[:, st] = ids
@@ -48,7 +55,8 @@ def advance(ids, pos, ctx, slots, block_tables, hist, step):
         step += 1
         return
     L = _lib.lib()
-    _lib.check(L.p2p_advance(ids.data_ptr(), pos.data_ptr(), ctx.data_ptr(), slots.data_ptr(),
+    _lib.check(L.p2p_advance(ids.data_ptr(), _lib.ptr(keys), pos.data_ptr(), ctx.data_ptr(),
+                             slots.data_ptr(),
                              block_tables.data_ptr(), block_tables.stride(0),
                              _lib.ptr(hist), 0 if hist is None else hist.stride(0),
                              step.data_ptr(), B, _lib.stream_ptr(ids.device)), "advance")

@@ -91,3 +91,82 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
                                      int(norm), os_.data_ptr(), out.stride(0), float(eps), waves, s),
                    "skinny_gemm")
     return out
+
+
+# ------------------------------------------------------------ fused epilogues
+def rope_row_perm(n_heads_total: int, head_dim: int = 128) -> torch.Tensor:
+    """Row order of the fused qkv+RoPE projection (skinny_gemm.hip, EPI_QKV_ROPE).
+
+    Within every head, 16-row group k holds dims 8k..8k+7 and 64+8k..64+8k+7 so the
+    rotate_half partner of a lane is lane ^ 8.  Returns perm with new_row = old[perm].
+    """
+    half = head_dim // 2
+    one = []
+    for k in range(head_dim // 16):
+        one += [8 * k + r for r in range(8)] + [half + 8 * k + r for r in range(8)]
+    one = torch.tensor(one, dtype=torch.long)
+    return (torch.arange(n_heads_total)[:, None] * head_dim + one[None, :]).reshape(-1)
+
+
+def qkv_rope_gemm(wt, x, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_cache,
+                  eps=1e-5, waves=0):
+    """q_out, k/v pages <- rope(rstd(x) * x @ Wqkv^T) with Wqkv rows in rope_row_perm order."""
+    from .attention import rope_cache_ref
+
+    M = x.shape[0]
+    N, K = tiled_shape(wt)
+    assert N == (n_heads + 2 * n_kv) * 128
+    if x.device.type != "cuda":
+        perm = rope_row_perm(n_heads + 2 * n_kv)
+        qkv_p = torch.empty(M, N, dtype=torch.bfloat16)
+        _ref(wt, x, EPI_STORE, True, qkv_p, eps)
+        qkv = torch.empty_like(qkv_p)
+        qkv[:, perm] = qkv_p
+        return rope_cache_ref(qkv, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_cache)
+    L = _lib.lib()
+    s = _lib.stream_ptr(x.device)
+    for m0 in range(0, M, SKINNY_MAX_M):
+        mc = min(SKINNY_MAX_M, M - m0)
+        _lib.check(L.p2p_skinny_gemm_qkv_rope(
+            wt.data_ptr(), x[m0:].data_ptr(), x.stride(0), mc, K, n_heads, n_kv,
+            pos[m0:].data_ptr(), slots[m0:].data_ptr(), cos_sin.data_ptr(), q_out[m0:].data_ptr(),
+            q_out.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), float(eps), waves, s),
+            "skinny_gemm_qkv_rope")
+    return q_out
+
+
+def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: int = 0):
+    """Greedy LM head: keys[m] = max over vocab of (ordered logit << 32 | ~token).
+
+    keys (int64 [M], zeroed) are turned into token ids by argmax_finalize / advance.
+    """
+    M = x.shape[0]
+    N, K = tiled_shape(wt)
+    if x.device.type != "cuda":
+        logits = _ref(wt, x, EPI_F32, True, torch.empty(M, N), eps)
+        v, i = logits.max(-1)
+        u = v.view(torch.int32).long() & 0xFFFFFFFF
+        u = torch.where(u >= 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+        k = (u << 32) | (0xFFFFFFFF - (i + col_offset))
+        # unsigned 64-bit max on int64 storage: compare with the sign bit flipped
+        sign = torch.tensor(-(2 ** 63), dtype=torch.int64)
+        cur = keys[:M]
+        keys[:M] = torch.where((k ^ sign) > (cur ^ sign), k, cur)
+        return keys
+    L = _lib.lib()
+    _lib.check(L.p2p_skinny_gemm_argmax(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N,
+                                        keys.data_ptr(), int(col_offset), float(eps), waves,
+                                        _lib.stream_ptr(x.device)), "skinny_gemm_argmax")
+    return keys
+
+
+def argmax_finalize(keys, ids):
+    M = ids.shape[0]
+    if keys.device.type != "cuda":
+        ids.copy_((0xFFFFFFFF - (keys[:M] & 0xFFFFFFFF)).to(torch.int32))
+        keys[:M] = 0
+        return ids
+    L = _lib.lib()
+    _lib.check(L.p2p_argmax_finalize(keys.data_ptr(), ids.data_ptr(), M,
+                                     _lib.stream_ptr(keys.device)), "argmax_finalize")
+    return ids

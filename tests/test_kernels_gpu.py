@@ -182,3 +182,61 @@ def test_gather_argmax_advance():
     for a, b in zip(d, (ids, pos, ctx, slots, bt, hist, step)):
         assert torch.equal(a.cpu(), b)
     assert slots.tolist() == [5 * 64 + 0, 7 * 64 + 1, 3 * 64 + 3]
+
+
+# ------------------------------------------------------------ fused epilogues
+@pytest.mark.parametrize("M", [1, 5, 40])
+def test_qkv_rope_gemm(M):
+    from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
+
+    torch.manual_seed(M)
+    Hq, Hkv, K = 4, 2, 512
+    N = (Hq + 2 * Hkv) * 128
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    Wp = W[ops.rope_row_perm(Hq + 2 * Hkv)]
+    Wt = ops.tile_weight(Wp)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    cs = rope_table(LLAMA31_8B, max_pos=2048)
+    pos = torch.randint(0, 2000, (M,), dtype=torch.int32)
+    slots = torch.randperm(4 * 64)[:M].to(torch.int32)
+    if M > 2:
+        slots[1] = -1
+    # oracle: natural-order qkv then rope_cache_ref
+    qkv = (x.float() @ W.float().t()) * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    q_ref = torch.zeros(M, Hq * 128, dtype=torch.bfloat16)
+    kr = torch.zeros(4, Hkv, 64, 128, dtype=torch.bfloat16)
+    vr = torch.zeros_like(kr)
+    A.rope_cache_ref(qkv.to(torch.bfloat16), pos, slots, cs, Hq, Hkv, q_ref, kr, vr)
+    qd = torch.zeros(M, Hq * 128, dtype=torch.bfloat16, device=DEV)
+    kd, vd = torch.zeros_like(kr).to(DEV), torch.zeros_like(vr).to(DEV)
+    ops.qkv_rope_gemm(Wt.to(DEV), x.to(DEV), pos.to(DEV), slots.to(DEV), cs.to(DEV), Hq, Hkv, qd,
+                      kd, vd)
+    torch.cuda.synchronize()
+    assert _rel(qd.cpu(), q_ref) < 1e-2
+    assert _rel(kd.cpu(), kr) < 1e-2
+    assert _rel(vd.cpu(), vr) < 1e-2
+    # CPU path of the same fused op agrees too
+    qc = torch.zeros_like(q_ref)
+    kc, vc = torch.zeros_like(kr), torch.zeros_like(vr)
+    ops.qkv_rope_gemm(Wt, x, pos, slots, cs, Hq, Hkv, qc, kc, vc)
+    assert _rel(qc, q_ref) < 1e-2 and _rel(kc, kr) < 1e-2
+
+
+@pytest.mark.parametrize("M,offset", [(1, 0), (7, 1000)])
+def test_lm_head_argmax(M, offset):
+    torch.manual_seed(M)
+    V, K = 4096, 512
+    W = (torch.randn(V, K) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    ref = ((x.float() @ W.float().t())).argmax(-1) + offset
+    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
+    ops.lm_head_argmax(ops.tile_weight(W).to(DEV), x.to(DEV), keys, col_offset=offset)
+    ids = torch.zeros(M, dtype=torch.int32, device=DEV)
+    ops.argmax_finalize(keys, ids)
+    assert ids.cpu().long().tolist() == ref.tolist()
+    assert int(keys.abs().sum()) == 0  # finalize resets the keys
+    kc = torch.zeros(M, dtype=torch.int64)
+    ops.lm_head_argmax(ops.tile_weight(W), x, kc, col_offset=offset)
+    ic = torch.zeros(M, dtype=torch.int32)
+    ops.argmax_finalize(kc, ic)
+    assert ic.long().tolist() == ref.tolist()
