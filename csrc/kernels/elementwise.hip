@@ -8,6 +8,20 @@ namespace {
 
 constexpr int PAGE = 64;
 constexpr int HD = 128;
+constexpr int KEY_SHARDS = 32;
+
+// max over the KEY_SHARDS argmax keys of row m, resetting them; -> token id
+__device__ __forceinline__ int reduce_keys(unsigned long long* keys, int m) {
+  unsigned long long best = 0;
+  unsigned long long* k = keys + (size_t)m * KEY_SHARDS;
+#pragma unroll
+  for (int i = 0; i < KEY_SHARDS; ++i) {
+    const unsigned long long v = k[i];
+    best = v > best ? v : best;
+    k[i] = 0ull;
+  }
+  return (int)(0xFFFFFFFFu - (unsigned)(best & 0xFFFFFFFFull));
+}
 
 // out[t, :] = src[idx[t], :]  (H bf16 per row, 16-B vectors)
 __global__ __launch_bounds__(256) void gather_rows_kernel(const bf16* __restrict__ src,
@@ -108,8 +122,7 @@ __global__ void advance_kernel(int* __restrict__ ids, unsigned long long* __rest
   const int st = *step;
   if (b < B) {
     if (keys) {  // greedy keys from the fused LM-head argmax -> token ids; reset for next step
-      ids[b] = (int)(0xFFFFFFFFu - (unsigned)(keys[b] & 0xFFFFFFFFull));
-      keys[b] = 0ull;
+      ids[b] = reduce_keys(keys, b);
     }
     if (hist) hist[(size_t)b * hist_stride + st] = ids[b];
     const int p = pos[b] + 1;
@@ -124,10 +137,7 @@ __global__ void advance_kernel(int* __restrict__ ids, unsigned long long* __rest
 __global__ void argmax_finalize_kernel(unsigned long long* __restrict__ keys, int* __restrict__ ids,
                                        int M) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m < M) {
-    ids[m] = (int)(0xFFFFFFFFu - (unsigned)(keys[m] & 0xFFFFFFFFull));
-    keys[m] = 0ull;
-  }
+  if (m < M) ids[m] = reduce_keys(keys, m);
 }
 
 }  // namespace

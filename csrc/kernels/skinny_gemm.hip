@@ -41,6 +41,7 @@ enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_F32 = 3, EPI_QKV_RO
 
 constexpr int PAGE = 64;
 constexpr int HD = 128;
+constexpr int KEY_SHARDS = 32;  // keys buffer: [M][KEY_SHARDS] u64 (see EPI_ARGMAX)
 
 struct EpiArgs {
   // EPI_QKV_ROPE
@@ -96,7 +97,11 @@ __device__ __forceinline__ void epi_store(int m, bool valid, int g, int r, float
       const unsigned long long ok = __shfl_xor(key, o, 64);
       key = ok > key ? ok : key;
     }
-    if (valid && r == 0) atomicMax(reinterpret_cast<unsigned long long*>(out) + m, key);
+    // sharded by block id: one 64-bit atomic per (row, shard) keeps contention at
+    // ~groups/KEY_SHARDS arrivals per word instead of all groups on one word.
+    if (valid && r == 0)
+      atomicMax(reinterpret_cast<unsigned long long*>(out) + (size_t)m * KEY_SHARDS + (g % KEY_SHARDS),
+                key);
   } else {
     if (!valid) return;
     const size_t o = (size_t)m * ldo + g * 16 + r;
@@ -389,8 +394,9 @@ P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K
   return skinny_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, waves, ea, stream);
 }
 
-// Greedy LM head: keys[m] = atomicMax over columns of (ordered(logit) << 32 | ~(col+col_offset)).
-// keys must be zero before the call (p2p_argmax_finalize / p2p_advance reset them).
+// Greedy LM head: keys[m][shard] = atomicMax over columns of (ordered(logit) << 32 | ~(col+off)).
+// keys ([M][32] u64) must be zero before the call (p2p_argmax_finalize / p2p_advance reduce
+// the shards and reset them).
 P2P_API int p2p_skinny_gemm_argmax(const void* Wt, const void* X, int ldx, int M, int K, int N,
                                    unsigned long long* keys, int col_offset, float eps, int waves,
                                    hipStream_t stream) {

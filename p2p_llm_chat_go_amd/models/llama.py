@@ -49,7 +49,7 @@ class Workspace:
         self.last = torch.zeros(mo, cfg.hidden, device=dev, dtype=bf)
         self.logits = torch.zeros(mo, cfg.vocab // tp_size, device=dev, dtype=torch.float32)
         self.ids_out = torch.zeros(mo, device=dev, dtype=torch.int32)
-        self.keys = torch.zeros(mo, device=dev, dtype=torch.int64)
+        self.keys = ops.new_argmax_keys(mo, dev)
         self.attn_ws = ops.attn_workspace(max_rows, nq, max_ctx, dev)
         self.moe = None  # lazily sized by models.moe
 

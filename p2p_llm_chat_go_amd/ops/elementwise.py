@@ -43,8 +43,9 @@ def advance(ids, pos, ctx, slots, block_tables, hist, step, keys=None):
     B = ids.shape[0]
     if ids.device.type != "cuda":
         if keys is not None:
-            ids.copy_((0xFFFFFFFF - (keys[:B] & 0xFFFFFFFF)).to(torch.int32))
-            keys[:B] = 0
+            from .gemm import reduce_keys_ref
+
+            ids.copy_(reduce_keys_ref(keys, B))
         st = int(step[0])
         if hist is not None:
             hist[:, st] = ids

@@ -135,10 +135,19 @@ def qkv_rope_gemm(wt, x, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_c
     return q_out
 
 
-def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: int = 0):
-    """Greedy LM head: keys[m] = max over vocab of (ordered logit << 32 | ~token).
+KEY_SHARDS = 32
 
-    keys (int64 [M], zeroed) are turned into token ids by argmax_finalize / advance.
+
+def new_argmax_keys(rows: int, device) -> torch.Tensor:
+    return torch.zeros(rows, KEY_SHARDS, dtype=torch.int64, device=device)
+
+
+def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: int = 0):
+    """Greedy LM head: keys[m, shard] = max of (ordered logit << 32 | ~token) over the
+    vocab columns of that shard's blocks.
+
+    keys (int64 [M, KEY_SHARDS], zeroed) are reduced into token ids (and reset) by
+    argmax_finalize / advance.
     """
     M = x.shape[0]
     N, K = tiled_shape(wt)
@@ -150,8 +159,8 @@ def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: i
         k = (u << 32) | (0xFFFFFFFF - (i + col_offset))
         # unsigned 64-bit max on int64 storage: compare with the sign bit flipped
         sign = torch.tensor(-(2 ** 63), dtype=torch.int64)
-        cur = keys[:M]
-        keys[:M] = torch.where((k ^ sign) > (cur ^ sign), k, cur)
+        cur = keys[:M, 0]
+        keys[:M, 0] = torch.where((k ^ sign) > (cur ^ sign), k, cur)
         return keys
     L = _lib.lib()
     _lib.check(L.p2p_skinny_gemm_argmax(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N,
@@ -160,11 +169,18 @@ def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: i
     return keys
 
 
+def reduce_keys_ref(keys, M):
+    sign = torch.tensor(-(2 ** 63), dtype=torch.int64)
+    k = keys[:M]
+    best = ((k ^ sign).max(dim=1).values) ^ sign
+    keys[:M] = 0
+    return (0xFFFFFFFF - (best & 0xFFFFFFFF)).to(torch.int32)
+
+
 def argmax_finalize(keys, ids):
     M = ids.shape[0]
     if keys.device.type != "cuda":
-        ids.copy_((0xFFFFFFFF - (keys[:M] & 0xFFFFFFFF)).to(torch.int32))
-        keys[:M] = 0
+        ids.copy_(reduce_keys_ref(keys, M))
         return ids
     L = _lib.lib()
     _lib.check(L.p2p_argmax_finalize(keys.data_ptr(), ids.data_ptr(), M,

@@ -229,13 +229,13 @@ def test_lm_head_argmax(M, offset):
     W = (torch.randn(V, K) * 0.05).to(torch.bfloat16)
     x = torch.randn(M, K).to(torch.bfloat16)
     ref = ((x.float() @ W.float().t())).argmax(-1) + offset
-    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
+    keys = ops.new_argmax_keys(M, DEV)
     ops.lm_head_argmax(ops.tile_weight(W).to(DEV), x.to(DEV), keys, col_offset=offset)
     ids = torch.zeros(M, dtype=torch.int32, device=DEV)
     ops.argmax_finalize(keys, ids)
     assert ids.cpu().long().tolist() == ref.tolist()
     assert int(keys.abs().sum()) == 0  # finalize resets the keys
-    kc = torch.zeros(M, dtype=torch.int64)
+    kc = ops.new_argmax_keys(M, "cpu")
     ops.lm_head_argmax(ops.tile_weight(W), x, kc, col_offset=offset)
     ic = torch.zeros(M, dtype=torch.int32)
     ops.argmax_finalize(kc, ic)
