@@ -1,0 +1,257 @@
+// pybind11 module `_native`: the C++ chat plane (node, directory, relay) for
+// in-process use with the GPU engine, plus codec entry points for unit tests.
+// The GIL is released while C++ blocks; the engine hook re-acquires it.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <sys/socket.h>
+
+#include <thread>
+
+#include "net/chat.h"
+#include "net/relay.h"
+#include "runtime/scheduler.h"
+
+namespace py = pybind11;
+using namespace p2p;
+
+void bind_runtime(py::module_& m);  // runtime_bind.cc
+
+namespace {
+
+py::bytes B(const Bytes& b) { return py::bytes((const char*)b.data(), b.size()); }
+Bytes U(const py::bytes& b) {
+  std::string s = b;
+  return Bytes(s.begin(), s.end());
+}
+
+NodeConfig cfg_from_dict(const py::dict& d) {
+  NodeConfig c = NodeConfig::from_env();
+  auto S = [&](const char* k, std::string* v) {
+    if (d.contains(k)) *v = py::str(d[k]);
+  };
+  S("username", &c.username);
+  S("http_addr", &c.http_addr);
+  S("directory_url", &c.directory_url);
+  S("bootstrap", &c.bootstrap);
+  S("relays", &c.relays);
+  S("key_type", &c.key_type);
+  S("identity_file", &c.identity_file);
+  S("inbox_file", &c.inbox_file);
+  S("engine_url", &c.engine_url);
+  S("llm_model", &c.llm_model);
+  S("ui_file", &c.ui_file);
+  if (d.contains("register_interval")) c.register_interval_s = py::int_(d["register_interval"]);
+  if (d.contains("strict_sender")) c.strict_sender = py::bool_(d["strict_sender"]);
+  if (d.contains("access_log")) c.access_log = py::bool_(d["access_log"]);
+  if (d.contains("listen")) c.listen = d["listen"].cast<std::vector<std::string>>();
+  return c;
+}
+
+// Noise + yamux self-test over a socketpair: returns the echoed payload.
+std::string secure_echo(const std::string& key_type, const std::string& payload) {
+  int sv[2];
+  if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) throw NetError("socketpair");
+  KeyType kt = key_type == "rsa" ? KeyType::RSA : KeyType::Ed25519;
+  PrivateKey ka = PrivateKey::generate(kt), kb = PrivateKey::generate(kt);
+  PeerId idb = PeerId::from_public_key(kb.public_key());
+  auto ca = std::make_shared<TcpConn>(sv[0]);
+  auto cb = std::make_shared<TcpConn>(sv[1]);
+  Bytes data(payload.begin(), payload.end());
+  std::string err;
+  std::thread srv([&] {
+    try {
+      auto b1 = std::make_shared<BufConn>(cb);
+      ms_handle(*b1, {"/noise"});
+      auto sec = NoiseConn::handshake(b1, kb, false);
+      auto b2 = std::make_shared<BufConn>(sec);
+      ms_handle(*b2, {"/yamux/1.0.0"});
+      auto sess = std::make_shared<YamuxSession>(b2, false);
+      std::mutex m;
+      std::condition_variable cv;
+      bool done = false;
+      sess->start([&](StreamPtr s) {
+        auto io = std::make_shared<BufConn>(s);
+        ms_handle(*io, {"/echo/1.0.0"});
+        Bytes all = io->read_all(64 << 20);
+        io->write_all(all);
+        s->close();
+        std::lock_guard<std::mutex> lk(m);
+        done = true;
+        cv.notify_all();
+      });
+      std::unique_lock<std::mutex> lk(m);
+      cv.wait_for(lk, std::chrono::seconds(20), [&] { return done; });
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      sess->close();
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+  });
+  Bytes got;
+  try {
+    auto b1 = std::make_shared<BufConn>(ca);
+    ms_select(*b1, "/noise");
+    auto sec = NoiseConn::handshake(b1, ka, true, idb);
+    auto b2 = std::make_shared<BufConn>(sec);
+    ms_select(*b2, "/yamux/1.0.0");
+    auto sess = std::make_shared<YamuxSession>(b2, true);
+    sess->start(nullptr);
+    StreamPtr s = sess->open_stream();
+    auto io = std::make_shared<BufConn>(s);
+    ms_select(*io, "/echo/1.0.0");
+    io->write_all(data);
+    s->close_write();
+    s->set_read_timeout(20000);
+    got = io->read_all(64 << 20);
+    s->close();
+    sess->close();
+  } catch (const std::exception& e) {
+    srv.join();
+    throw NetError(std::string("client: ") + e.what() + (err.empty() ? "" : " / server: " + err));
+  }
+  srv.join();
+  if (!err.empty()) throw NetError("server: " + err);
+  return std::string(got.begin(), got.end());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "native chat plane (libp2p subset, HTTP, directory, relay) + engine runtime";
+  py::register_exception<NetError>(m, "NetError");
+  py::register_exception<JsonError>(m, "JsonError");
+
+  // ---- codecs ----
+  m.def("uvarint", [](uint64_t v) { return B(uvarint(v)); });
+  m.def("read_uvarint", [](const py::bytes& b) {
+    Bytes x = U(b);
+    size_t pos = 0;
+    uint64_t v = get_uvarint(x, &pos);
+    return py::make_tuple(v, pos);
+  });
+  m.def("base58_encode", [](const py::bytes& b) { return base58_encode(U(b)); });
+  m.def("base58_decode", [](const std::string& s) { return B(base58_decode(s)); });
+  m.def("multiaddr_to_bytes", [](const std::string& s) { return B(Multiaddr::parse(s).bytes()); });
+  m.def("multiaddr_from_bytes", [](const py::bytes& b) { return Multiaddr::from_bytes(U(b)).str(); });
+  m.def("multiaddr_normalize", [](const std::string& s) { return Multiaddr::parse(s).str(); });
+  m.def("keygen", [](const std::string& t) {
+    PrivateKey k = PrivateKey::generate(t == "rsa" ? KeyType::RSA : KeyType::Ed25519);
+    PublicKey p = k.public_key();
+    return py::make_tuple(B(k.marshal()), B(p.marshal()), PeerId::from_public_key(p).to_base58());
+  });
+  m.def("peer_id_from_public_key", [](const py::bytes& pb) {
+    return PeerId::from_public_key(PublicKey::unmarshal(U(pb))).to_base58();
+  });
+  m.def("peer_id_decode", [](const std::string& s) { return B(PeerId::decode(s).bytes()); });
+  m.def("sign", [](const py::bytes& priv, const py::bytes& msg) {
+    return B(PrivateKey::unmarshal(U(priv)).sign(U(msg)));
+  });
+  m.def("verify", [](const py::bytes& pub, const py::bytes& msg, const py::bytes& sig) {
+    return PublicKey::unmarshal(U(pub)).verify(U(msg), U(sig));
+  });
+  m.def("json_roundtrip", [](const std::string& s, bool sorted) {
+    Json j = Json::parse(s);
+    return sorted ? j.dump_sorted() : j.dump();
+  }, py::arg("text"), py::arg("sorted") = false);
+  m.def("parse_rfc3339", &parse_rfc3339);
+  m.def("rfc3339_now", &rfc3339_now_local);
+  m.def("uuid4", &uuid4);
+  m.def("secure_echo", [](const std::string& kt, const py::bytes& payload) {
+    std::string in = payload, out;
+    {
+      py::gil_scoped_release rel;
+      out = secure_echo(kt, in);
+    }
+    return py::bytes(out);
+  });
+  m.def("chat_message_from_json", [](const std::string& s) {
+    return ChatMessage::from_json(Json::parse(s)).to_json().dump();
+  });
+  m.def("set_log_quiet", &set_log_quiet);
+  m.def("http_request", [](const std::string& method, const std::string& url,
+                           const std::string& body, const std::string& ctype, int timeout_ms) {
+    HttpResult r;
+    {
+      py::gil_scoped_release rel;
+      r = http_request(method, url, body, ctype, timeout_ms);
+    }
+    return py::make_tuple(r.status, r.body);
+  }, py::arg("method"), py::arg("url"), py::arg("body") = "", py::arg("content_type") = "",
+        py::arg("timeout_ms") = 5000);
+
+  // ---- node ----
+  py::class_<Node>(m, "Node")
+      .def(py::init([](py::dict d) { return new Node(cfg_from_dict(d)); }), py::arg("config") = py::dict())
+      .def("start", &Node::start, py::call_guard<py::gil_scoped_release>())
+      .def("wait", &Node::wait, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &Node::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("http_port", &Node::http_port)
+      .def_property_readonly("peer_id", &Node::peer_id)
+      .def_property_readonly("addrs", &Node::addrs)
+      .def("send", [](Node& n, const std::string& to, const std::string& content) {
+        std::pair<int, Json> r;
+        {
+          py::gil_scoped_release rel;
+          r = n.send(to, content);
+        }
+        return py::make_tuple(r.first, r.second.dump_sorted());
+      })
+      .def("inbox", [](Node& n, const std::string& after) {
+        Json arr = Json::array();
+        for (auto& x : n.inbox().drain(after)) arr.push(x.to_json());
+        return arr.dump();
+      }, py::arg("after") = "")
+      .def("set_generate_hook", [](Node& n, py::function fn) {
+        auto holder = std::make_shared<py::function>(std::move(fn));
+        n.set_generate_hook([holder](const Json& req) -> Json {
+          std::string out;
+          {
+            py::gil_scoped_acquire g;
+            out = py::str((*holder)(req.dump()));
+          }
+          return Json::parse(out);
+        });
+      })
+      .def("metrics", [](Node& n) { return n.metrics_json().dump(); });
+
+  // ---- directory ----
+  py::class_<HttpServer>(m, "_HttpServer");
+  struct Dir {
+    DirectoryService svc;
+    HttpServer srv{"GIN"};
+    explicit Dir(int ttl) : svc(ttl) { svc.install(srv); }
+  };
+  py::class_<Dir>(m, "Directory")
+      .def(py::init<int>(), py::arg("ttl") = 0)
+      .def("start", [](Dir& d, const std::string& addr, bool log) {
+        d.srv.set_access_log(log);
+        return d.srv.start(addr);
+      }, py::arg("addr") = "127.0.0.1:0", py::arg("access_log") = false)
+      .def("stop", [](Dir& d) { d.srv.stop(); }, py::call_guard<py::gil_scoped_release>())
+      .def("size", [](Dir& d) { return d.svc.size(); });
+
+  // ---- relay ----
+  struct Relay {
+    std::shared_ptr<Host> h;
+    std::unique_ptr<RelayService> svc;
+  };
+  py::class_<Relay>(m, "Relay")
+      .def(py::init([](const std::string& listen) {
+        auto r = new Relay();
+        r->h = std::make_shared<Host>(PrivateKey::generate(KeyType::Ed25519), "p2p-relay");
+        r->h->listen(Multiaddr::parse(listen));
+        r->svc = std::make_unique<RelayService>(r->h);
+        return r;
+      }), py::arg("listen") = "/ip4/127.0.0.1/tcp/0")
+      .def_property_readonly("peer_id", [](Relay& r) { return r.h->id().to_base58(); })
+      .def("addrs", [](Relay& r) {
+        std::vector<std::string> out;
+        for (auto& a : r.h->addrs()) out.push_back(a.str() + "/p2p/" + r.h->id().to_base58());
+        return out;
+      })
+      .def("reservations", [](Relay& r) { return r.svc->reservations(); })
+      .def("stop", [](Relay& r) { r.h->close(); }, py::call_guard<py::gil_scoped_release>());
+
+  bind_runtime(m);
+}

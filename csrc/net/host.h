@@ -1,0 +1,116 @@
+// libp2p host: identity, listeners, connection upgrade (multistream -> Noise ->
+// multistream -> yamux), peerstore, protocol handlers, identify + ping, and
+// dialing through circuit-relay-v2 (relay.h).  Mirrors the subset of the
+// go-libp2p host the reference uses (`go/cmd/node/main.go:137-172,243-245`).
+#pragma once
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "conn.h"
+#include "multiaddr.h"
+#include "yamux.h"
+
+namespace p2p {
+
+extern const char* kIdentifyProto;  // "/ipfs/id/1.0.0"
+extern const char* kPingProto;      // "/ipfs/ping/1.0.0"
+extern const char* kNoiseProto;     // "/noise"
+extern const char* kYamuxProto;     // "/yamux/1.0.0"
+
+struct StreamCtx {
+  StreamPtr stream;
+  std::shared_ptr<BufConn> io;  // read/write through this (keeps pipelined bytes)
+  PeerId peer;
+  std::string protocol;
+  bool relayed = false;
+};
+using StreamHandler = std::function<void(StreamCtx&)>;
+
+struct PeerInfo {
+  PeerId id;
+  std::vector<Multiaddr> addrs;
+};
+
+class Host {
+ public:
+  explicit Host(PrivateKey key, std::string agent = "p2p-llm-chat-amd/0.1.0");
+  ~Host();
+  const PeerId& id() const { return id_; }
+  const PrivateKey& key() const { return key_; }
+  std::string agent() const { return agent_; }
+
+  // Listen on /ip4/<host>/tcp/<port> (port 0 = ephemeral).  Other transports
+  // (quic-v1) are accepted in the address list but skipped with a log line.
+  void listen(const Multiaddr& ma);
+  // h.Addrs(): listen addrs with 0.0.0.0 expanded to interface addresses, plus
+  // relay circuit addresses of active reservations.
+  std::vector<Multiaddr> addrs();
+  void add_advertised_addr(const Multiaddr& ma);
+
+  void set_stream_handler(const std::string& proto, StreamHandler h);
+  void remove_stream_handler(const std::string& proto);
+  std::vector<std::string> protocols();
+
+  // Peerstore
+  void add_addrs(const PeerId& p, const std::vector<Multiaddr>& addrs);
+  std::vector<Multiaddr> peer_addrs(const PeerId& p);
+  std::vector<PeerId> peers();            // peers with a live connection
+  bool connected(const PeerId& p);
+
+  // Connect (reuse an existing session, else dial known addrs in order,
+  // including /p2p-circuit addresses).  Throws NetError.
+  SessionPtr connect(const PeerId& p, const std::vector<Multiaddr>& addrs, int timeout_ms);
+  // Open a stream and negotiate `proto` on it.
+  StreamCtx new_stream(const PeerId& p, const std::string& proto, int timeout_ms);
+  long ping(const PeerId& p, int timeout_ms);
+
+  // Upgrade a raw (TCP or relayed) connection and register the session.
+  SessionPtr upgrade_outbound(ConnPtr raw, const PeerId& expected, bool relayed);
+  SessionPtr upgrade_inbound(ConnPtr raw, bool relayed);
+
+  // Identify results for a peer (protocols / listen addrs / agent).
+  std::vector<std::string> peer_protocols(const PeerId& p);
+  std::string peer_agent(const PeerId& p);
+
+  // Relay dialer hook (installed by RelayClient).
+  std::function<SessionPtr(const Multiaddr& relay, const PeerId& target, int timeout_ms)> relay_dialer;
+
+  void close();
+  bool closed() const { return closed_; }
+
+ private:
+  void accept_loop(std::shared_ptr<TcpListener> l);
+  void handle_stream(StreamPtr s, PeerId peer, bool relayed);
+  void add_session(const PeerId& p, SessionPtr s, bool relayed);
+  void run_identify(const PeerId& p, SessionPtr s);
+  void identify_handler(StreamCtx& ctx);
+
+  PrivateKey key_;
+  PeerId id_;
+  std::string agent_;
+  std::mutex mu_;
+  std::map<std::string, StreamHandler> handlers_;
+  std::map<PeerId, std::vector<Multiaddr>> peerstore_;
+  std::map<PeerId, SessionPtr> sessions_;
+  std::map<PeerId, std::vector<std::string>> peer_protos_;
+  std::map<PeerId, std::string> peer_agents_;
+  std::vector<std::shared_ptr<TcpListener>> listeners_;
+  std::vector<Multiaddr> listen_addrs_;
+  std::vector<Multiaddr> extra_addrs_;
+  std::vector<std::thread> threads_;
+  std::atomic<bool> closed_{false};
+  std::atomic<int> busy_{0};  // detached threads that use `this` (drained by close())
+  struct Busy {
+    Host* h;
+    explicit Busy(Host* x) : h(x) { h->busy_++; }
+    ~Busy() { h->busy_--; }
+  };
+};
+
+}  // namespace p2p

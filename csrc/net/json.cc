@@ -168,8 +168,18 @@ struct Parser {
   int depth = 0;
   explicit Parser(const std::string& t) : s(t) {}
   [[noreturn]] void fail(const char* m) {
-    char b[128];
+    char b[160];
     snprintf(b, sizeof(b), "json: %s at offset %zu", m, i);
+    throw JsonError(b);
+  }
+  // Go encoding/json wording for the common syntax errors (gin BindJSON bodies).
+  [[noreturn]] void fail_char(const char* ctx) {
+    if (i >= s.size()) throw JsonError("unexpected EOF");
+    char b[160];
+    char c = s[i];
+    if (c == '\'') snprintf(b, sizeof(b), "invalid character '\\'' %s", ctx);
+    else if ((unsigned char)c < 0x20) snprintf(b, sizeof(b), "invalid character '\\x%02x' %s", (unsigned char)c, ctx);
+    else snprintf(b, sizeof(b), "invalid character '%c' %s", c, ctx);
     throw JsonError(b);
   }
   void ws() {
@@ -249,7 +259,7 @@ struct Parser {
   }
   Json value() {
     ws();
-    if (i >= s.size()) fail("unexpected end");
+    if (i >= s.size()) throw JsonError("unexpected end of JSON input");
     if (++depth > 512) fail("nesting too deep");
     Json out;
     char c = s[i];
@@ -321,7 +331,7 @@ struct Parser {
       if (isint && num.size() < 18) out = Json((long long)strtoll(num.c_str(), nullptr, 10));
       else out = Json(strtod(num.c_str(), nullptr));
     } else {
-      fail("unexpected character");
+      fail_char("looking for beginning of value");
     }
     --depth;
     return out;
@@ -333,7 +343,7 @@ Json Json::parse(const std::string& text) {
   Parser p(text);
   Json v = p.value();
   p.ws();
-  if (p.i != text.size()) p.fail("trailing data");
+  if (p.i != text.size()) p.fail_char("after top-level value");
   return v;
 }
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <map>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <utility>
 #include <vector>

@@ -6,7 +6,11 @@
 #include <string.h>
 #include <time.h>
 
+#include <stdarg.h>
+
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 
 namespace p2p {
 
@@ -243,6 +247,29 @@ std::string uuid4() {
            "%02x%02x%02x%02x-%02x%02x-%02x%02x-%02x%02x-%02x%02x%02x%02x%02x%02x", b[0], b[1],
            b[2], b[3], b[4], b[5], b[6], b[7], b[8], b[9], b[10], b[11], b[12], b[13], b[14], b[15]);
   return out;
+}
+
+static std::atomic<bool> g_quiet{false};
+static std::mutex g_log_mu;
+
+void set_log_quiet(bool q) { g_quiet = q; }
+
+void logf(const char* fmt, ...) {
+  if (g_quiet) return;
+  char msg[4096];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(msg, sizeof(msg), fmt, ap);
+  va_end(ap);
+  time_t now = time(nullptr);
+  struct tm lt;
+  localtime_r(&now, &lt);
+  char ts[32];
+  strftime(ts, sizeof(ts), "%Y/%m/%d %H:%M:%S", &lt);
+  std::lock_guard<std::mutex> lk(g_log_mu);
+  size_t n = strlen(msg);
+  fprintf(stderr, "%s %s%s", ts, msg, (n && msg[n - 1] == '\n') ? "" : "\n");
+  fflush(stderr);
 }
 
 std::string env_or(const char* key, const std::string& def) {

@@ -71,6 +71,9 @@ double parse_rfc3339(const std::string& s);
 int64_t unix_ms();
 
 std::string uuid4();
+// Go `log` package format: "2006/01/02 15:04:05 message" on stderr.
+void logf(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void set_log_quiet(bool quiet);
 std::string env_or(const char* key, const std::string& def);
 
 }  // namespace p2p

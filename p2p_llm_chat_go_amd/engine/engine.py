@@ -87,12 +87,12 @@ class Engine:
             self._prefill_ws[key] = ws
         return ws
 
-    def decode_graph(self, B: int, ctx: int) -> DecodeGraph:
-        key = (bucket(B, BATCH_BUCKETS), bucket(ctx, CTX_BUCKETS))
+    def decode_graph(self, B: int, ctx: int, greedy: bool = True) -> DecodeGraph:
+        key = (bucket(B, BATCH_BUCKETS), bucket(ctx, CTX_BUCKETS), greedy)
         g = self._graphs.get(key)
         if g is None:
             st = DecodeState(self.model, key[0], key[1] // PAGE, key[1], key[1])
-            g = DecodeGraph(st, self.use_graph).capture()
+            g = DecodeGraph(st, self.use_graph, greedy=greedy).capture()
             self._graphs[key] = g
         return g
 

@@ -67,6 +67,14 @@ class DecodeState:
         self.ids.copy_(i, non_blocking=True)
         self.slots.copy_(slots, non_blocking=True)
 
+    def body_logits(self):
+        """Forward only (sampling mode): logits of every row in ws.logits."""
+        self.model.forward(self.ws, self.ids, self.pos, self.slots, self.bt, self.row_bt,
+                           self.ctx, self.B, self.max_ctx)
+
+    def advance(self):
+        ops.advance(self.ids, self.pos, self.ctx, self.slots, self.bt, self.hist, self.step)
+
     def body(self):
         m = self.model
         keys = m.forward(self.ws, self.ids, self.pos, self.slots, self.bt, self.row_bt, self.ctx,
@@ -79,10 +87,20 @@ class DecodeState:
 
 
 class DecodeGraph:
-    def __init__(self, state: DecodeState, use_graph: bool = True):
+    """greedy=True: the whole step incl. argmax + advance is one graph replay.
+    greedy=False: the graph computes logits; sampling + advance run after it."""
+
+    def __init__(self, state: DecodeState, use_graph: bool = True, greedy: bool = True):
         self.state = state
         self.graph = None
+        self.greedy = greedy
         self.use_graph = use_graph and state.model.device.type == "cuda"
+
+    def _body(self):
+        if self.greedy:
+            self.state.body()
+        else:
+            self.state.body_logits()
 
     def capture(self, warmup: int = 2):
         st = self.state
@@ -93,21 +111,36 @@ class DecodeGraph:
         s.wait_stream(torch.cuda.current_stream(st.model.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                st.body()
+                self._body()
         torch.cuda.current_stream(st.model.device).wait_stream(s)
         torch.cuda.synchronize(st.model.device)
         st.reset_dummy()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            st.body()
+            self._body()
         torch.cuda.synchronize(st.model.device)
         st.reset_dummy()
         self.graph = g
         return self
 
     def replay(self, n: int = 1):
+        assert self.greedy
         for _ in range(n):
             if self.graph is not None:
                 self.graph.replay()
             else:
                 self.state.body()
+
+    def step_sampled(self, params: list, generator=None):
+        """One decode step with per-row SamplingParams (non-greedy rows sample)."""
+        from .sampling import sample
+
+        st = self.state
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            st.body_logits()
+        ids = sample(st.ws.logits[:st.B], list(params) + [params[-1]] * (st.B - len(params)),
+                     generator)
+        st.ids.copy_(ids)
+        st.advance()

@@ -1,0 +1,203 @@
+"""Continuous-batching suggest-reply server (the in-process Ollama replacement).
+
+HTTP threads of the C++ node call ``handle_json`` (Ollama ``/api/generate`` /
+``/api/chat`` request JSON -> response JSON).  Requests are queued in the
+native ``Scheduler`` (csrc/runtime/scheduler.cc); one engine thread runs the
+loop:
+
+    plan = scheduler.schedule()
+    prefill the newly admitted prompts (one flat batch)     -> first tokens (TTFT)
+    decode every running sequence for a chunk of k steps     (hipGraph replays)
+    retire finished sequences (EOS / num_predict), free their KV pages
+
+so concurrent peers share every weight read of the decode step (the reference
+serves one blocking request per click, `web/streamlit_app.py:163-165`).
+"""
+from __future__ import annotations
+
+import json
+import threading
+import time
+from concurrent.futures import Future
+
+import torch
+
+from ..native import load as load_native
+from .engine import CTX_BUCKETS, Engine
+from .sampling import SamplingParams
+from .tokenizer import get_tokenizer
+
+
+class EngineServer:
+    def __init__(self, engine: Engine, tokenizer=None, model_name: str = "llama3.1",
+                 max_batch: int | None = None, decode_chunk: int = 8,
+                 default_max_tokens: int = 128, max_ctx: int | None = None):
+        self.engine = engine
+        self.tok = tokenizer or get_tokenizer(engine.cfg)
+        self.model_name = model_name
+        self.max_batch = max_batch or engine.max_batch
+        self.decode_chunk = decode_chunk
+        self.default_max_tokens = default_max_tokens
+        self.max_ctx = max_ctx or min(engine.cfg.max_pos, CTX_BUCKETS[-1],
+                                      engine.kv.num_pages * 64)
+        N = load_native()
+        self.sched = N.Scheduler(num_pages=engine.kv.num_pages, page_size=64,
+                                 max_batch=self.max_batch,
+                                 max_prefill_tokens=engine.max_prefill_tokens, max_ctx=self.max_ctx)
+        # the scheduler owns page allocation for served requests
+        self._lock = threading.Condition()
+        self._reqs = {}      # id -> dict(prompt, params, future, t_submit, t_admit, t_first)
+        self._pending = []   # (prompt_ids, params, future, t_submit) waiting to enter the scheduler
+        self._stop = False
+        self._gen = torch.Generator(device=engine.device)
+        self.stats = {"requests": 0, "tokens": 0, "prefill_tokens": 0, "decode_steps": 0,
+                      "busy_s": 0.0}
+        self._thread = threading.Thread(target=self._loop, name="engine-loop", daemon=True)
+        self._thread.start()
+
+    # --------------------------------------------------------------- API
+    def submit(self, prompt_ids: list, params: SamplingParams) -> Future:
+        fut = Future()
+        with self._lock:
+            self._pending.append((list(prompt_ids), params, fut, time.perf_counter_ns()))
+            self._lock.notify()
+        return fut
+
+    def generate(self, prompt_ids, params: SamplingParams, timeout: float = 600.0) -> dict:
+        return self.submit(prompt_ids, params).result(timeout)
+
+    def close(self):
+        with self._lock:
+            self._stop = True
+            self._lock.notify()
+        self._thread.join(timeout=10)
+
+    def metrics(self) -> dict:
+        s = dict(self.stats)
+        s["running"] = self.sched.n_running
+        s["waiting"] = self.sched.n_waiting + len(self._pending)
+        s["free_kv_pages"] = self.sched.free_pages
+        return s
+
+    def handle_json(self, req_text: str) -> str:
+        """Ollama-compatible generate/chat handler (installed as the node's hook)."""
+        req = json.loads(req_text)
+        if req.get("endpoint") == "metrics":
+            return json.dumps(self.metrics())
+        params = SamplingParams.from_ollama(req.get("options"), self.default_max_tokens)
+        if req.get("endpoint") == "chat":
+            msgs = req.get("messages") or []
+            text = "\n".join(m.get("content", "") for m in msgs if m.get("role") != "system")
+            ids = self.tok.chat_ids(text)
+        elif req.get("raw"):
+            ids = self.tok.encode(req.get("prompt", ""), bos=True)
+        else:
+            ids = self.tok.chat_ids(req.get("prompt", ""))
+        r = self.generate(ids, params)
+        text = self.tok.decode(r["tokens"])
+        now = time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime()) + ".000000Z"
+        out = {"model": req.get("model", self.model_name), "created_at": now, "done": True,
+               "done_reason": r["done_reason"], "total_duration": r["total_duration"],
+               "load_duration": 0, "prompt_eval_count": r["prompt_eval_count"],
+               "prompt_eval_duration": r["prompt_eval_duration"], "eval_count": r["eval_count"],
+               "eval_duration": r["eval_duration"]}
+        if req.get("endpoint") == "chat":
+            out["message"] = {"role": "assistant", "content": text}
+        else:
+            out["response"] = text
+            out["context"] = []
+        return json.dumps(out)
+
+    # --------------------------------------------------------------- loop
+    def _admit_pending(self):
+        with self._lock:
+            pend, self._pending = self._pending, []
+        for prompt, params, fut, t0 in pend:
+            try:
+                rid = self.sched.add(len(prompt), params.max_tokens, params.stop_on_eos,
+                                     list(self.engine.cfg.eos_ids))
+            except Exception as e:  # too long / bad request
+                fut.set_exception(e)
+                continue
+            self._reqs[rid] = {"prompt": prompt, "params": params, "future": fut, "t_submit": t0}
+
+    def _loop(self):
+        eng = self.engine
+        while True:
+            with self._lock:
+                while (not self._stop and not self._pending and self.sched.n_running == 0
+                       and self.sched.n_waiting == 0):
+                    self._lock.wait(timeout=0.5)
+                if self._stop:
+                    break
+            t_busy = time.perf_counter()
+            try:
+                self._step(eng)
+            except Exception as e:  # fail every in-flight request, keep serving
+                for rid, r in list(self._reqs.items()):
+                    if not r["future"].done():
+                        r["future"].set_exception(e)
+                    self.sched.cancel(rid)
+                self.sched.take_finished()
+                self._reqs.clear()
+            self.stats["busy_s"] += time.perf_counter() - t_busy
+
+    def _step(self, eng: Engine):
+        self._admit_pending()
+        plan = self.sched.schedule()
+        if plan.prefill:
+            prompts = [self._reqs[i]["prompt"] for i in plan.prefill]
+            pages = [list(self.sched.get(i).pages) for i in plan.prefill]
+            t0 = time.perf_counter_ns()
+            for i in plan.prefill:
+                self._reqs[i]["t_admit"] = t0
+            first = eng.prefill(prompts, pages).cpu().tolist()
+            t1 = time.perf_counter_ns()
+            self.stats["prefill_tokens"] += sum(len(p) for p in prompts)
+            for i, tkn in zip(plan.prefill, first):
+                self._reqs[i]["t_first"] = t1
+                self.sched.on_first_token(i, int(tkn))
+        running = [i for i in list(plan.decode) + list(plan.prefill)
+                   if self.sched.get(i).state == 1]
+        if running:
+            self._decode(eng, running)
+        self._retire()
+
+    def _decode(self, eng: Engine, running: list):
+        reqs = [self.sched.get(i) for i in running]
+        params = [self._reqs[i]["params"] for i in running]
+        greedy = all(p.greedy for p in params)
+        ctx = max(r.prompt_len + r.max_new for r in reqs)
+        g = eng.decode_graph(len(running), ctx, greedy=greedy)
+        st = g.state
+        st.load([r.tokens[-1] for r in reqs], [r.pos for r in reqs], [list(r.pages) for r in reqs])
+        remaining = min(r.max_new - len(r.tokens) for r in reqs)
+        waiting = self.sched.n_waiting + len(self._pending)
+        k = max(1, min(self.decode_chunk if not waiting else 2, remaining))
+        if greedy:
+            g.replay(k)
+        else:
+            for _ in range(k):
+                g.step_sampled(params, self._gen)
+        hist = st.hist[:len(running), :k].cpu().tolist()
+        self.stats["decode_steps"] += k
+        self.sched.on_decode_tokens(running, hist)
+
+    def _retire(self):
+        now = time.perf_counter_ns()
+        for rid in self.sched.take_finished():
+            r = self._reqs.pop(rid, None)
+            sr = self.sched.get(rid)
+            if r is not None and not r["future"].done():
+                t_first = r.get("t_first", now)
+                toks = list(sr.tokens)
+                self.stats["requests"] += 1
+                self.stats["tokens"] += len(toks)
+                r["future"].set_result({
+                    "tokens": toks, "done_reason": sr.finish_reason or "stop",
+                    "prompt_eval_count": sr.prompt_len,
+                    "prompt_eval_duration": t_first - r.get("t_admit", r["t_submit"]),
+                    "eval_count": len(toks), "eval_duration": now - t_first,
+                    "total_duration": now - r["t_submit"],
+                    "ttft_ns": t_first - r["t_submit"]})
+            self.sched.release(rid)

@@ -1,0 +1,93 @@
+"""Chat node with the in-process suggest-reply engine.
+
+    python -m p2p_llm_chat_go_amd.net.node
+
+Same environment as the reference node (`go/cmd/node/main.go:131-134`):
+MYNAMEIS, HTTP_ADDR, DIRECTORY_URL, BOOTSTRAP_ADDRS -- plus opt-in extras
+(RELAY_ADDRS, KEY_TYPE, IDENTITY_FILE, INBOX_FILE, REGISTER_INTERVAL,
+STRICT_SENDER, UI_FILE) and the engine knobs:
+
+  ENGINE          1 (default) / 0: attach the in-process engine
+  ENGINE_MODEL    preset name (default: llama3.1-8b on a GPU, tiny-llama on CPU)
+  ENGINE_DEVICE   cuda:N / cpu (default: cuda:0 if available)
+  ENGINE_CHECKPOINT  HF checkpoint dir (safetensors + config.json); default random-init
+  ENGINE_MAX_BATCH   concurrent sequences (default 16)
+  ENGINE_MAX_TOKENS  default num_predict (default 128)
+  TOKENIZER_PATH  tokenizer.json (default: synthetic offline tokenizer)
+
+The libp2p host, HTTP API and Directory client are the C++ ``Node``; this
+process only adds the GPU engine behind the node's /api/generate, /api/chat
+and /suggest routes (no Ollama process boundary).
+"""
+from __future__ import annotations
+
+import os
+import signal
+import sys
+import threading
+
+
+def build_engine_server(model: str | None = None, device: str | None = None):
+    import torch
+
+    from ..engine import Engine
+    from ..engine.server import EngineServer
+    from ..engine.tokenizer import get_tokenizer
+    from ..models.config import get_config
+    from ..models.weights import (EngineWeights, config_from_hf, load_safetensors_dir)
+
+    dev = device or os.environ.get("ENGINE_DEVICE") or ("cuda:0" if torch.cuda.is_available()
+                                                        else "cpu")
+    ckpt = os.environ.get("ENGINE_CHECKPOINT", "")
+    max_batch = int(os.environ.get("ENGINE_MAX_BATCH", "16"))
+    if ckpt:
+        cfg = config_from_hf(ckpt)
+        weights = EngineWeights.from_state_dict(load_safetensors_dir(ckpt, dev), cfg, dev)
+    else:
+        name = model or os.environ.get("ENGINE_MODEL") or (
+            "llama3.1-8b" if str(dev).startswith("cuda") else "tiny-llama")
+        cfg = get_config(name)
+        weights = None
+    kv_pages = None if str(dev).startswith("cuda") else 256
+    eng = Engine(cfg, weights=weights, device=dev, kv_pages=kv_pages, max_batch=max_batch)
+    tok = get_tokenizer(cfg, os.environ.get("TOKENIZER_PATH") or (ckpt or None))
+    return EngineServer(eng, tok, model_name=os.environ.get("LLM_MODEL", "llama3.1"),
+                        default_max_tokens=int(os.environ.get("ENGINE_MAX_TOKENS", "128")))
+
+
+def main(argv=None):
+    from ..native import load
+
+    N = load()
+    cfg = {}
+    ui = os.environ.get("UI_FILE") or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "web",
+        "index.html")
+    if os.path.exists(ui):
+        cfg["ui_file"] = ui
+    node = N.Node(cfg)
+    server = None
+    if os.environ.get("ENGINE", "1") != "0":
+        server = build_engine_server()
+        node.set_generate_hook(server.handle_json)
+    try:
+        node.start()
+    except Exception as e:  # log.Fatal("directory register failed:", err)
+        print("directory register failed: %s" % e, file=sys.stderr, flush=True)
+        sys.exit(1)
+    stop = threading.Event()
+
+    def _sig(*_):
+        stop.set()
+
+    signal.signal(signal.SIGTERM, _sig)
+    signal.signal(signal.SIGINT, _sig)
+    while not stop.wait(0.5):
+        pass
+    node.stop()
+    if server is not None:
+        server.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,229 @@
+"""Loopback integration of the chat plane (BASELINE config 1 plumbing).
+
+Directory + N node daemons on 127.0.0.1 with ephemeral libp2p ports, exactly
+the reference's manual test topology (`start_all.sh:5-40`), checked against
+the HTTP contracts of SURVEY §2A.1 (`go/cmd/node/main.go:213-283`,
+`go/cmd/directory/main.go:57-97`), plus the relay-only path.
+"""
+import json
+import os
+import time
+
+import pytest
+
+from netutil import BIN, Procs, free_port, http, wait_http
+
+pytestmark = pytest.mark.skipif(not os.path.exists(os.path.join(BIN, "p2p-node")),
+                                reason="native daemons not built")
+
+
+@pytest.fixture()
+def procs():
+    p = Procs()
+    yield p
+    p.close()
+
+
+def start_directory(procs, ttl=0):
+    port = free_port()
+    procs.spawn("p2p-directory", {"ADDR": "127.0.0.1:%d" % port, "DIRECTORY_TTL": str(ttl)})
+    url = "http://127.0.0.1:%d" % port
+    wait_http(url + "/health")
+    return url
+
+
+def start_node(procs, name, dir_url, extra=None, key="ed25519"):
+    port = free_port()
+    env = {"MYNAMEIS": name, "HTTP_ADDR": "127.0.0.1:%d" % port, "DIRECTORY_URL": dir_url,
+           "KEY_TYPE": key, "LISTEN_ADDRS": "/ip4/127.0.0.1/tcp/0"}
+    env.update(extra or {})
+    procs.spawn("p2p-node", env)
+    url = "http://127.0.0.1:%d" % port
+    wait_http(url + "/me")
+    return url
+
+
+# ------------------------------------------------------------------ directory
+def test_directory_contract(procs):
+    d = start_directory(procs)
+    assert http("POST", d + "/register", {"username": "a", "peer_id": "P", "addrs": ["/x"]})[:2] == \
+        (200, '{"ok":true}')
+    assert http("POST", d + "/register", {"username": "", "peer_id": "P"})[:2] == (400, "missing fields")
+    assert http("POST", d + "/register", {"username": "a"})[:2] == (400, "missing fields")
+    st, body, _ = http("POST", d + "/register", "not json")
+    assert st == 400 and body.startswith("invalid character")
+    assert http("POST", d + "/register", "")[:2] == (400, "EOF")
+    assert http("GET", d + "/lookup")[:2] == (400, "username required")
+    assert http("GET", d + "/lookup?username=zz")[:2] == (404, "not found")
+    st, body, hdr = http("GET", d + "/lookup?username=a")
+    assert st == 200 and json.loads(body) == {"addrs": ["/x"], "peer_id": "P"}
+    assert hdr["Content-Type"].startswith("application/json")
+    # last writer wins
+    http("POST", d + "/register", {"username": "a", "peer_id": "Q", "addrs": []})
+    assert json.loads(http("GET", d + "/lookup?username=a")[1])["peer_id"] == "Q"
+    # usernames with reserved characters round-trip through URL escaping
+    http("POST", d + "/register", {"username": "a b&c", "peer_id": "R", "addrs": []})
+    assert json.loads(http("GET", d + "/lookup?username=a%20b%26c")[1])["peer_id"] == "R"
+
+
+def test_directory_ttl(procs):
+    d = start_directory(procs, ttl=1)
+    http("POST", d + "/register", {"username": "a", "peer_id": "P", "addrs": []})
+    assert http("GET", d + "/lookup?username=a")[0] == 200
+    time.sleep(1.3)
+    assert http("GET", d + "/lookup?username=a")[0] == 404
+
+
+# ------------------------------------------------------------------ nodes
+@pytest.mark.parametrize("key", ["ed25519", "rsa"])
+def test_two_nodes_send_inbox_me(procs, key):
+    d = start_directory(procs)
+    a = start_node(procs, "Najy", d, key=key)
+    b = start_node(procs, "Cannan", d, key=key)
+    st, body, _ = http("GET", a + "/me")
+    me = json.loads(body)
+    assert st == 200 and list(me) == ["addrs", "peer_id", "username"] and me["username"] == "Najy"
+    assert me["peer_id"].startswith("12D3KooW" if key == "ed25519" else "Qm")
+    assert all(x.endswith("/p2p/" + me["peer_id"]) for x in me["addrs"])
+    # directory holds the same record
+    rec = json.loads(http("GET", d + "/lookup?username=Najy")[1])
+    assert rec["peer_id"] == me["peer_id"] and rec["addrs"] == me["addrs"]
+
+    assert http("GET", b + "/inbox")[1] == "[]"
+    ids = []
+    for i in range(3):
+        st, body, _ = http("POST", a + "/send", {"to_username": "Cannan", "content": "msg %d <&>" % i})
+        r = json.loads(body)
+        assert st == 200 and list(r) == ["id", "status"] and r["status"] == "sent"
+        ids.append(r["id"])
+    for _ in range(100):
+        inbox = json.loads(http("GET", b + "/inbox?after=")[1])
+        if len(inbox) == 3:
+            break
+        time.sleep(0.05)
+    assert [m["id"] for m in inbox] == ids
+    m0 = inbox[0]
+    assert list(m0) == ["id", "from_user", "to_user", "content", "timestamp"]
+    assert m0["from_user"] == "Najy" and m0["to_user"] == "Cannan" and m0["content"] == "msg 0 <&>"
+    from datetime import datetime
+    datetime.fromisoformat(m0["timestamp"].replace("Z", "+00:00"))  # reference UI parse_ts
+    # Drain(after) semantics: strictly after, non-destructive, unknown id -> []
+    assert [m["id"] for m in json.loads(http("GET", b + "/inbox?after=" + ids[0])[1])] == ids[1:]
+    assert json.loads(http("GET", b + "/inbox?after=" + ids[2])[1]) == []
+    assert json.loads(http("GET", b + "/inbox?after=nope")[1]) == []
+    assert len(json.loads(http("GET", b + "/inbox")[1])) == 3
+    # reply the other way
+    st, _, _ = http("POST", b + "/send", {"to_username": "Najy", "content": "back"})
+    assert st == 200
+    for _ in range(100):
+        got = json.loads(http("GET", a + "/inbox")[1])
+        if got:
+            break
+        time.sleep(0.05)
+    assert got[0]["content"] == "back" and got[0]["from_user"] == "Cannan"
+
+
+def test_send_error_contract(procs):
+    d = start_directory(procs)
+    a = start_node(procs, "A", d)
+    assert http("POST", a + "/send", {"to_username": "ghost", "content": "x"})[:2] == \
+        (404, '{"error":"user not found"}')
+    st, body, _ = http("POST", a + "/send", {"to_username": "A", "content": "x"})
+    assert st == 500 and json.loads(body)["error"].startswith("open stream failed:")
+    st, body, _ = http("POST", a + "/send", "{bad")
+    assert st == 400 and "error" in json.loads(body)
+    st, body, _ = http("POST", a + "/send", {"to_username": 5})
+    assert st == 400 and "cannot unmarshal number" in json.loads(body)["error"]
+    # a directory entry with an undecodable peer id -> 400 bad peer id
+    http("POST", d + "/register", {"username": "bad", "peer_id": "not-a-peer-id", "addrs": []})
+    assert http("POST", a + "/send", {"to_username": "bad", "content": "x"})[:2] == \
+        (400, '{"error":"bad peer id"}')
+    # a registered but unreachable peer -> 500 open stream failed
+    from p2p_llm_chat_go_amd.native import load
+    _, _, pid = load().keygen("ed25519")
+    http("POST", d + "/register", {"username": "gone", "peer_id": pid,
+                                   "addrs": ["/ip4/127.0.0.1/tcp/%d/p2p/%s" % (free_port(), pid)]})
+    st, body, _ = http("POST", a + "/send", {"to_username": "gone", "content": "x"})
+    assert st == 500 and json.loads(body)["error"].startswith("open stream failed:")
+
+
+def test_directory_down_is_404(procs):
+    d = start_directory(procs)
+    a = start_node(procs, "A", d)
+    procs.procs[0].terminate()
+    procs.procs[0].wait()
+    assert http("POST", a + "/send", {"to_username": "B", "content": "x"})[:2] == \
+        (404, '{"error":"user not found"}')
+
+
+def test_node_exits_when_directory_unreachable(procs):
+    port = free_port()
+    p = procs.spawn("p2p-node", {"MYNAMEIS": "x", "HTTP_ADDR": "127.0.0.1:%d" % port,
+                                 "DIRECTORY_URL": "http://127.0.0.1:%d" % free_port()})
+    assert p.wait(timeout=20) == 1  # log.Fatal("directory register failed")
+
+
+def test_bootstrap_and_peers(procs):
+    d = start_directory(procs)
+    a = start_node(procs, "A", d)
+    boot = json.loads(http("GET", a + "/me")[1])["addrs"][0]
+    b = start_node(procs, "B", d, {"BOOTSTRAP_ADDRS": " %s , /bad/addr ," % boot})
+    pid_a = json.loads(http("GET", a + "/me")[1])["peer_id"]
+    for _ in range(100):
+        peers = json.loads(http("GET", b + "/peers")[1])
+        if peers and peers[0]["protocols"]:
+            break
+        time.sleep(0.05)
+    assert peers[0]["peer_id"] == pid_a  # connected via bootstrap, identify ran
+    assert "/p2p-llm-chat/1.0.0" in peers[0]["protocols"]
+
+
+def test_relay_only_path(procs, tmp_path):
+    """Node B has no listener; it is reachable only through a circuit-relay-v2 reservation."""
+    d = start_directory(procs)
+    out = tmp_path / "relay.out"
+    with open(out, "w") as f:
+        procs.spawn("p2p-relay", {"RELAY_LISTEN": "/ip4/127.0.0.1/tcp/0"}, stdout=f)
+    for _ in range(200):
+        lines = [x.strip() for x in open(out).read().splitlines() if "/p2p/" in x]
+        if lines:
+            break
+        time.sleep(0.05)
+    relay = lines[0]
+    a = start_node(procs, "A", d)
+    b = start_node(procs, "B", d, {"LISTEN_ADDRS": "none", "RELAY_ADDRS": relay})
+    me_b = json.loads(http("GET", b + "/me")[1])
+    assert me_b["addrs"] and all("/p2p-circuit/p2p/" in x for x in me_b["addrs"])
+    st, body, _ = http("POST", a + "/send", {"to_username": "B", "content": "via relay"})
+    assert st == 200, body
+    for _ in range(100):
+        inbox = json.loads(http("GET", b + "/inbox")[1])
+        if inbox:
+            break
+        time.sleep(0.05)
+    assert inbox[0]["content"] == "via relay"
+    # and back: B dials A directly
+    assert http("POST", b + "/send", {"to_username": "A", "content": "direct back"})[0] == 200
+
+
+def test_identity_and_inbox_persistence(procs, tmp_path):
+    d = start_directory(procs)
+    idf, ibf = str(tmp_path / "id.key"), str(tmp_path / "inbox.jsonl")
+    a = start_node(procs, "A", d)
+    b = start_node(procs, "B", d, {"IDENTITY_FILE": idf, "INBOX_FILE": ibf})
+    pid1 = json.loads(http("GET", b + "/me")[1])["peer_id"]
+    assert http("POST", a + "/send", {"to_username": "B", "content": "persist me"})[0] == 200
+    time.sleep(0.3)
+    procs.procs[-1].terminate()
+    procs.procs[-1].wait()
+    b2 = start_node(procs, "B", d, {"IDENTITY_FILE": idf, "INBOX_FILE": ibf})
+    assert json.loads(http("GET", b2 + "/me")[1])["peer_id"] == pid1
+    assert json.loads(http("GET", b2 + "/inbox")[1])[0]["content"] == "persist me"
+
+
+def test_suggest_without_engine_is_503(procs):
+    d = start_directory(procs)
+    a = start_node(procs, "A", d)
+    st, body, _ = http("POST", a + "/suggest", {"message": "hi"})
+    assert st == 503 and "LLM unavailable" in json.loads(body)["error"]
+    assert http("GET", a + "/metrics")[0] == 200
