@@ -55,6 +55,17 @@ struct EpiArgs {
   int Hq, Hkv;
   // EPI_ARGMAX: global column offset of this shard (vocab-parallel LM head)
   int col_offset;
+  // Grouped (MoE) mode: blockIdx.y = local expert e.  Its rows are the slot ids
+  // rows[e * rows_stride + i], i < cnt[e]; the A row of slot s is X[s / x_div]
+  // (x_div = top_k when X holds token rows), the output row is s, scaled by
+  // row_w[s] when row_w != null.  Expert weights are w_stride bf16x8 apart.
+  const int* moe_cnt;
+  const int* moe_rows;
+  int rows_stride;
+  int x_div;
+  const float* row_w;
+  long long w_stride;
+  int n_experts;
 };
 
 __device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) {
@@ -118,7 +129,7 @@ __device__ __forceinline__ void epi_store(int m, bool valid, int g, int r, float
   }
 }
 
-template <int MT, int WAVES, int EPI, bool NORM, int U>
+template <int MT, int WAVES, int EPI, bool NORM, int U, bool MOE = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     const bf16x8* __restrict__ Wt, const bf16* __restrict__ X, int ldx, int M, int K,
     int up_group_offset, void* __restrict__ out, int ldo, float eps, EpiArgs ea) {
@@ -130,6 +141,14 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   const int s0 = (S * w) / WAVES;
   const int s1 = (S * (w + 1)) / WAVES;
   const int r = lane & 15, q = lane >> 4;
+  const int* mrows = nullptr;
+  if constexpr (MOE) {
+    const int e = blockIdx.y;
+    M = min(ea.moe_cnt[e], M);
+    if (M <= 0) return;  // expert not selected by any row: its weights are never read
+    Wt += (size_t)e * ea.w_stride;
+    mrows = ea.moe_rows + (size_t)e * ea.rows_stride;
+  }
 
   const bf16x8* wp[NB];
   wp[0] = Wt + (size_t)g * S * 64 + lane;
@@ -141,7 +160,9 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   for (int mt = 0; mt < MT; ++mt) {
     const int row = mt * 16 + r;
     xv[mt] = row < M;
-    xp[mt] = X + (size_t)(xv[mt] ? row : 0) * ldx + 8 * q;
+    int xrow = xv[mt] ? row : 0;
+    if constexpr (MOE) xrow = xv[mt] ? mrows[row] / ea.x_div : 0;
+    xp[mt] = X + (size_t)xrow * ldx + 8 * q;
   }
 
   f32x4 acc[NB][MT];
@@ -277,8 +298,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           for (int ww = 0; ww < WAVES; ++ww) t += red_ss[ww][mt][q * 4 + j];
           scale = rsqrtf(t / (float)K + eps);
         }
-        epi_store<EPI>(m, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out, ldo,
-                       ea);
+        int orow = m;
+        if constexpr (MOE) {
+          orow = m < M ? mrows[m] : 0;
+          if (ea.row_w && m < M) scale *= ea.row_w[orow];
+        }
+        epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out,
+                       ldo, ea);
       }
     }
   } else {
@@ -293,8 +319,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           const float t = __shfl(ss[mt], q * 4 + j, 64);
           scale = rsqrtf(t / (float)K + eps);
         }
-        epi_store<EPI>(m, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out, ldo,
-                       ea);
+        int orow = m;
+        if constexpr (MOE) {
+          orow = m < M ? mrows[m] : 0;
+          if (ea.row_w && m < M) scale *= ea.row_w[orow];
+        }
+        epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out,
+                       ldo, ea);
       }
     }
   }
@@ -304,6 +335,16 @@ template <int MT, int WAVES, int EPI, bool NORM>
 int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   constexpr int U = (MT == 1) ? 8 : 4;
+  if (ea.moe_cnt) {
+    if constexpr (EPI == EPI_SILU || EPI == EPI_STORE) {
+      hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, true>),
+                         dim3(groups, ea.n_experts),
+                         dim3(WAVES * 64), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K,
+                         up_off, out, ldo, eps, ea);
+      return (int)hipGetLastError();
+    }
+    return (int)hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>), dim3(groups), dim3(WAVES * 64), 0,
                      st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, up_off, out, ldo, eps, ea);
   return (int)hipGetLastError();
@@ -422,4 +463,25 @@ P2P_API int p2p_skinny_gemm_qkv_rope(const void* Wt, const void* X, int ldx, int
   ea.Hkv = Hkv;
   const int N = (Hq + 2 * Hkv) * HD;
   return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_QKV_ROPE, 1, nullptr, 0, eps, waves, ea, stream);
+}
+
+// Grouped (MoE) projection over the local experts (blockIdx.y = expert):
+//   expert e multiplies rows slot = rows[e*rows_stride + i] (i < cnt[e], <= max_rows) of
+//   X (row slot / x_div) with its weights (Wt + e*w_stride) and writes output row slot.
+// epi: 0 store (scaled by row_w[slot] if row_w) | 2 silu(gate)*up with RMSNorm (norm=1).
+P2P_API int p2p_grouped_gemm(const void* Wt, long long w_stride, int n_experts, const int* cnt,
+                             const int* rows, int rows_stride, int x_div, const float* row_w,
+                             const void* X, int ldx, int max_rows, int K, int N, int epi, int norm,
+                             void* out, int ldo, float eps, int waves, hipStream_t stream) {
+  if (n_experts <= 0 || !cnt || !rows) return (int)hipErrorInvalidValue;
+  if (epi != EPI_STORE && epi != EPI_SILU) return (int)hipErrorInvalidValue;
+  EpiArgs ea = {};
+  ea.moe_cnt = cnt;
+  ea.moe_rows = rows;
+  ea.rows_stride = rows_stride;
+  ea.x_div = x_div > 0 ? x_div : 1;
+  ea.row_w = row_w;
+  ea.w_stride = w_stride;
+  ea.n_experts = n_experts;
+  return skinny_dispatch(Wt, X, ldx, max_rows, K, N, epi, norm, out, ldo, eps, waves, ea, stream);
 }

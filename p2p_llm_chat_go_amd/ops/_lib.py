@@ -48,6 +48,13 @@ _SIGS = {
     "p2p_skinny_gemm_qkv_rope": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float,
                                  c_int, c_void_p],
+    "p2p_grouped_gemm": [c_void_p, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_int, c_int,
+                         c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                         c_int, c_float, c_int, c_void_p],
+    "p2p_moe_route": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                      c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_moe_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                        c_int, c_int, c_void_p],
 }
 
 

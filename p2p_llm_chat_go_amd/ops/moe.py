@@ -1,0 +1,86 @@
+"""Sparse-MoE ops (Mixtral): routing, grouped expert GEMMs, combine.
+
+The expert GEMMs are the grouped mode of the skinny MFMA kernel
+(``csrc/kernels/skinny_gemm.hip``): one launch covers all local experts
+(grid.y), each expert reads its weights only if at least one row was routed to
+it -- at decode batch 1 Mixtral streams 2 of its 8 experts per layer.
+Slots: a token r routed to its k-th expert is slot r*top_k + k.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .gemm import EPI_SILU, EPI_STORE, _ref, tiled_shape
+
+
+def moe_route(logits, E, K, e_lo, e_local, topk_ids, topk_w, cnt, rows):
+    """logits [R, >=E] fp32 -> topk ids/weights [R*K], cnt [e_local], rows [e_local, R]."""
+    R = logits.shape[0]
+    if logits.device.type != "cuda":
+        p = torch.softmax(logits[:, :E].float(), -1)
+        w, ids = p.topk(K, dim=-1)
+        w = w / w.sum(-1, keepdim=True)
+        topk_ids[:R * K] = ids.reshape(-1).to(torch.int32)
+        topk_w[:R * K] = w.reshape(-1)
+        cnt.zero_()
+        for s, e in enumerate(ids.reshape(-1).tolist()):
+            le = e - e_lo
+            if 0 <= le < e_local:
+                rows[le, int(cnt[le])] = s
+                cnt[le] += 1
+        return
+    L = _lib.lib()
+    _lib.check(L.p2p_moe_route(logits.data_ptr(), logits.stride(0), R, E, K, e_lo, e_local,
+                               topk_ids.data_ptr(), topk_w.data_ptr(), cnt.data_ptr(),
+                               rows.data_ptr(), rows.stride(0), _lib.stream_ptr(logits.device)),
+               "moe_route")
+
+
+def grouped_gemm(wt, cnt, rows, x, x_div, max_rows, epi, out, norm=False, row_w=None, eps=1e-5):
+    """Per local expert e: out[slot] = epi(x[slot // x_div] @ W_e^T) for its routed slots.
+
+    wt: [E_local, N/16, K/32, 64, 8] tiled expert weights.
+    """
+    E = wt.shape[0]
+    N, K = tiled_shape(wt[0])
+    if x.device.type != "cuda":
+        for e in range(E):
+            c = int(cnt[e])
+            if c == 0:
+                continue
+            slots = rows[e, :c].long()
+            xs = x[slots // x_div]
+            n_out = N // 2 if epi == EPI_SILU else N
+            o = torch.empty(c, n_out, dtype=torch.bfloat16)
+            _ref(wt[e], xs, epi, norm, o, eps)
+            if row_w is not None:
+                o = (o.float() * row_w[slots][:, None]).to(torch.bfloat16)
+            out[slots] = o
+        return out
+    L = _lib.lib()
+    w_stride = wt[0].numel() // 8  # in bf16x8 units
+    _lib.check(L.p2p_grouped_gemm(wt.data_ptr(), w_stride, E, cnt.data_ptr(), rows.data_ptr(),
+                                  rows.stride(0), x_div, _lib.ptr(row_w), x.data_ptr(), x.stride(0),
+                                  max_rows, K, N, epi, int(norm), out.data_ptr(), out.stride(0),
+                                  float(eps), 0, _lib.stream_ptr(x.device)), "grouped_gemm")
+    return out
+
+
+def moe_combine(o, topk_ids, R, K, e_lo, e_local, out, accumulate=True):
+    """accumulate: out[r] += sum_k o[r*K+k] (local experts only); else out[r] = the sum."""
+    H = out.shape[1]
+    if o.device.type != "cpu":
+        L = _lib.lib()
+        _lib.check(L.p2p_moe_combine(o.data_ptr(), o.stride(0), topk_ids.data_ptr(), R, K, e_lo,
+                                     e_local, H, out.data_ptr(), out.stride(0), int(accumulate),
+                                     _lib.stream_ptr(o.device)), "moe_combine")
+        return out
+    ids = topk_ids[:R * K].view(R, K).long() - e_lo
+    mask = ((ids >= 0) & (ids < e_local)).float()
+    s = (o[:R * K].float().view(R, K, H) * mask[..., None]).sum(1)
+    if accumulate:
+        out[:R] = (out[:R].float() + s).to(out.dtype)
+    else:
+        out[:R] = s.to(out.dtype)
+    return out

@@ -1,0 +1,84 @@
+"""Collectives for tensor / expert parallelism over ``torch.distributed``.
+
+On ROCm the ``nccl`` backend *is* RCCL, which rides xGMI between the GPUs of a
+node; on CPU the same code runs over ``gloo`` (used by the multi-process CPU
+tests).  One process per GPU; every collective is issued on the current
+stream so it is captured into the decode hipGraph together with the kernels.
+
+Decode-size messages are tiny (B x 8192 bf16 = 16 KiB per all-reduce for 70B
+at batch 1), i.e. latency-bound: 2 all-reduces per layer plus one 64-bit MAX
+all-reduce of the greedy argmax keys per step.  Greedy sampling never gathers
+vocab-parallel logits: each rank reduces its vocab shard to (value, token) keys
+in the LM-head epilogue and one MAX all-reduce picks the global argmax.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+_SIGN = -(2 ** 63)
+
+
+class TPComm:
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    # row-parallel outputs: h += sum_r partial_r
+    def allreduce_add_(self, h: torch.Tensor, partial: torch.Tensor):
+        if h.device.type == "cpu":
+            buf = partial.float()
+            dist.all_reduce(buf, group=self.group)
+            h.copy_((h.float() + buf).to(h.dtype))
+            return h
+        dist.all_reduce(partial, group=self.group)
+        h.add_(partial)
+        return h
+
+    def allreduce_(self, t: torch.Tensor):
+        dist.all_reduce(t, group=self.group)
+        return t
+
+    def allreduce_max_u64_(self, keys: torch.Tensor):
+        """MAX all-reduce of unsigned 64-bit argmax keys stored in int64."""
+        keys.bitwise_xor_(_SIGN)  # unsigned order -> signed order
+        dist.all_reduce(keys, op=dist.ReduceOp.MAX, group=self.group)
+        keys.bitwise_xor_(_SIGN)
+        return keys
+
+    def vocab_parallel_argmax(self, logits: torch.Tensor, out: torch.Tensor, v_local: int):
+        v, i = logits.max(-1)
+        g = i.to(torch.int64) + self.rank * v_local
+        vals = [torch.empty_like(v) for _ in range(self.world)]
+        idxs = [torch.empty_like(g) for _ in range(self.world)]
+        dist.all_gather(vals, v, group=self.group)
+        dist.all_gather(idxs, g, group=self.group)
+        V = torch.stack(vals, 0)
+        I = torch.stack(idxs, 0)
+        best = V.argmax(0)
+        out.copy_(I.gather(0, best[None])[0].to(out.dtype))
+        return out
+
+    def all_gather_rows(self, t: torch.Tensor):
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t, group=self.group)
+        return torch.cat(parts, 0)
+
+
+def init_distributed(backend: str | None = None):
+    """Init from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); returns (rank, world, local)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local

@@ -107,3 +107,18 @@ def test_llama8b_two_layers_gpu():
     _check_prefill_logits(eng, sd, cfg, prompts)
     r = eng.generate(prompts, 4, stop_on_eos=False)[0]
     _greedy_ok(sd, cfg, prompts[0], r.tokens)
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_tiny_mixtral(dev):
+    from p2p_llm_chat_go_amd.models import TINY_MIXTRAL
+
+    cfg = TINY_MIXTRAL
+    sd = random_state_dict(cfg, seed=5)
+    w = EngineWeights.from_state_dict(sd, cfg, dev)
+    eng = Engine(cfg, weights=w, device=dev, kv_pages=64, max_prefill_tokens=100, max_batch=4)
+    prompts = [[1, 5, 9, 33, 100, 7], list(range(3, 90)), [4]]
+    _check_prefill_logits(eng, sd, cfg, prompts)
+    res = eng.generate(prompts, max_new_tokens=6, stop_on_eos=False)
+    for p, r in zip(prompts, res):
+        _greedy_ok(sd, cfg, p, r.tokens)

@@ -240,3 +240,36 @@ def test_lm_head_argmax(M, offset):
     ic = torch.zeros(M, dtype=torch.int32)
     ops.argmax_finalize(kc, ic)
     assert ic.long().tolist() == ref.tolist()
+
+
+# ------------------------------------------------------------ MoE
+@pytest.mark.parametrize("R,E,K,e_lo,e_local", [(1, 8, 2, 0, 8), (13, 8, 2, 0, 8), (64, 8, 2, 4, 4)])
+def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
+    from p2p_llm_chat_go_amd.ops import moe as M
+
+    torch.manual_seed(R + E)
+    H, F = 512, 256
+    logits = torch.randn(R, 16)
+    w13 = torch.stack([ops.tile_weight((torch.randn(2 * F, H) * 0.05).to(torch.bfloat16))
+                       for _ in range(e_local)])
+    w2 = torch.stack([ops.tile_weight((torch.randn(H, F) * 0.05).to(torch.bfloat16))
+                      for _ in range(e_local)])
+    h = torch.randn(R, H).to(torch.bfloat16)
+    outs = {}
+    for dev in ("cpu", DEV):
+        ids = torch.zeros(R * K, dtype=torch.int32, device=dev)
+        tw = torch.zeros(R * K, dtype=torch.float32, device=dev)
+        cnt = torch.zeros(e_local, dtype=torch.int32, device=dev)
+        rows = torch.zeros(e_local, R, dtype=torch.int32, device=dev)
+        M.moe_route(logits.to(dev), E, K, e_lo, e_local, ids, tw, cnt, rows)
+        act = torch.zeros(R * K, F, dtype=torch.bfloat16, device=dev)
+        o = torch.zeros(R * K, H, dtype=torch.bfloat16, device=dev)
+        M.grouped_gemm(w13.to(dev), cnt, rows, h.to(dev), K, R, ops.EPI_SILU, act, norm=True)
+        M.grouped_gemm(w2.to(dev), cnt, rows, act, 1, R, ops.EPI_STORE, o, row_w=tw)
+        hh = h.clone().to(dev)
+        M.moe_combine(o, ids, R, K, e_lo, e_local, hh, accumulate=True)
+        outs[dev] = (ids.cpu(), tw.cpu(), cnt.cpu(), hh.cpu())
+    a, b = outs["cpu"], outs[DEV]
+    assert torch.equal(a[0], b[0]) and torch.allclose(a[1], b[1], atol=1e-5)
+    assert torch.equal(a[2], b[2])
+    assert _rel(b[3] - h, a[3] - h) < 2e-2
