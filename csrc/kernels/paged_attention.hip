@@ -6,13 +6,11 @@
 // carries a block-table row (its sequence) and a context length; a query row
 // is either one decode token or one prefill token (causal: ctx = pos + 1).
 //
-// Grid: (chunk, kv_head, row); a chunk = 4 pages = 256 keys, one page per wave.
+// Grid: (chunk, kv_head, row); a chunk = 4 pages = 256 keys (16 waves x 16 keys).
 // GQA packing: all G = Hq / Hkv query heads of a kv head are scored against the
 // same K/V bytes in one pass (K/V read once per group, not once per q head).
-// Within a wave each lane scores one key (full 256-B K row), softmax partials
-// are wave-reduced, then each lane owns 2 of the 128 output dims for P.V.
-// The 4 waves are merged through LDS; with one chunk the block writes the
-// final bf16 output, otherwise fp32 partials (m, l, o) for the combine kernel.
+// With one chunk the block writes the final bf16 output, otherwise fp32
+// partials (m, l, o) for the combine kernel.
 #include "common.h"
 
 namespace {
@@ -21,8 +19,20 @@ constexpr int PAGE = 64;
 constexpr int HD = 128;
 constexpr int CHUNK = 4 * PAGE;
 
+// Block = 16 waves = one 256-key chunk of one (row, kv head); wave w owns keys
+// [16w, 16w+16).  QK: lane = (key t = lane>>2, quarter c = lane&3) holds 32 dims of
+// K row t (four 16-B loads) and dots them with the G query heads; the four
+// quarter partials meet by two xor-shuffles.  Softmax over the wave's 16 keys by
+// xor-shuffles over the key bits.  PV: the wave's V rows go to LDS (row stride 272 B:
+// conflict-free 16-B writes and 4-B column reads) and lane owns output dims
+// 2*lane, 2*lane+1 over the 16 keys.  The 16 wave partials (m, l, o) merge
+// through LDS.  Every global load of a wave is issued before any math, so the
+// kernel pays one memory latency; the serial per-lane work is 16 keys deep.
+constexpr int WAVES = 16;
+constexpr int KPW = CHUNK / WAVES;  // keys per wave = 16
+
 template <int G>
-__global__ __launch_bounds__(256) void paged_attn_kernel(
+__global__ __launch_bounds__(WAVES * 64) void paged_attn_kernel(
     const bf16* __restrict__ q, int ldq, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ bt, int bt_stride, const int* __restrict__ row_bt,
     const int* __restrict__ ctx_lens, int Hkv, float scale, int n_chunks, bf16* __restrict__ out,
@@ -31,34 +41,34 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   const int ctx = ctx_lens[r];
   if (c * CHUNK >= ctx) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int t = lane >> 2, quarter = lane & 3;
 
-  // V rows are transposed through LDS: row stride 136 bf16 (272 B) keeps both
-  // the per-lane 16-B row writes and the per-lane 4-B column reads conflict-free.
   constexpr int VS = HD + 8;
-  __shared__ float qs[G][HD];
-  __shared__ __attribute__((aligned(16))) bf16 vs[4][PAGE][VS];
-  __shared__ float ps[4][G][PAGE];
-  __shared__ float sm[4][G], sl[4][G];
-  __shared__ float so[4][G][HD];
+  __shared__ bf16x2 qs[G][HD / 2];
+  __shared__ __attribute__((aligned(16))) bf16 vs[WAVES][KPW][VS];
+  __shared__ float ps[WAVES][G][KPW];
+  __shared__ float sm[WAVES][G], sl[WAVES][G];
+  __shared__ float so[WAVES][G][HD];
 
-  const int pi = c * 4 + w;
-  const int n_valid = min(max(ctx - pi * PAGE, 0), PAGE);
+  const int key0 = c * CHUNK + w * KPW;  // first key of this wave
+  const int n_valid = min(max(ctx - key0, 0), KPW);
+  const bool mine = t < n_valid;
 
-  // 1) issue every global load of this wave up front (one memory latency):
-  //    lane t holds K row t and V row t of its page (16 x 16 B each).
-  bf16x8 kr[HD / 8], vr[HD / 8];
-  if (lane < n_valid) {
-    const int page = bt[(size_t)row_bt[r] * bt_stride + pi];
-    const size_t tile = ((size_t)page * Hkv + h) * PAGE * HD + (size_t)lane * HD;
-    const bf16x8* kp = reinterpret_cast<const bf16x8*>(kc + tile);
-    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vc + tile);
+  // 1) all global loads first: 32 dims (4 x 16 B) of K and V row `t` per lane
+  bf16x8 kr[4], vr[4];
+  if (mine) {
+    const int key = key0 + t;
+    const int page = bt[(size_t)row_bt[r] * bt_stride + key / PAGE];
+    const size_t off = (((size_t)page * Hkv + h) * PAGE + (key % PAGE)) * HD + quarter * 32;
+    const bf16x8* kp = reinterpret_cast<const bf16x8*>(kc + off);
+    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vc + off);
 #pragma unroll
-    for (int ch = 0; ch < HD / 8; ++ch) kr[ch] = kp[ch];
+    for (int i = 0; i < 4; ++i) kr[i] = kp[i];
 #pragma unroll
-    for (int ch = 0; ch < HD / 8; ++ch) vr[ch] = vp[ch];
+    for (int i = 0; i < 4; ++i) vr[i] = vp[i];
   }
-  const bf16* qrow = q + (size_t)r * ldq + (size_t)h * G * HD;
-  for (int i = tid; i < G * HD; i += 256) qs[i / HD][i % HD] = (float)qrow[i] * scale;
+  const bf16x2* qrow = reinterpret_cast<const bf16x2*>(q + (size_t)r * ldq + (size_t)h * G * HD);
+  for (int i = tid; i < G * HD / 2; i += WAVES * 64) qs[i / (HD / 2)][i % (HD / 2)] = qrow[i];
   __syncthreads();
 
   float o[G][2];
@@ -70,43 +80,54 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
     lg[g] = 0.f;
   }
   if (n_valid > 0) {
-    // 2) scores: lane t scores key t against the G query heads of this kv head.
+    // 2) scores
     float s[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) s[g] = 0.f;
-    if (lane < n_valid) {
+    if (mine) {
+      // bf16 dot2 (v_dot2_f32_bf16): K stays packed, 2 MACs per instruction
 #pragma unroll
-      for (int ch = 0; ch < HD / 8; ++ch) {
+      for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float kf = (float)kr[ch][j];
+        for (int j = 0; j < 4; ++j) {
+          const bf16x2 k2 = {kr[i][2 * j], kr[i][2 * j + 1]};
+          const int d2 = quarter * 16 + i * 4 + j;
 #pragma unroll
-          for (int g = 0; g < G; ++g) s[g] = fmaf(qs[g][ch * 8 + j], kf, s[g]);
+          for (int g = 0; g < G; ++g) s[g] = __builtin_amdgcn_fdot2_f32_bf16(qs[g][d2], k2, s[g], false);
         }
       }
-      bf16x8* vrow = reinterpret_cast<bf16x8*>(&vs[w][lane][0]);
 #pragma unroll
-      for (int ch = 0; ch < HD / 8; ++ch) vrow[ch] = vr[ch];
+      for (int g = 0; g < G; ++g) s[g] *= scale;
+      bf16x8* vrow = reinterpret_cast<bf16x8*>(&vs[w][t][quarter * 32]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) vrow[i] = vr[i];
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float sv = lane < n_valid ? s[g] : -INFINITY;
-      mg[g] = wave_max(sv);
-      const float p = lane < n_valid ? __expf(sv - mg[g]) : 0.f;
-      lg[g] = wave_sum(p);
-      ps[w][g][lane] = p;
+      s[g] += __shfl_xor(s[g], 1, 64);
+      s[g] += __shfl_xor(s[g], 2, 64);
+      float sv = mine ? s[g] : -INFINITY;
+      float m = sv;
+#pragma unroll
+      for (int o2 = 4; o2 < 64; o2 <<= 1) m = fmaxf(m, __shfl_xor(m, o2, 64));
+      const float p = mine ? __expf(sv - m) : 0.f;
+      float l = p;
+#pragma unroll
+      for (int o2 = 4; o2 < 64; o2 <<= 1) l += __shfl_xor(l, o2, 64);
+      mg[g] = m;
+      lg[g] = l;  // the xor-4..32 sum runs over one lane per key (same quarter)
+      if (quarter == 0) ps[w][g][t] = p;
     }
-    // 3) P.V from the wave's own LDS rows (same-wave LDS ops stay in order):
-    //    lane owns output dims 2*lane, 2*lane+1.
+    // 3) P.V over the wave's keys (same-wave LDS ops stay in order)
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
 #pragma unroll 4
-    for (int t = 0; t < n_valid; ++t) {
-      const bf16x2 vv = *reinterpret_cast<const bf16x2*>(&vs[w][t][2 * lane]);
+    for (int k = 0; k < n_valid; ++k) {
+      const bf16x2 vv = *reinterpret_cast<const bf16x2*>(&vs[w][k][2 * lane]);
       const float v0 = (float)vv[0], v1 = (float)vv[1];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const float p = ps[w][g][t];
+        const float p = ps[w][g][k];
         o[g][0] = fmaf(p, v0, o[g][0]);
         o[g][1] = fmaf(p, v1, o[g][1]);
       }
@@ -123,15 +144,15 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   }
   __syncthreads();
   const int Hq = Hkv * G;
-  for (int i = tid; i < G * HD; i += 256) {
+  for (int i = tid; i < G * HD; i += WAVES * 64) {
     const int g = i / HD, d = i % HD;
     float M = -INFINITY;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm[ww][g]);
+    for (int ww = 0; ww < WAVES; ++ww) M = fmaxf(M, sm[ww][g]);
     float num = 0.f, den = 0.f;
     if (M != -INFINITY) {
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) {
+      for (int ww = 0; ww < WAVES; ++ww) {
         const float e = __expf(sm[ww][g] - M);
         num = fmaf(e, so[ww][g][d], num);
         den = fmaf(e, sl[ww][g], den);
@@ -176,7 +197,7 @@ template <int G>
 int launch_attn(const void* q, int ldq, const void* kc, const void* vc, const int* bt,
                 int bt_stride, const int* row_bt, const int* ctx, int R, int Hkv, float scale,
                 int n_chunks, void* out, int ldo, float* part_o, float* part_ml, hipStream_t st) {
-  hipLaunchKernelGGL((paged_attn_kernel<G>), dim3(n_chunks, Hkv, R), dim3(256), 0, st,
+  hipLaunchKernelGGL((paged_attn_kernel<G>), dim3(n_chunks, Hkv, R), dim3(WAVES * 64), 0, st,
                      (const bf16*)q, ldq, (const bf16*)kc, (const bf16*)vc, bt, bt_stride, row_bt,
                      ctx, Hkv, scale, n_chunks, (bf16*)out, ldo, part_o, part_ml);
   int e = (int)hipGetLastError();

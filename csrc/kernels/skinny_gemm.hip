@@ -66,6 +66,7 @@ struct EpiArgs {
   const float* row_w;
   long long w_stride;
   int n_experts;
+  int u;  // requested pipeline depth (0 = default)
 };
 
 __device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) {
@@ -78,25 +79,25 @@ __device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) 
 // all 64 lanes of the epilogue wave (the QKV/ARGMAX epilogues shuffle).
 template <int EPI>
 __device__ __forceinline__ void epi_store(int m, bool valid, int g, int r, float v, float u,
-                                          void* __restrict__ out, int ldo, const EpiArgs& ea) {
+                                          void* __restrict__ out, int ldo, const EpiArgs& ea,
+                                          float2 c = float2{1.f, 0.f}, int slot = -1) {
   if constexpr (EPI == EPI_QKV_ROPE) {
+    // c (cos, sin) and slot were prefetched before the main loop (rope_prefetch)
     const float vp = __shfl_xor(v, 8, 64);
     if (!valid) return;
-    const int head = g >> 3, k = g & 7;
+    const int head = g >> 3;
+    const int k = g & 7;
     const int d = (r < 8) ? 8 * k + r : 64 + 8 * k + (r - 8);
     if (head < ea.Hq + ea.Hkv) {
-      const float2 c = ea.cs[(size_t)ea.pos[m] * 64 + (d & 63)];
       const float y = (r < 8) ? (v * c.x - vp * c.y) : (v * c.x + vp * c.y);
       if (head < ea.Hq) {
         ea.q_out[(size_t)m * ea.ldq + (size_t)head * HD + d] = f2bf(y);
       } else {
-        const int slot = ea.slots[m];
         if (slot >= 0)
           ea.kc[(((size_t)(slot / PAGE) * ea.Hkv + (head - ea.Hq)) * PAGE + slot % PAGE) * HD + d] =
               f2bf(y);
       }
     } else {
-      const int slot = ea.slots[m];
       if (slot >= 0)
         ea.vc[(((size_t)(slot / PAGE) * ea.Hkv + (head - ea.Hq - ea.Hkv)) * PAGE + slot % PAGE) *
                   HD + d] = f2bf(v);
@@ -163,6 +164,26 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     int xrow = xv[mt] ? row : 0;
     if constexpr (MOE) xrow = xv[mt] ? mrows[row] / ea.x_div : 0;
     xp[mt] = X + (size_t)xrow * ldx + 8 * q;
+  }
+
+  // EPI_QKV_ROPE: fetch (cos, sin) and the KV slot of this lane's output rows now,
+  // so the epilogue's dependent pos -> table loads overlap the weight stream.
+  float2 rc[MT][4];
+  int rslot[MT][4];
+  if constexpr (EPI == EPI_QKV_ROPE) {
+    const int kk = g & 7;
+    const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int m = mt * 16 + q * 4 + j;
+        int mm = m;
+        if constexpr (MOE) mm = 0;
+        const bool ok = m < M && w == 0;
+        rslot[mt][j] = ok ? ea.slots[mm] : -1;
+        rc[mt][j] = ok ? ea.cs[(size_t)ea.pos[mm] * 64 + dd] : float2{1.f, 0.f};
+      }
   }
 
   f32x4 acc[NB][MT];
@@ -303,8 +324,12 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           orow = m < M ? mrows[m] : 0;
           if (ea.row_w && m < M) scale *= ea.row_w[orow];
         }
-        epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out,
-                       ldo, ea);
+        if constexpr (EPI == EPI_QKV_ROPE)
+          epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, 0.f, out, ldo, ea, rc[mt][j],
+                         rslot[mt][j]);
+        else
+          epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out,
+                         ldo, ea);
       }
     }
   } else {
@@ -324,17 +349,36 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           orow = m < M ? mrows[m] : 0;
           if (ea.row_w && m < M) scale *= ea.row_w[orow];
         }
-        epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out,
-                       ldo, ea);
+        if constexpr (EPI == EPI_QKV_ROPE)
+          epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, 0.f, out, ldo, ea, rc[mt][j],
+                         rslot[mt][j]);
+        else
+          epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out,
+                         ldo, ea);
       }
     }
   }
 }
 
+// k-steps per pipeline batch for MT=1 (tunable: p2p_skinny_gemm_tune); MT>1 uses 4.
+static int g_u_mt1 = 4;
+
+template <int MT, int WAVES, int EPI, bool NORM, int U>
+int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
+               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st);
+
 template <int MT, int WAVES, int EPI, bool NORM>
 int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
-  constexpr int U = (MT == 1) ? 8 : 4;
+  const int u = ea.u ? ea.u : (MT == 1 ? g_u_mt1 : 4);
+  if (MT == 1 && u == 8)
+    return launch_mwu<MT, WAVES, EPI, NORM, 8>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+  return launch_mwu<MT, WAVES, EPI, NORM, 4>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+}
+
+template <int MT, int WAVES, int EPI, bool NORM, int U>
+int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
+               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   if (ea.moe_cnt) {
     if constexpr (EPI == EPI_SILU || EPI == EPI_STORE) {
       hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, true>),
@@ -375,12 +419,15 @@ int launch_e(int mt, int waves, const void* Wt, const void* X, int ldx, int M, i
 
 }  // namespace
 
-// Picks the split-K factor so that the launch has >= ~2048 waves in flight
-// (256 CUs x 4 SIMDs x 2) while every wave still streams >= 8 k-steps.
+// Picks the split-K factor: enough waves to keep ~8+ MB of weight loads in flight,
+// but every wave resident in the first dispatch round (256 CUs x 4 SIMDs x
+// g_resident waves/SIMD) and streaming >= 8 k-steps.
+static int g_resident = 4;
 static int pick_waves(int groups, int K, int mt) {
   const int S = K / 32;
+  const int cap = 1024 * g_resident;
   int waves = 1;
-  while (waves < 8 && groups * waves < 2048 && S / (waves * 2) >= 8) waves *= 2;
+  while (waves < 8 && groups * waves * 2 <= cap && S / (waves * 2) >= 8) waves *= 2;
   // LDS budget for the reduction buffer at the largest tile (SiLU, MT=4): keep <= 64 KiB.
   (void)mt;
   return waves;
@@ -402,29 +449,41 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
     groups = N / 32;
     up_off = groups;
   }
+  // waves: low 8 bits = split-K waves (0 = heuristic), bits 8..15 = pipeline depth U (0 = default)
+  const int u_req = (waves >> 8) & 0xff;
+  waves &= 0xff;
   if (waves <= 0) waves = pick_waves(groups, K, mt);
   if (epi == EPI_SILU && mt == 4 && waves > 4) waves = 4;
+  EpiArgs ea2 = ea;
+  ea2.u = u_req;
   switch (epi) {
     case EPI_STORE:
-      return norm ? launch_e<EPI_STORE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream)
-                  : launch_e<EPI_STORE, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      return norm ? launch_e<EPI_STORE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream)
+                  : launch_e<EPI_STORE, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream);
     case EPI_RESID:
       if (norm) return (int)hipErrorInvalidValue;
-      return launch_e<EPI_RESID, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      return launch_e<EPI_RESID, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream);
     case EPI_SILU:
       if (!norm) return (int)hipErrorInvalidValue;
-      return launch_e<EPI_SILU, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      return launch_e<EPI_SILU, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream);
     case EPI_F32:
-      return norm ? launch_e<EPI_F32, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream)
-                  : launch_e<EPI_F32, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      return norm ? launch_e<EPI_F32, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream)
+                  : launch_e<EPI_F32, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream);
     case EPI_QKV_ROPE:
       if (!norm) return (int)hipErrorInvalidValue;
-      return launch_e<EPI_QKV_ROPE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      return launch_e<EPI_QKV_ROPE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream);
     case EPI_ARGMAX:
       if (!norm) return (int)hipErrorInvalidValue;
-      return launch_e<EPI_ARGMAX, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      return launch_e<EPI_ARGMAX, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream);
   }
   return (int)hipErrorInvalidValue;
+}
+
+// Tuning knobs (benchmarks): u_mt1 = k-steps per pipeline batch at M<=16 (4|8);
+// resident = waves/SIMD assumed resident when picking the split-K factor.
+P2P_API void p2p_skinny_gemm_tune(int u_mt1, int resident) {
+  if (u_mt1 == 4 || u_mt1 == 8) g_u_mt1 = u_mt1;
+  if (resident >= 1 && resident <= 8) g_resident = resident;
 }
 
 P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,

@@ -1,0 +1,99 @@
+"""Launch-configuration autotuning of the skinny MFMA GEMMs for one model.
+
+For every projection of the model (qkv+RoPE, o, gate_up+SiLU, down, LM head
+argmax) and every M tile the engine will use, each legal (pipeline depth U,
+split-K waves) pair is timed as a hipGraph that runs the projection of every
+layer once (cold weights, like the real decode step) and the fastest launch
+code is installed in ``ops.gemm._TUNE``.  Measured on MI355X the spread between
+configurations is up to ~2x at M=1 (e.g. down_proj 18.7 vs 42.9 us), and the
+best choice differs per shape, so a fixed heuristic leaves time on the table.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..ops import gemm as G
+
+
+def _graph_time(fn, reps=3):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = float("inf")
+    for _ in range(reps):
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    del g
+    return best
+
+
+def _configs(K):
+    out = []
+    for u in (4, 8):
+        for w in (1, 2, 4, 8):
+            if (K // 32) // w >= 8:
+                out.append(w | (u << 8))
+    return out
+
+
+def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
+    if model.device.type != "cuda":
+        return {}
+    cfg, w = model.cfg, model.w
+    dev = model.device
+    H = cfg.hidden
+    nq, nkv = model.nq, model.nkv
+    kc, vc = model.kv.layer(0)
+    result = {}
+    layers = w.layers
+    for M in sorted(set(min(b, G.SKINNY_MAX_M) for b in batch_sizes)):
+        x = torch.randn(M, H, device=dev).to(torch.bfloat16)
+        h = torch.zeros(M, H, device=dev, dtype=torch.bfloat16)
+        q = torch.zeros(M, nq * 128, device=dev, dtype=torch.bfloat16)
+        pos = torch.zeros(M, device=dev, dtype=torch.int32)
+        slots = torch.arange(M, device=dev, dtype=torch.int32) % 64  # null page 0
+        keys = ops.new_argmax_keys(M, dev)
+        jobs = [("qkv_rope", [lw.qkv for lw in layers], G.EPI_QKV_ROPE,
+                 lambda wt, c: ops.qkv_rope_gemm(wt, x, pos, slots, model.rope, nq, nkv, q, kc, vc,
+                                                 waves=c)),
+                ("o_proj", [lw.o for lw in layers], G.EPI_RESID,
+                 lambda wt, c: ops.skinny_gemm(wt, q, ops.EPI_RESID, out=h, waves=c))]
+        if not cfg.is_moe:
+            F = layers[0].gate_up.shape[0] * 16 // 2
+            act = torch.zeros(M, F, device=dev, dtype=torch.bfloat16)
+            xf = torch.randn(M, F, device=dev).to(torch.bfloat16)
+            jobs += [("gate_up", [lw.gate_up for lw in layers], G.EPI_SILU,
+                      lambda wt, c: ops.skinny_gemm(wt, x, ops.EPI_SILU, norm=True, out=act,
+                                                    waves=c)),
+                     ("down", [lw.down for lw in layers], G.EPI_RESID,
+                      lambda wt, c: ops.skinny_gemm(wt, xf, ops.EPI_RESID, out=h, waves=c))]
+        jobs.append(("lm_head", [w.lm_head], G.EPI_ARGMAX,
+                     lambda wt, c: ops.lm_head_argmax(wt, x, keys, waves=c)))
+        for name, wts, epi, fn in jobs:
+            K = G.tiled_shape(wts[0])[1]
+            times = {}
+            for code in _configs(K):
+                times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
+            best = min(times, key=times.get)
+            norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)
+            G.set_tune(G.tune_key(wts[0], M, epi, norm), best)
+            result[(name, M)] = (best & 0xff, best >> 8, times[best] * 1000 / len(wts))
+            if verbose:
+                print("autotune %-9s M=%-2d waves=%d U=%d  %.2f us" % (
+                    name, M, best & 0xff, best >> 8, times[best] * 1000 / len(wts)), flush=True)
+        keys.zero_()
+    torch.cuda.synchronize()
+    return result

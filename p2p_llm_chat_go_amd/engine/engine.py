@@ -17,6 +17,7 @@ the execution backend it drives (``prefill`` / ``decode_graph``).
 from __future__ import annotations
 
 import dataclasses
+import os
 import time
 
 import torch
@@ -96,7 +97,17 @@ class Engine:
             self._graphs[key] = g
         return g
 
-    def warmup(self, batch_sizes=(1,), ctx=256):
+    def autotune(self, batch_sizes=(1,), verbose=False):
+        """Pick the fastest GEMM launch configs for this model (before graph capture)."""
+        from .autotune import autotune_model
+
+        if self.device.type == "cuda" and os.environ.get("P2P_AUTOTUNE", "1") != "0":
+            self.tuning = autotune_model(self.model, batch_sizes, verbose=verbose)
+        return getattr(self, "tuning", {})
+
+    def warmup(self, batch_sizes=(1,), ctx=256, autotune=True):
+        if autotune and not getattr(self, "tuning", None):
+            self.autotune(tuple(bucket(b, BATCH_BUCKETS) for b in batch_sizes))
         for b in batch_sizes:
             self.decode_graph(b, ctx)
 

@@ -79,6 +79,10 @@ def lib():
                 "HIP kernel library missing at %s -- run `python -m p2p_llm_chat_go_amd._build` "
                 "(or __graft_entry__.build())" % _LIB_PATH)
         L = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        fn = getattr(L, "p2p_skinny_gemm_tune", None)
+        if fn is not None:
+            fn.argtypes = [c_int, c_int]
+            fn.restype = None
         for name, args in _SIGS.items():
             fn = getattr(L, name, None)
             if fn is None:

@@ -17,7 +17,30 @@ import torch
 from . import _lib
 
 EPI_STORE, EPI_RESID, EPI_SILU, EPI_F32 = 0, 1, 2, 3
+EPI_QKV_ROPE, EPI_ARGMAX = 4, 5
 SKINNY_MAX_M = 64
+
+# Autotuned launch codes: (N, K, epi, norm, m_tile) -> waves | (U << 8)  (engine/autotune.py)
+_TUNE: dict = {}
+
+
+def m_tile(M: int) -> int:
+    return 1 if M <= 16 else (2 if M <= 32 else 4)
+
+
+def tune_key(wt, M, epi, norm):
+    N, K = tiled_shape(wt)
+    return (N, K, int(epi), bool(norm), m_tile(min(M, SKINNY_MAX_M)))
+
+
+def set_tune(key, code: int):
+    _TUNE[key] = int(code)
+
+
+def _code(wt, M, epi, norm, waves):
+    if waves:
+        return waves
+    return _TUNE.get(tune_key(wt, M, epi, norm), 0)
 
 
 def tile_weight(w: torch.Tensor) -> torch.Tensor:
@@ -88,8 +111,8 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
         xs = x[m0:m0 + mc]
         os_ = out[m0:m0 + mc]
         _lib.check(L.p2p_skinny_gemm(wt.data_ptr(), xs.data_ptr(), x.stride(0), mc, K, N, epi,
-                                     int(norm), os_.data_ptr(), out.stride(0), float(eps), waves, s),
-                   "skinny_gemm")
+                                     int(norm), os_.data_ptr(), out.stride(0), float(eps),
+                                     _code(wt, mc, epi, norm, waves), s), "skinny_gemm")
     return out
 
 
@@ -130,8 +153,8 @@ def qkv_rope_gemm(wt, x, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_c
         _lib.check(L.p2p_skinny_gemm_qkv_rope(
             wt.data_ptr(), x[m0:].data_ptr(), x.stride(0), mc, K, n_heads, n_kv,
             pos[m0:].data_ptr(), slots[m0:].data_ptr(), cos_sin.data_ptr(), q_out[m0:].data_ptr(),
-            q_out.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), float(eps), waves, s),
-            "skinny_gemm_qkv_rope")
+            q_out.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), float(eps),
+            _code(wt, mc, EPI_QKV_ROPE, True, waves), s), "skinny_gemm_qkv_rope")
     return q_out
 
 
@@ -164,7 +187,8 @@ def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: i
         return keys
     L = _lib.lib()
     _lib.check(L.p2p_skinny_gemm_argmax(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N,
-                                        keys.data_ptr(), int(col_offset), float(eps), waves,
+                                        keys.data_ptr(), int(col_offset), float(eps),
+                                        _code(wt, M, EPI_ARGMAX, True, waves),
                                         _lib.stream_ptr(x.device)), "skinny_gemm_argmax")
     return keys
 
