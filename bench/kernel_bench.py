@@ -53,6 +53,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, nargs="*", default=[1, 8])
     ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--prefill", type=int, nargs="*", default=[512, 2048])
     a = ap.parse_args()
     cfg = LLAMA31_8B
     H, F, V = cfg.hidden, cfg.ffn, cfg.vocab
@@ -61,6 +62,7 @@ def main():
     P = 64
     kc = torch.randn(P, nkv, 64, 128, device="cuda").to(torch.bfloat16)
     vc = torch.randn_like(kc)
+    prefill_bench(a.prefill)
     for M in a.M:
         x = torch.randn(M, H, device="cuda").to(torch.bfloat16)
         xf = torch.randn(M, F, device="cuda").to(torch.bfloat16)
@@ -117,6 +119,34 @@ def main():
         print(json.dumps({"M": M, "layer_us_ctx100": round(layer, 2),
                           "est_step_ms": round((32 * layer + d["lm_head_argmax"]) / 1000, 3)}),
               flush=True)
+
+
+def prefill_bench(Ms):
+    """Tiled MFMA GEMMs at prefill M (compute-bound): TFLOP/s per projection."""
+    cfg = LLAMA31_8B
+    H, F = cfg.hidden, cfg.ffn
+    for M in Ms:
+        x = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+        xf = torch.randn(M, F, device="cuda").to(torch.bfloat16)
+        h = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+        act = torch.zeros(M, F, device="cuda", dtype=torch.bfloat16)
+        o = torch.zeros(M, 6144, device="cuda", dtype=torch.bfloat16)
+        for name, N, K, fn in [
+            ("qkv", 6144, H, lambda W: ops.skinny_gemm(W, x, ops.EPI_STORE, norm=True, out=o)),
+            ("gate_up", 2 * F, H, lambda W: ops.skinny_gemm(W, x, ops.EPI_SILU, norm=True, out=act)),
+            ("down", H, F, lambda W: ops.skinny_gemm(W, xf, ops.EPI_RESID, out=h))]:
+            W = copies(N, K, nbytes_target=0)
+            t = graph_time(lambda i: fn(W[0]), n_inner=10)
+            torch_t = graph_time(lambda i: torch.matmul(x if K == H else xf,
+                                                        torch.empty(K, N, device="cuda",
+                                                                    dtype=torch.bfloat16)),
+                                 n_inner=10) if False else None
+            print(json.dumps({"prefill_M": M, "gemm": name, "us": round(t, 1),
+                              "TFLOPs": round(2 * M * N * K / (t * 1e-6) / 1e12, 1)}), flush=True)
+        Wb = torch.randn(H, 2 * F, device="cuda").to(torch.bfloat16)
+        t = graph_time(lambda i: torch.matmul(x, Wb), n_inner=10)
+        print(json.dumps({"prefill_M": M, "gemm": "hipblaslt_gate_up_reference", "us": round(t, 1),
+                          "TFLOPs": round(2 * M * 2 * F * H / (t * 1e-6) / 1e12, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -40,9 +40,9 @@ def _graph_time(fn, reps=3):
     return best
 
 
-def _configs(K):
+def _configs(K, M=1):
     out = []
-    for u in (4, 8):
+    for u in ((4, 8) if M <= 16 else (2, 4)):
         for w in (1, 2, 4, 8):
             if (K // 32) // w >= 8:
                 out.append(w | (u << 8))
@@ -85,7 +85,7 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
         for name, wts, epi, fn in jobs:
             K = G.tiled_shape(wts[0])[1]
             times = {}
-            for code in _configs(K):
+            for code in _configs(K, M):
                 times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
             best = min(times, key=times.get)
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)

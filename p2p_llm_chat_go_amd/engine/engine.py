@@ -107,7 +107,8 @@ class Engine:
 
     def warmup(self, batch_sizes=(1,), ctx=256, autotune=True):
         if autotune and not getattr(self, "tuning", None):
-            self.autotune(tuple(bucket(b, BATCH_BUCKETS) for b in batch_sizes))
+            # decode buckets + the prefill tile (prompt chunks run at M <= 64 rows per call)
+            self.autotune(tuple(bucket(b, BATCH_BUCKETS) for b in batch_sizes) + (64,))
         for b in batch_sizes:
             self.decode_graph(b, ctx)
 

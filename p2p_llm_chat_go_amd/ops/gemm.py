@@ -37,6 +37,13 @@ def set_tune(key, code: int):
     _TUNE[key] = int(code)
 
 
+def use_tiled(M, N, K, epi) -> bool:
+    """Prefill-sized M goes to the LDS-tiled MFMA kernel (compute-bound), decode to skinny."""
+    if M <= SKINNY_MAX_M or K % 64:
+        return False
+    return (N // 2) % 64 == 0 if epi == EPI_SILU else N % 128 == 0
+
+
 def _code(wt, M, epi, norm, waves):
     if waves:
         return waves
@@ -106,6 +113,11 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
     assert x.stride(1) == 1 and out.stride(1) == 1
     L = _lib.lib()
     s = _lib.stream_ptr(x.device)
+    if use_tiled(M, N, K, epi):
+        _lib.check(L.p2p_tiled_gemm(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N, epi,
+                                    int(norm), out.data_ptr(), out.stride(0), float(eps), s),
+                   "tiled_gemm")
+        return out
     for m0 in range(0, M, SKINNY_MAX_M):
         mc = min(SKINNY_MAX_M, M - m0)
         xs = x[m0:m0 + mc]
@@ -148,6 +160,12 @@ def qkv_rope_gemm(wt, x, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_c
         return rope_cache_ref(qkv, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_cache)
     L = _lib.lib()
     s = _lib.stream_ptr(x.device)
+    if use_tiled(M, N, K, EPI_QKV_ROPE):
+        _lib.check(L.p2p_tiled_gemm_qkv_rope(
+            wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, n_heads, n_kv, pos.data_ptr(),
+            slots.data_ptr(), cos_sin.data_ptr(), q_out.data_ptr(), q_out.stride(0),
+            k_cache.data_ptr(), v_cache.data_ptr(), float(eps), s), "tiled_gemm_qkv_rope")
+        return q_out
     for m0 in range(0, M, SKINNY_MAX_M):
         mc = min(SKINNY_MAX_M, M - m0)
         _lib.check(L.p2p_skinny_gemm_qkv_rope(
@@ -186,6 +204,11 @@ def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: i
         keys[:M, 0] = torch.where((k ^ sign) > (cur ^ sign), k, cur)
         return keys
     L = _lib.lib()
+    if use_tiled(M, N, K, EPI_ARGMAX):
+        _lib.check(L.p2p_tiled_gemm_argmax(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N,
+                                           keys.data_ptr(), int(col_offset), float(eps),
+                                           _lib.stream_ptr(x.device)), "tiled_gemm_argmax")
+        return keys
     _lib.check(L.p2p_skinny_gemm_argmax(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N,
                                         keys.data_ptr(), int(col_offset), float(eps),
                                         _code(wt, M, EPI_ARGMAX, True, waves),

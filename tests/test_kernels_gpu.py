@@ -273,3 +273,65 @@ def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
     assert torch.equal(a[0], b[0]) and torch.allclose(a[1], b[1], atol=1e-5)
     assert torch.equal(a[2], b[2])
     assert _rel(b[3] - h, a[3] - h) < 2e-2
+
+
+# ------------------------------------------------------------ tiled (prefill) GEMM
+@pytest.mark.parametrize("M", [65, 200, 513])
+@pytest.mark.parametrize("epi", ["store", "store_norm", "resid", "silu", "f32"])
+def test_tiled_gemm(M, epi):
+    torch.manual_seed(M)
+    K, N = 1024, 768
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    norm = epi in ("store_norm", "silu", "f32")
+    acc = x.float() @ W.float().t()
+    if norm:
+        acc = acc * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    Wt = ops.tile_weight(W).to(DEV)
+    if epi == "resid":
+        h = torch.randn(M, N).to(torch.bfloat16)
+        hd = h.to(DEV)
+        ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_RESID, out=hd)
+        assert _rel(hd.cpu(), h.float() + acc) < 1e-2
+        return
+    if epi == "silu":
+        out = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_SILU, norm=True)
+        ref = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
+    elif epi == "f32":
+        out = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_F32, norm=True)
+        assert out.dtype == torch.float32
+        ref = acc
+    else:
+        out = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_STORE, norm=norm)
+        ref = acc
+    assert _rel(out.cpu(), ref) < 1e-2
+
+
+def test_tiled_qkv_rope_and_argmax():
+    from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
+
+    torch.manual_seed(0)
+    M, Hq, Hkv, K = 150, 4, 2, 512
+    W = (torch.randn((Hq + 2 * Hkv) * 128, K) * 0.05).to(torch.bfloat16)
+    Wt = ops.tile_weight(W[ops.rope_row_perm(Hq + 2 * Hkv)])
+    x = torch.randn(M, K).to(torch.bfloat16)
+    cs = rope_table(LLAMA31_8B, max_pos=512)
+    pos = torch.arange(M, dtype=torch.int32)
+    slots = torch.randperm(4 * 64)[:M].to(torch.int32)
+    q_ref = torch.zeros(M, Hq * 128, dtype=torch.bfloat16)
+    kr = torch.zeros(4, Hkv, 64, 128, dtype=torch.bfloat16)
+    vr = torch.zeros_like(kr)
+    ops.qkv_rope_gemm(Wt, x, pos, slots, cs, Hq, Hkv, q_ref, kr, vr)  # CPU reference path
+    qd = torch.zeros_like(q_ref).to(DEV)
+    kd, vd = torch.zeros_like(kr).to(DEV), torch.zeros_like(vr).to(DEV)
+    ops.qkv_rope_gemm(Wt.to(DEV), x.to(DEV), pos.to(DEV), slots.to(DEV), cs.to(DEV), Hq, Hkv, qd,
+                      kd, vd)
+    assert _rel(qd.cpu(), q_ref) < 1e-2 and _rel(kd.cpu(), kr) < 1e-2 and _rel(vd.cpu(), vr) < 1e-2
+    V = 1024
+    Wl = (torch.randn(V, K) * 0.05).to(torch.bfloat16)
+    ref = (x.float() @ Wl.float().t()).argmax(-1)
+    keys = ops.new_argmax_keys(M, DEV)
+    ops.lm_head_argmax(ops.tile_weight(Wl).to(DEV), x.to(DEV), keys)
+    ids = torch.zeros(M, dtype=torch.int32, device=DEV)
+    ops.argmax_finalize(keys, ids)
+    assert (ids.cpu().long() == ref).float().mean() > 0.98  # bf16 near-ties may differ
