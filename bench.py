@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--peers", type=int, default=1, help="concurrent peers per GPU (batched decode)")
     ap.add_argument("--new-tokens", type=int, default=64)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree (ranks per engine replica, RCCL over xGMI)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -59,13 +61,23 @@ def main():
 
     cfg = get_config(a.model)
     tok = get_tokenizer(cfg)
+    tp = max(1, a.tp)
+    assert world % tp == 0, "world size must be a multiple of --tp"
+    replica, tp_rank = rank // tp, rank % tp
+    comm = None
+    if tp > 1:
+        from p2p_llm_chat_go_amd.parallel.comm import TPComm
+
+        groups = [dist.new_group(list(range(g * tp, (g + 1) * tp))) for g in range(world // tp)]
+        comm = TPComm(groups[replica])
     prompts = []
     for p in range(a.peers):
-        msg = SAMPLE_MESSAGES[(rank * a.peers + p) % len(SAMPLE_MESSAGES)]
+        msg = SAMPLE_MESSAGES[(replica * a.peers + p) % len(SAMPLE_MESSAGES)]
         prompts.append(tok.chat_ids(suggest_prompt(msg)))
     need_pages = sum((len(p) + a.new_tokens + 63) // 64 for p in prompts) + 8
-    eng = Engine(cfg, device=dev, seed=1234 + rank, kv_pages=max(need_pages, 64),
-                 max_prefill_tokens=1024, max_batch=max(a.peers, 1), use_graph=not a.no_graph)
+    eng = Engine(cfg, device=dev, seed=1234 + replica, kv_pages=max(need_pages, 64),
+                 max_prefill_tokens=1024, max_batch=max(a.peers, 1), use_graph=not a.no_graph,
+                 comm=comm, tp_rank=tp_rank, tp_size=tp)
     eng.warmup((a.peers,), ctx=max(len(p) for p in prompts) + a.new_tokens)
 
     for _ in range(a.warmup):
@@ -83,7 +95,8 @@ def main():
         res = eng.generate(prompts, a.new_tokens, stop_on_eos=False)
         for r in res:
             ttfts.append(r.ttft_ns / 1e6)
-            toks += r.eval_count
+            if tp_rank == 0:  # a TP group produces each token once
+                toks += r.eval_count
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -117,7 +130,9 @@ def main():
                     "random-init weights",
             "config": {"model": cfg.name, "global_batch": world * a.peers,
                        "seq_len": prompt_len + a.new_tokens, "prompt_tokens": prompt_len,
-                       "new_tokens": a.new_tokens, "parallelism": "dp%d" % world, "tp": 1,
+                       "new_tokens": a.new_tokens,
+                       "parallelism": ("dp%d" % (world // tp)) + ("-tp%d" % tp if tp > 1 else ""),
+                       "tp": tp,
                        "peers_per_gpu": a.peers, "hipgraph_decode": not a.no_graph},
             "ttft_p50_ms": round(statistics.median(all_ttft), 3),
             "ttft_p99_ms": round(sorted(all_ttft)[min(len(all_ttft) - 1,

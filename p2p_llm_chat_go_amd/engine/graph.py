@@ -116,8 +116,17 @@ class DecodeGraph:
         torch.cuda.synchronize(st.model.device)
         st.reset_dummy()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._body()
+        try:
+            with torch.cuda.graph(g):
+                self._body()
+        except Exception as e:  # e.g. a collective backend that cannot be captured
+            import warnings
+
+            warnings.warn("decode graph capture failed (%s); running the step eagerly" % e)
+            torch.cuda.synchronize(st.model.device)
+            st.reset_dummy()
+            self.graph = None
+            return self
         torch.cuda.synchronize(st.model.device)
         st.reset_dummy()
         self.graph = g

@@ -26,10 +26,12 @@ class TPComm:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
 
     # row-parallel outputs: h += sum_r partial_r
     def allreduce_add_(self, h: torch.Tensor, partial: torch.Tensor):
-        if h.device.type == "cpu":
+        if h.device.type == "cpu" or self.backend != "nccl":
+            # gloo (CPU tests, virtual ranks on one GPU): reduce in fp32
             buf = partial.float()
             dist.all_reduce(buf, group=self.group)
             h.copy_((h.float() + buf).to(h.dtype))

@@ -1,0 +1,65 @@
+"""Tensor / expert parallelism on the GPU kernels with *virtual ranks*: two
+processes share the one MI355X of the test box (SURVEY §4.2 tier (b)), their
+collectives run over gloo (RCCL refuses two ranks on one device), graphs off.
+Sharded engines must reproduce the unsharded engine's greedy tokens."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q, moe):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from p2p_llm_chat_go_amd.engine import Engine
+        from p2p_llm_chat_go_amd.models import TINY_LLAMA, TINY_MIXTRAL
+        from p2p_llm_chat_go_amd.models.reference import random_state_dict
+        from p2p_llm_chat_go_amd.models.weights import EngineWeights
+        from p2p_llm_chat_go_amd.parallel.comm import TPComm
+
+        base = TINY_MIXTRAL if moe else TINY_LLAMA
+        cfg = base.replace(n_heads=4, n_kv_heads=4, ffn=512 if not moe else 256)
+        sd = random_state_dict(cfg, seed=3)
+        prompts = [[1, 2, 3, 4, 5], list(range(10, 90))]
+        full = Engine(cfg, weights=EngineWeights.from_state_dict(sd, cfg, "cuda"), device="cuda",
+                      kv_pages=32, use_graph=False)
+        ref = [r.tokens for r in full.generate(prompts, 6, stop_on_eos=False)]
+        kw = dict(ep_rank=rank, ep_size=world) if moe else dict(tp_rank=rank, tp_size=world)
+        w = EngineWeights.from_state_dict(sd, cfg, "cuda", **kw)
+        eng = Engine(cfg, weights=w, device="cuda", kv_pages=32, comm=TPComm(),
+                     tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=False)
+        got = [r.tokens for r in eng.generate(prompts, 6, stop_on_eos=False)]
+        q.put((rank, got == ref, got, ref))
+    except Exception:
+        import traceback
+        q.put((rank, False, traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("moe", [False, True])
+def test_virtual_rank_parallel_gpu(moe):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    world = 2
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe)) for r in range(world)]
+    [p.start() for p in ps]
+    res = [q.get(timeout=600) for _ in range(world)]
+    [p.join(timeout=60) for p in ps]
+    for rank, ok, got, ref in res:
+        assert ok, (rank, got, ref)
