@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--M", type=int, nargs="*", default=[1, 8])
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--prefill", type=int, nargs="*", default=[512, 2048])
+    ap.add_argument("--attn-prefill", type=int, nargs="*", default=[64, 512, 2048, 8192])
     a = ap.parse_args()
     cfg = LLAMA31_8B
     H, F, V = cfg.hidden, cfg.ffn, cfg.vocab
@@ -62,6 +63,7 @@ def main():
     P = 64
     kc = torch.randn(P, nkv, 64, 128, device="cuda").to(torch.bfloat16)
     vc = torch.randn_like(kc)
+    prefill_attn_bench(a.attn_prefill)
     prefill_bench(a.prefill)
     for M in a.M:
         x = torch.randn(M, H, device="cuda").to(torch.bfloat16)
@@ -119,6 +121,33 @@ def main():
         print(json.dumps({"M": M, "layer_us_ctx100": round(layer, 2),
                           "est_step_ms": round((32 * layer + d["lm_head_argmax"]) / 1000, 3)}),
               flush=True)
+
+
+def prefill_attn_bench(Ts):
+    """Causal prefill attention, one sequence of T tokens (8B heads): MFMA flash
+    kernel vs the per-row paged kernel.  TFLOP/s counts the causal half."""
+    cfg = LLAMA31_8B
+    nq, nkv = cfg.n_heads, cfg.n_kv_heads
+    for T in Ts:
+        npg = (T + 63) // 64
+        kc = torch.randn(npg + 1, nkv, 64, 128, device="cuda").to(torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(1, npg + 1, device="cuda", dtype=torch.int32)[None]
+        q = torch.randn(T, nq * 128, device="cuda").to(torch.bfloat16)
+        out = torch.empty_like(q)
+        pos = list(range(T))
+        tiles = ops.prefill_tiles([0] * T, pos).to("cuda")
+        rb = torch.zeros(T, device="cuda", dtype=torch.int32)
+        ctx = torch.arange(1, T + 1, device="cuda", dtype=torch.int32)
+        ws = ops.attn_workspace(T, nq, T, "cuda")
+        flops = 2 * 2 * nq * 128 * T * (T + 1) / 2
+        tf = graph_time(lambda i: ops.flash_prefill(q, kc, vc, bt, tiles, nq, nkv, out=out),
+                        n_inner=10)
+        tr = graph_time(lambda i: ops.paged_attention(q, kc, vc, bt, rb, ctx, nq, nkv, T, out=out,
+                                                      workspace=ws), n_inner=10)
+        for name, t in (("flash_prefill", tf), ("per_row_paged", tr)):
+            print(json.dumps({"prefill_attn_T": T, "kernel": name, "us": round(t, 1),
+                              "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1)}), flush=True)
 
 
 def prefill_bench(Ms):

@@ -46,4 +46,13 @@ __device__ __forceinline__ bf16x8 load_nt(const bf16x8* p) {
   return __builtin_nontemporal_load(p);
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2).
+// Bijective remap so that logically consecutive blocks (which share operands)
+// land on the same XCD: physical blocks b and b+8 get logical ids i and i+1.
+__device__ __forceinline__ int xcd_remap(int b, int nblocks) {
+  const int q = nblocks / 8, r = nblocks % 8;
+  const int xcd = b % 8, idx = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 #define P2P_CHECK_LAUNCH() return (int)hipGetLastError()

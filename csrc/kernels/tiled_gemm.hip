@@ -23,13 +23,6 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int NT = 256;
 
-__device__ __forceinline__ int xcd_remap(int b, int nblocks) {
-  // bijective round-robin-to-contiguous remap (blocks b and b+8 share an XCD)
-  const int q = nblocks / 8, r = nblocks % 8;
-  const int xcd = b % 8, idx = b / 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
-
 template <int EPI, bool NORM>
 __global__ __launch_bounds__(NT) void tiled_gemm_kernel(const bf16x8* __restrict__ Wt,
                                                         const bf16* __restrict__ X, int ldx, int M,

@@ -25,6 +25,7 @@ import torch
 from ..models.config import ModelConfig
 from ..models.llama import LlamaModel
 from ..models.weights import EngineWeights
+from .. import ops
 from ..ops import PAGE
 from .graph import DecodeGraph, DecodeState
 from .kv_cache import KVCache, pages_for
@@ -70,6 +71,9 @@ class Engine:
             self.kv = KVCache(cfg, kv_pages, self.device, tp_size)
         self.model = LlamaModel(weights, self.kv, comm)
         self.max_prefill_tokens = max_prefill_tokens
+        # prefill chunks with at least this many rows use the MFMA flash kernel
+        # (0 = always the per-row paged kernel)
+        self.flash_prefill_min = int(os.environ.get("P2P_FLASH_PREFILL_MIN", "1"))
         self.max_batch = max_batch
         self.use_graph = use_graph
         self._prefill_ws = {}
@@ -154,8 +158,13 @@ class Engine:
             seq_d, pos_d, ids_d, slots_d, ctx_d = dev_t[0], dev_t[1], dev_t[2], dev_t[3], dev_t[4]
             out_rows = torch.tensor(outs or [0], dtype=torch.int32).to(dev, non_blocking=True)
             greedy = all_logits is None
+            tiles = tiles_h = None
+            if self.flash_prefill_min and R >= self.flash_prefill_min:
+                tiles_h = ops.prefill_tiles(seq.tolist(), pos.tolist())
+                tiles = tiles_h.to(dev, non_blocking=True)
             res = self.model.forward(ws, ids_d, pos_d, slots_d, bt_d, seq_d, ctx_d, R,
-                                     max_ctx, out_rows=out_rows, n_out=len(outs), greedy=greedy)
+                                     max_ctx, out_rows=out_rows, n_out=len(outs), greedy=greedy,
+                                     tiles=tiles, tiles_host=tiles_h)
             if not outs:
                 continue
             if greedy:

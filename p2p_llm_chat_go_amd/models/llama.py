@@ -92,13 +92,16 @@ class LlamaModel:
         self._row_parallel(lw.down, act, h, ws, R)
 
     def forward(self, ws: Workspace, ids, pos, slots, block_tables, row_bt, ctx_lens, R: int,
-                max_ctx: int, out_rows=None, n_out: int | None = None, greedy: bool = False):
+                max_ctx: int, out_rows=None, n_out: int | None = None, greedy: bool = False,
+                tiles=None, tiles_host=None):
         """Run all layers on R query rows.
 
         out_rows: int32 [n_out] indices of rows whose logits are needed (prefill:
         the last token of each sequence); None = all R rows (decode).
         Returns fp32 logits of the selected rows, or with greedy=True the int64
         argmax keys (ws.keys, see ops.lm_head_argmax).
+        tiles: int32 [n, 4] prefill query tiles (ops.prefill_tiles) -> causal
+        attention runs on the MFMA flash-prefill kernel instead of per row.
         """
         cfg = self.cfg
         h = ws.h[:R]
@@ -108,8 +111,12 @@ class LlamaModel:
             kc, vc = self.kv.layer(i)
             ops.qkv_rope_gemm(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc,
                               vc, eps=cfg.eps)
-            ops.paged_attention(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R], self.nq,
-                                self.nkv, max_ctx, out=attn, workspace=ws.attn_ws)
+            if tiles is not None:
+                ops.flash_prefill(q, kc, vc, block_tables, tiles, self.nq, self.nkv, out=attn,
+                                  tiles_host=tiles_host)
+            else:
+                ops.paged_attention(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R], self.nq,
+                                    self.nkv, max_ctx, out=attn, workspace=ws.attn_ws)
             self._row_parallel(lw.o, attn, h, ws, R)
             self._mlp(lw, ws, R)
         if n_out == 0:

@@ -36,6 +36,8 @@ _SIGS = {
     "p2p_paged_attention": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                             c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int,
                             c_void_p, c_void_p, c_void_p],
+    "p2p_flash_prefill": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                          c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
     "p2p_gather_rows": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
     "p2p_rope_cache": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_void_p, c_int, c_void_p, c_void_p, c_void_p],

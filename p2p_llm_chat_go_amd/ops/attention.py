@@ -80,6 +80,61 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return out
 
 
+QTILE = 16
+
+
+def prefill_tiles(seq, pos, tile: int = QTILE) -> torch.Tensor:
+    """Split flat prefill rows into query tiles for :func:`flash_prefill`.
+
+    ``seq``/``pos`` are host int sequences (one entry per row, rows of one
+    sequence consecutive with consecutive positions).  Returns int32 [n, 4] =
+    (first row, n tokens, sequence, first position).
+    """
+    seq = [int(s) for s in seq]
+    pos = [int(p) for p in pos]
+    out = []
+    r, R = 0, len(seq)
+    while r < R:
+        e = r + 1
+        while e < R and e - r < tile and seq[e] == seq[r] and pos[e] == pos[e - 1] + 1:
+            e += 1
+        out.append((r, e - r, seq[r], pos[r]))
+        r = e
+    return torch.tensor(out, dtype=torch.int32).view(-1, 4)
+
+
+def flash_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                  block_tables: torch.Tensor, tiles: torch.Tensor, n_heads: int, n_kv: int,
+                  out: torch.Tensor | None = None, scale: float | None = None,
+                  tiles_host: torch.Tensor | None = None) -> torch.Tensor:
+    """Causal prefill attention on MFMA for query tiles (see ``prefill_tiles``).
+
+    Equivalent to :func:`paged_attention` with one row per prompt token
+    (ctx = pos + 1), but reads each K/V tile once per 16 tokens x G heads.
+    """
+    R = q.shape[0]
+    if scale is None:
+        scale = 1.0 / math.sqrt(HEAD_DIM)
+    if out is None:
+        out = torch.empty(R, n_heads * HEAD_DIM, device=q.device, dtype=q.dtype)
+    if q.device.type != "cuda":
+        th = (tiles_host if tiles_host is not None else tiles).cpu()
+        row_bt = torch.empty(R, dtype=torch.int32)
+        ctx = torch.empty(R, dtype=torch.int32)
+        for r0, n, s, p0 in th.tolist():
+            row_bt[r0:r0 + n] = s
+            ctx[r0:r0 + n] = torch.arange(p0 + 1, p0 + n + 1, dtype=torch.int32)
+        return paged_attention_ref(q, k_cache, v_cache, block_tables, row_bt, ctx, n_heads, n_kv,
+                                   scale, out)
+    L = _lib.lib()
+    _lib.check(L.p2p_flash_prefill(q.data_ptr(), q.stride(0), k_cache.data_ptr(),
+                                   v_cache.data_ptr(), block_tables.data_ptr(),
+                                   block_tables.stride(0), tiles.data_ptr(), tiles.shape[0],
+                                   n_heads, n_kv, HEAD_DIM, float(scale), out.data_ptr(),
+                                   out.stride(0), _lib.stream_ptr(q.device)), "flash_prefill")
+    return out
+
+
 def rope_cache_ref(qkv, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_cache):
     T = qkv.shape[0]
     D = HEAD_DIM
