@@ -138,7 +138,7 @@ def main():
             "ttft_p99_ms": round(sorted(all_ttft)[min(len(all_ttft) - 1,
                                                       int(0.99 * len(all_ttft)))], 3),
             "per_gpu_tokens_per_sec": round(value / world, 2),
-            "gemm_autotune": {"%s@M%d" % k: "w%d/U%d %.1fus" % v
+            "gemm_autotune": {"%s@M%d" % k: "%s %.1fus" % v
                               for k, v in getattr(eng, "tuning", {}).items()},
         }
         print(json.dumps(out), flush=True)

@@ -35,7 +35,8 @@ struct EpiArgs {
   const float* row_w;
   long long w_stride;
   int n_experts;
-  int u;  // requested pipeline depth (0 = default)
+  int u;   // requested pipeline depth (0 = default)
+  int ng;  // requested column groups per block (skinny GEMM, M > 16; 0/1 = one)
 };
 
 __device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) {

@@ -36,15 +36,18 @@
 
 namespace {
 
-template <int MT, int WAVES, int EPI, bool NORM, int U, bool MOE = false>
+template <int MT, int WAVES, int EPI, bool NORM, int U, bool MOE = false, int NG = 1>
 __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     const bf16x8* __restrict__ Wt, const bf16* __restrict__ X, int ldx, int M, int K,
     int up_group_offset, void* __restrict__ out, int ldo, float eps, EpiArgs ea) {
+  // NG column groups per block share every A (activation) fragment: at MT > 1 the
+  // A loads (MT per k-step) and the NORM sum of squares dominate unless reused.
   constexpr int NB = (EPI == EPI_SILU) ? 2 : 1;
+  constexpr int NW = NG * NB;  // weight fragments per k-step
   const int S = K >> 5;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int g = blockIdx.x;
+  const int g0 = blockIdx.x * NG;
   const int s0 = (S * w) / WAVES;
   const int s1 = (S * (w + 1)) / WAVES;
   const int r = lane & 15, q = lane >> 4;
@@ -57,9 +60,12 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     mrows = ea.moe_rows + (size_t)e * ea.rows_stride;
   }
 
-  const bf16x8* wp[NB];
-  wp[0] = Wt + (size_t)g * S * 64 + lane;
-  if constexpr (NB == 2) wp[NB - 1] = Wt + (size_t)(g + up_group_offset) * S * 64 + lane;
+  const bf16x8* wp[NW];
+#pragma unroll
+  for (int c = 0; c < NG; ++c) {
+    wp[c * NB] = Wt + (size_t)(g0 + c) * S * 64 + lane;
+    if constexpr (NB == 2) wp[c * NB + 1] = Wt + (size_t)(g0 + c + up_group_offset) * S * 64 + lane;
+  }
 
   const bf16* xp[MT];
   bool xv[MT];
@@ -74,10 +80,12 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 
   // EPI_QKV_ROPE: fetch (cos, sin) and the KV slot of this lane's output rows now,
   // so the epilogue's dependent pos -> table loads overlap the weight stream.
+  // (NG > 1: the rows' slots/positions only; the table is read in the epilogue.)
   float2 rc[MT][4];
   int rslot[MT][4];
+  int rpos[MT][4];
   if constexpr (EPI == EPI_QKV_ROPE) {
-    const int kk = g & 7;
+    const int kk = g0 & 7;
     const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -88,53 +96,56 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
         if constexpr (MOE) mm = 0;
         const bool ok = m < M && w == 0;
         rslot[mt][j] = ok ? ea.slots[mm] : -1;
-        rc[mt][j] = ok ? ea.cs[(size_t)ea.pos[mm] * 64 + dd] : float2{1.f, 0.f};
+        rpos[mt][j] = ok ? ea.pos[mm] : 0;
+        if constexpr (NG == 1)
+          rc[mt][j] = ok ? ea.cs[(size_t)rpos[mt][j] * 64 + dd] : float2{1.f, 0.f};
       }
   }
 
-  f32x4 acc[NB][MT];
+  f32x4 acc[NW][MT];
   float ss[MT];
 #pragma unroll
-  for (int b = 0; b < NB; ++b)
+  for (int b = 0; b < NW; ++b)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[b][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
 
-  auto load = [&](int s, bf16x8(&bw)[U][NB], bf16x8(&ax)[U][MT]) {
+  auto load = [&](int s, bf16x8(&bw)[U][NW], bf16x8(&ax)[U][MT]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int b = 0; b < NB; ++b) bw[u][b] = load_nt(wp[b] + (size_t)(s + u) * 64);
+      for (int b = 0; b < NW; ++b) bw[u][b] = load_nt(wp[b] + (size_t)(s + u) * 64);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
         ax[u][mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + (s + u) * 32)
                            : zero_bf16x8();
     }
   };
-  auto compute = [&](bf16x8(&bw)[U][NB], bf16x8(&ax)[U][MT]) {
+  auto compute1 = [&](const bf16x8(&bw)[NW], const bf16x8(&ax)[MT]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+      for (int b = 0; b < NW; ++b)
+        acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[mt], bw[b], acc[b][mt], 0, 0, 0);
+      if constexpr (NORM) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b)
-          acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[u][mt], bw[u][b], acc[b][mt], 0, 0, 0);
-        if constexpr (NORM) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xf = (float)ax[u][mt][j];
-            ss[mt] = fmaf(xf, xf, ss[mt]);
-          }
+        for (int j = 0; j < 8; ++j) {
+          const float xf = (float)ax[mt][j];
+          ss[mt] = fmaf(xf, xf, ss[mt]);
         }
       }
     }
+  };
+  auto compute = [&](bf16x8(&bw)[U][NW], bf16x8(&ax)[U][MT]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) compute1(bw[u], ax[u]);
   };
 
   const int n = s1 - s0;
   const int nb = n / U;
   if (nb > 0) {
-    bf16x8 bA[U][NB], aA[U][MT], bB[U][NB], aB[U][MT];
+    bf16x8 bA[U][NW], aA[U][MT], bB[U][NW], aB[U][MT];
     load(s0, bA, aA);
     int b = 0;
     for (; b + 2 < nb; b += 2) {
@@ -152,25 +163,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     }
   }
   for (int s = s0 + nb * U; s < s1; ++s) {
-    bf16x8 b1[1][NB], a1[1][MT];
+    bf16x8 b1[NW], a1[MT];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) b1[0][b] = load_nt(wp[b] + (size_t)s * 64);
+    for (int b = 0; b < NW; ++b) b1[b] = load_nt(wp[b] + (size_t)s * 64);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
-      a1[0][mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + s * 32) : zero_bf16x8();
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-        acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[0][mt], b1[0][b], acc[b][mt], 0, 0, 0);
-      if constexpr (NORM) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xf = (float)a1[0][mt][j];
-          ss[mt] = fmaf(xf, xf, ss[mt]);
-        }
-      }
-    }
+      a1[mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + s * 32) : zero_bf16x8();
+    compute1(b1, a1);
   }
 
   // ---- split-K reduction across the block's waves ----
@@ -181,12 +180,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
       ss[mt] += __shfl_xor(ss[mt], 32, 64);
     }
   }
+  float rstd[MT][4];
   if constexpr (WAVES > 1) {
-    __shared__ float red[WAVES - 1][NB * MT * 4][64];
+    __shared__ float red[WAVES - 1][NW * MT * 4][64];
     __shared__ float red_ss[WAVES][MT][16];
     if (w > 0) {
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
+      for (int b = 0; b < NW; ++b)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -203,64 +203,67 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 #pragma unroll
     for (int ww = 0; ww < WAVES - 1; ++ww)
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
+      for (int b = 0; b < NW; ++b)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[b][mt][j] += red[ww][(b * MT + mt) * 4 + j][lane];
-    if constexpr (NORM) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;  // recomputed per (mt, j) below
-    }
-    // epilogue with rstd from LDS
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = mt * 16 + q * 4 + j;
-        float scale = 1.f;
+        rstd[mt][j] = 1.f;
         if constexpr (NORM) {
           float t = 0.f;
 #pragma unroll
           for (int ww = 0; ww < WAVES; ++ww) t += red_ss[ww][mt][q * 4 + j];
-          scale = rsqrtf(t / (float)K + eps);
+          rstd[mt][j] = rsqrtf(t / (float)K + eps);
         }
-        int orow = m;
-        if constexpr (MOE) {
-          orow = m < M ? mrows[m] : 0;
-          if (ea.row_w && m < M) scale *= ea.row_w[orow];
-        }
-        if constexpr (EPI == EPI_QKV_ROPE)
-          epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, 0.f, out, ldo, ea, rc[mt][j],
-                         rslot[mt][j]);
-        else
-          epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out,
-                         ldo, ea);
       }
-    }
   } else {
     // single wave: rstd for row m lives in lane (m & 15) of the same m-tile.
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        rstd[mt][j] = 1.f;
+        if constexpr (NORM) {
+          const float t = __shfl(ss[mt], q * 4 + j, 64);
+          rstd[mt][j] = rsqrtf(t / (float)K + eps);
+        }
+      }
+  }
+
+  // ---- epilogue (wave 0) ----
+#pragma unroll
+  for (int c = 0; c < NG; ++c) {
+    const int g = g0 + c;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = mt * 16 + q * 4 + j;
-        float scale = 1.f;
-        if constexpr (NORM) {
-          const float t = __shfl(ss[mt], q * 4 + j, 64);
-          scale = rsqrtf(t / (float)K + eps);
-        }
+        float scale = rstd[mt][j];
         int orow = m;
         if constexpr (MOE) {
           orow = m < M ? mrows[m] : 0;
           if (ea.row_w && m < M) scale *= ea.row_w[orow];
         }
-        if constexpr (EPI == EPI_QKV_ROPE)
-          epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, 0.f, out, ldo, ea, rc[mt][j],
+        if constexpr (EPI == EPI_QKV_ROPE) {
+          float2 cs;
+          if constexpr (NG == 1) {
+            cs = rc[mt][j];
+          } else {
+            const int kk = g & 7;
+            const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+            cs = m < M ? ea.cs[(size_t)rpos[mt][j] * 64 + dd] : float2{1.f, 0.f};
+          }
+          epi_store<EPI>(orow, m < M, g, r, acc[c][mt][j] * scale, 0.f, out, ldo, ea, cs,
                          rslot[mt][j]);
-        else
-          epi_store<EPI>(orow, m < M, g, r, acc[0][mt][j] * scale, acc[NB - 1][mt][j] * scale, out,
-                         ldo, ea);
+        } else {
+          epi_store<EPI>(orow, m < M, g, r, acc[c * NB][mt][j] * scale,
+                         acc[c * NB + NB - 1][mt][j] * scale, out, ldo, ea);
+        }
       }
     }
   }
@@ -302,6 +305,20 @@ int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups,
       return (int)hipGetLastError();
     }
     return (int)hipErrorInvalidValue;
+  }
+  if constexpr (MT > 1) {
+    // two column groups per block (shared A fragments); only where the split-K
+    // reduction buffer still fits the 64 KiB static LDS window
+    constexpr int NW2 = 2 * ((EPI == EPI_SILU) ? 2 : 1);
+    constexpr size_t lds2 = (size_t)(WAVES - 1) * NW2 * MT * 4 * 64 * 4;
+    if constexpr (lds2 <= 56 * 1024) {
+      if (ea.ng == 2 && groups % 2 == 0) {
+        hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, false, 2>),
+                           dim3(groups / 2), dim3(WAVES * 64), 0, st, (const bf16x8*)Wt,
+                           (const bf16*)X, ldx, M, K, up_off, out, ldo, eps, ea);
+        return (int)hipGetLastError();
+      }
+    }
   }
   hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>), dim3(groups), dim3(WAVES * 64), 0,
                      st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, up_off, out, ldo, eps, ea);
@@ -363,13 +380,16 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
     groups = N / 32;
     up_off = groups;
   }
-  // waves: low 8 bits = split-K waves (0 = heuristic), bits 8..15 = pipeline depth U (0 = default)
+  // waves: low 8 bits = split-K waves (0 = heuristic), bits 8..15 = pipeline depth U
+  // (0 = default), bits 16..23 = column groups per block (M > 16 only; 0 = 1)
   const int u_req = (waves >> 8) & 0xff;
+  const int ng_req = (waves >> 16) & 0xff;
   waves &= 0xff;
   if (waves <= 0) waves = pick_waves(groups, K, mt);
   if (epi == EPI_SILU && mt == 4 && waves > 4) waves = 4;
   EpiArgs ea2 = ea;
   ea2.u = u_req;
+  ea2.ng = ng_req;
   switch (epi) {
     case EPI_STORE:
       return norm ? launch_e<EPI_STORE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream)

@@ -41,12 +41,19 @@ def _graph_time(fn, reps=3):
 
 
 def _configs(K, M=1):
+    """Launch codes: waves | U << 8 | NG << 16 (NG = column groups per block, M > 16)."""
     out = []
-    for u in ((4, 8) if M <= 16 else (2, 4)):
-        for w in (1, 2, 4, 8):
-            if (K // 32) // w >= 8:
-                out.append(w | (u << 8))
+    for ng in ((1,) if M <= 16 else (1, 2)):
+        for u in ((4, 8) if M <= 16 else (2, 4)):
+            for w in (1, 2, 4, 8):
+                if (K // 32) // w >= 8 and not (ng > 1 and w == 8):
+                    out.append(w | (u << 8) | ((ng if ng > 1 else 0) << 16))
     return out
+
+
+def describe(code: int) -> str:
+    ng = (code >> 16) & 0xff
+    return "w%d/U%d%s" % (code & 0xff, (code >> 8) & 0xff, "/NG%d" % ng if ng > 1 else "")
 
 
 def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
@@ -90,10 +97,10 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
             best = min(times, key=times.get)
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)
             G.set_tune(G.tune_key(wts[0], M, epi, norm), best)
-            result[(name, M)] = (best & 0xff, best >> 8, times[best] * 1000 / len(wts))
+            result[(name, M)] = (describe(best), times[best] * 1000 / len(wts))
             if verbose:
-                print("autotune %-9s M=%-2d waves=%d U=%d  %.2f us" % (
-                    name, M, best & 0xff, best >> 8, times[best] * 1000 / len(wts)), flush=True)
+                print("autotune %-9s M=%-2d %s  %.2f us" % (
+                    name, M, describe(best), times[best] * 1000 / len(wts)), flush=True)
         keys.zero_()
     torch.cuda.synchronize()
     return result

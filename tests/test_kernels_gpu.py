@@ -87,6 +87,64 @@ def test_skinny_gemm_matches_cpu_path_bitwise_shape():
     assert _rel(b, a) < 5e-3
 
 
+def _ng_code(w, u):
+    return w | (u << 8) | (2 << 16)
+
+
+@pytest.mark.parametrize("M", [20, 40, 64])
+@pytest.mark.parametrize("w,u", [(1, 2), (2, 4), (4, 2), (4, 4)])
+def test_skinny_two_groups_per_block(M, w, u):
+    """NG=2 launch codes (two column groups share the A fragments) on every epilogue."""
+    from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
+
+    torch.manual_seed(M + 10 * w + u)
+    code = _ng_code(w, u)
+    K, N = 1024, 512
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    Wt = ops.tile_weight(W).to(DEV)
+    xd = x.to(DEV)
+    raw = x.float() @ W.float().t()
+    rn = torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    out = ops.skinny_gemm(Wt, xd, ops.EPI_STORE, norm=True, waves=code)
+    assert _rel(out.cpu(), raw * rn) < 1e-2
+    out = ops.skinny_gemm(Wt, xd, ops.EPI_F32, norm=False, waves=code)
+    assert _rel(out.cpu(), raw) < 5e-3
+    h = torch.randn(M, N).to(torch.bfloat16)
+    hd = h.to(DEV)
+    ops.skinny_gemm(Wt, xd, ops.EPI_RESID, out=hd, waves=code)
+    assert _rel(hd.cpu(), h.float() + raw) < 1e-2
+    act = ops.skinny_gemm(Wt, xd, ops.EPI_SILU, norm=True, waves=code)
+    a = raw * rn
+    assert _rel(act.cpu(), torch.nn.functional.silu(a[:, :N // 2]) * a[:, N // 2:]) < 1e-2
+    keys = ops.new_argmax_keys(M, DEV)
+    ops.lm_head_argmax(Wt, xd, keys, waves=code)
+    ids = torch.zeros(M, dtype=torch.int32, device=DEV)
+    ops.argmax_finalize(keys, ids)
+    assert ids.cpu().long().tolist() == raw.argmax(-1).tolist()
+    # qkv + rope + kv write
+    Hq, Hkv = 4, 2
+    Nq = (Hq + 2 * Hkv) * 128
+    Wq = (torch.randn(Nq, K) * 0.05).to(torch.bfloat16)
+    Wqt = ops.tile_weight(Wq[ops.rope_row_perm(Hq + 2 * Hkv)]).to(DEV)
+    cs = rope_table(LLAMA31_8B, max_pos=2048)
+    pos = torch.randint(0, 2000, (M,), dtype=torch.int32)
+    slots = torch.randperm(4 * 64)[:M].to(torch.int32)
+    qkv = (x.float() @ Wq.float().t()) * rn
+    q_ref = torch.zeros(M, Hq * 128, dtype=torch.bfloat16)
+    kr = torch.zeros(4, Hkv, 64, 128, dtype=torch.bfloat16)
+    vr = torch.zeros_like(kr)
+    A.rope_cache_ref(qkv.to(torch.bfloat16), pos, slots, cs, Hq, Hkv, q_ref, kr, vr)
+    qd = torch.zeros(M, Hq * 128, dtype=torch.bfloat16, device=DEV)
+    kd, vd = torch.zeros_like(kr).to(DEV), torch.zeros_like(vr).to(DEV)
+    ops.qkv_rope_gemm(Wqt, xd, pos.to(DEV), slots.to(DEV), cs.to(DEV), Hq, Hkv, qd, kd, vd,
+                      waves=code)
+    torch.cuda.synchronize()
+    assert _rel(qd.cpu(), q_ref) < 1e-2
+    assert _rel(kd.cpu(), kr) < 1e-2
+    assert _rel(vd.cpu(), vr) < 1e-2
+
+
 # ------------------------------------------------------------ paged attention
 def _make_cache(P, Hkv, seed=0):
     g = torch.Generator().manual_seed(seed)
