@@ -38,6 +38,14 @@ _SIGS = {
                             c_void_p, c_void_p, c_void_p],
     "p2p_flash_prefill": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                           c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
+    "p2p_car_alloc": [ctypes.c_size_t, c_void_p],
+    "p2p_car_free": [c_void_p],
+    "p2p_car_get_handle": [c_void_p, c_void_p],
+    "p2p_car_open_handle": [c_void_p, c_void_p],
+    "p2p_car_close_handle": [c_void_p],
+    "p2p_car_handle_size": [],
+    "p2p_car_allreduce_add": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p, c_int,
+                              c_void_p, c_void_p, c_int, c_void_p],
     "p2p_gather_rows": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
     "p2p_rope_cache": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_void_p, c_int, c_void_p, c_void_p, c_void_p],
@@ -88,6 +96,10 @@ def lib():
                 "HIP kernel library missing at %s -- run `python -m p2p_llm_chat_go_amd._build` "
                 "(or __graft_entry__.build())" % _LIB_PATH)
         L = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        fn = getattr(L, "p2p_car_buffer_bytes", None)
+        if fn is not None:
+            fn.argtypes = [ctypes.c_size_t]
+            fn.restype = ctypes.c_size_t
         fn = getattr(L, "p2p_skinny_gemm_tune", None)
         if fn is not None:
             fn.argtypes = [c_int, c_int]

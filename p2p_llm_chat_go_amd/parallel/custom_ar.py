@@ -1,0 +1,91 @@
+"""One-shot all-reduce over IPC-mapped peer buffers (kernel K12, xGMI).
+
+Decode-size tensor-parallel messages (B x hidden bf16: 16 KiB for 70B at
+batch 1, 160 of them per token) are latency-bound.  RCCL's ring needs 2(W-1)
+dependent hops; here every rank pushes its partial into every peer's buffer
+at once (all 7 xGMI links of a rank in parallel), posts a flag, waits for the
+peers' flags on its own memory and sums locally -- one hop.  The kernel is an
+ordinary launch on the current stream, so it is captured in the decode
+hipGraph with the GEMMs around it.  See ``csrc/kernels/custom_allreduce.hip``.
+
+Handles are exchanged with ``dist.all_gather_object`` over the TP group (any
+backend).  Messages above ``max_bytes`` fall back to the caller's RCCL path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+
+class CustomAllReduce:
+    MAX_RANKS = 8
+
+    def __init__(self, group=None, device=None, max_bytes: int = 1 << 20):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > self.MAX_RANKS:
+            raise ValueError("custom all-reduce supports at most 8 ranks")
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.max_bytes = int(max_bytes)
+        L = self.L = _lib.lib()
+        with torch.cuda.device(self.device):
+            size = L.p2p_car_buffer_bytes(self.max_bytes)
+            buf = ctypes.c_void_p()
+            _lib.check(L.p2p_car_alloc(size, ctypes.byref(buf)), "car_alloc")
+            self._own = buf
+            hsz = L.p2p_car_handle_size()
+            handle = ctypes.create_string_buffer(hsz)
+            _lib.check(L.p2p_car_get_handle(buf, handle), "car_get_handle")
+            handles = [None] * self.world
+            dist.all_gather_object(handles, handle.raw, group=group)
+            self._opened = []
+            bases = []
+            for r, hb in enumerate(handles):
+                if r == self.rank:
+                    bases.append(buf.value)
+                    continue
+                ptr = ctypes.c_void_p()
+                _lib.check(L.p2p_car_open_handle(ctypes.create_string_buffer(hb, hsz),
+                                                 ctypes.byref(ptr)), "car_open_handle")
+                self._opened.append(ptr)
+                bases.append(ptr.value)
+            self._bases = (ctypes.c_void_p * self.world)(*bases)
+            self.counters = torch.zeros(64, dtype=torch.int32, device=self.device)
+            self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)
+
+    def fits(self, t: torch.Tensor) -> bool:
+        return (t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() % 8 == 0
+                and t.numel() * 2 <= self.max_bytes)
+
+    def allreduce_add_(self, h: torch.Tensor, partial: torch.Tensor, blocks: int = 0):
+        """h += sum over ranks of partial (bf16, same shape, contiguous)."""
+        assert self.fits(partial) and h.is_contiguous() and h.numel() == partial.numel()
+        _lib.check(self.L.p2p_car_allreduce_add(self._bases, self.rank, self.world,
+                                                self.max_bytes, partial.data_ptr(), h.data_ptr(),
+                                                partial.numel(), self.counters.data_ptr(),
+                                                self.err.data_ptr(), blocks,
+                                                _lib.stream_ptr(h.device)), "car_allreduce_add")
+        return h
+
+    def check(self):
+        """Raise if any call timed out waiting for a peer (numbers would be wrong)."""
+        if int(self.err.item()) != 0:
+            raise RuntimeError("custom all-reduce: a peer never arrived (timeout)")
+
+    def close(self):
+        if self._own is None:
+            return
+        torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            self.L.p2p_car_close_handle(p)
+        self._opened = []
+        self.L.p2p_car_free(self._own)
+        self._own = None
