@@ -26,6 +26,7 @@ from ..models.config import ModelConfig
 from ..models.llama import LlamaModel
 from ..models.weights import EngineWeights
 from .. import ops
+from ..utils.trace import span
 from ..ops import PAGE
 from .graph import DecodeGraph, DecodeState
 from .kv_cache import KVCache, pages_for
@@ -69,6 +70,8 @@ class Engine:
                                                tp_size=tp_size)
         else:
             self.kv = KVCache(cfg, kv_pages, self.device, tp_size)
+        if comm is not None and hasattr(comm, "setup"):
+            comm.setup(self.device)
         self.model = LlamaModel(weights, self.kv, comm)
         self.max_prefill_tokens = max_prefill_tokens
         # prefill chunks with at least this many rows use the MFMA flash kernel
@@ -187,8 +190,9 @@ class Engine:
         need = [len(p) + max_new_tokens for p in prompts]
         pages = [self.kv.allocator.alloc(pages_for(n)) for n in need]
         try:
-            first = self.prefill(prompts, pages)
-            first_h = first.cpu()  # sync: first token is on the host -> TTFT
+            with span("prefill", batch=B, tokens=sum(len(p) for p in prompts)):
+                first = self.prefill(prompts, pages)
+                first_h = first.cpu()  # sync: first token is on the host -> TTFT
             t1 = time.perf_counter_ns()
             out = [[int(first_h[b])] for b in range(B)]
             done = [stop_on_eos and out[b][0] in self.cfg.eos_ids for b in range(B)]
@@ -201,7 +205,8 @@ class Engine:
                 while steps_run < n_dec:
                     k = n_dec - steps_run if not stop_on_eos else min(check_every,
                                                                       n_dec - steps_run)
-                    g.replay(k)
+                    with span("decode", batch=B, steps=k):
+                        g.replay(k)
                     steps_run += k
                     if stop_on_eos:
                         h = st.hist[:B, :steps_run].cpu()

@@ -23,6 +23,7 @@ from concurrent.futures import Future
 import torch
 
 from ..native import load as load_native
+from ..utils.trace import span
 from .engine import CTX_BUCKETS, Engine
 from .sampling import SamplingParams
 from .tokenizer import get_tokenizer
@@ -151,7 +152,8 @@ class EngineServer:
             t0 = time.perf_counter_ns()
             for i in plan.prefill:
                 self._reqs[i]["t_admit"] = t0
-            first = eng.prefill(prompts, pages).cpu().tolist()
+            with span("server.prefill", batch=len(prompts)):
+                first = eng.prefill(prompts, pages).cpu().tolist()
             t1 = time.perf_counter_ns()
             self.stats["prefill_tokens"] += sum(len(p) for p in prompts)
             for i, tkn in zip(plan.prefill, first):
@@ -174,11 +176,12 @@ class EngineServer:
         remaining = min(r.max_new - len(r.tokens) for r in reqs)
         waiting = self.sched.n_waiting + len(self._pending)
         k = max(1, min(self.decode_chunk if not waiting else 2, remaining))
-        if greedy:
-            g.replay(k)
-        else:
-            for _ in range(k):
-                g.step_sampled(params, self._gen)
+        with span("server.decode", batch=len(running), steps=k):
+            if greedy:
+                g.replay(k)
+            else:
+                for _ in range(k):
+                    g.step_sampled(params, self._gen)
         hist = st.hist[:len(running), :k].cpu().tolist()
         self.stats["decode_steps"] += k
         self.sched.on_decode_tokens(running, hist)

@@ -7,7 +7,10 @@ stream so it is captured into the decode hipGraph together with the kernels.
 
 Decode-size messages are tiny (B x 8192 bf16 = 16 KiB per all-reduce for 70B
 at batch 1), i.e. latency-bound: 2 all-reduces per layer plus one 64-bit MAX
-all-reduce of the greedy argmax keys per step.  Greedy sampling never gathers
+all-reduce of the greedy argmax keys per step.  On GPUs those row-parallel
+sums go through the one-shot IPC all-reduce kernel (``custom_ar.py``, one
+xGMI hop instead of RCCL's 2(W-1)); messages above its buffer (long prefill
+chunks) use RCCL.  Greedy sampling never gathers
 vocab-parallel logits: each rank reduces its vocab shard to (value, token) keys
 in the LM-head epilogue and one MAX all-reduce picks the global argmax.
 """
@@ -22,14 +25,36 @@ _SIGN = -(2 ** 63)
 
 
 class TPComm:
-    def __init__(self, group=None):
+    def __init__(self, group=None, custom_ar: bool | None = None, car_max_bytes: int = 1 << 21):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        if custom_ar is None:
+            custom_ar = os.environ.get("P2P_CUSTOM_AR", "1") == "1"
+        self.want_custom_ar = custom_ar
+        self.car_max_bytes = car_max_bytes
+        self.car = None
+
+    def setup(self, device):
+        """Collective-side allocations for ``device`` (call before graph capture)."""
+        device = torch.device(device)
+        if self.want_custom_ar and device.type == "cuda" and self.car is None and self.world > 1:
+            from .custom_ar import CustomAllReduce
+
+            self.car = CustomAllReduce(self.group, device, self.car_max_bytes)
+        return self
+
+    def close(self):
+        if self.car is not None:
+            self.car.close()
+            self.car = None
 
     # row-parallel outputs: h += sum_r partial_r
     def allreduce_add_(self, h: torch.Tensor, partial: torch.Tensor):
+        if (self.car is not None and h.device.type == "cuda" and self.car.fits(partial)
+                and h.is_contiguous()):
+            return self.car.allreduce_add_(h, partial)
         if h.device.type == "cpu" or self.backend != "nccl":
             # gloo (CPU tests, virtual ranks on one GPU): reduce in fp32
             buf = partial.float()
