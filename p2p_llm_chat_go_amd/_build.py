@@ -141,6 +141,54 @@ def build_native(force=False, jobs=8):
     return outs
 
 
+SANITIZERS = {
+    # SURVEY.md §5 "Race detection / sanitizers": CPU-side variants of the daemons
+    "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+    "tsan": ["-fsanitize=thread"],
+}
+
+
+# ROCm's clang: its compiler-rt TSan intercepts pthread_cond_clockwait (used by
+# libstdc++'s condition_variable::wait_for); GCC 11's libtsan does not, which
+# makes every timed wait look like a double lock / race.
+SAN_CXX = os.environ.get("P2P_SAN_CXX", os.path.join(ROCM, "lib", "llvm", "bin", "clang++"))
+
+
+def build_sanitized(kind: str, force=False, jobs=8):
+    """Daemons (directory / node / relay) built with ASan+UBSan or TSan into bin/<kind>/."""
+    san = SANITIZERS[kind]
+    cxx = SAN_CXX if os.path.exists(SAN_CXX) else CXX
+    subdirs = ["net", "runtime"]
+    odir = os.path.join(BUILDDIR, "native-" + kind)
+    bdir = os.path.join(BINDIR, kind)
+    os.makedirs(odir, exist_ok=True)
+    os.makedirs(bdir, exist_ok=True)
+    inc = ["-I", os.path.join(CSRC, "include"), "-I", CSRC]
+    base = ["-O1", "-g", "-std=c++17", "-pthread"] + san + inc
+    srcs, hdrs = [], []
+    for d in subdirs:
+        srcs += sorted(glob.glob(os.path.join(CSRC, d, "*.cc")))
+    for d in subdirs + ["include"]:
+        hdrs += glob.glob(os.path.join(CSRC, d, "*.h"))
+    objs, todo = [], []
+    for s_ in srcs:
+        o = os.path.join(odir, os.path.relpath(s_, CSRC).replace(os.sep, "_") + ".o")
+        objs.append(o)
+        if force or _stale(o, [s_] + hdrs):
+            todo.append((s_, o))
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(_run, [cxx] + base + ["-c", a, "-o", b]) for a, b in todo]:
+            f.result()
+    outs = []
+    for app in sorted(glob.glob(os.path.join(CSRC, "apps", "*.cc"))):
+        name = os.path.splitext(os.path.basename(app))[0]
+        exe = os.path.join(bdir, name)
+        if force or _stale(exe, [app] + objs + hdrs):
+            _run([cxx] + base + [app] + objs + ["-o", exe, "-lssl", "-lcrypto", "-pthread"])
+        outs.append(exe)
+    return outs
+
+
 def build(force=False, jobs=8, only=None):
     outs = []
     if only in (None, "kernels"):
@@ -158,7 +206,13 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--only", choices=["kernels", "native"], default=None)
+    ap.add_argument("--sanitize", choices=sorted(SANITIZERS), default=None,
+                    help="build only the sanitizer variant of the daemons into bin/<kind>/")
     a = ap.parse_args(argv)
+    if a.sanitize:
+        for o in build_sanitized(a.sanitize, a.force, a.jobs):
+            print(o)
+        return
     for o in build(a.force, a.jobs, a.only):
         print(o)
 
