@@ -228,6 +228,7 @@ NodeConfig NodeConfig::from_env() {
   c.register_interval_s = atoi(env_or("REGISTER_INTERVAL", "0").c_str());
   c.strict_sender = env_or("STRICT_SENDER", "0") == "1";
   c.access_log = env_or("GIN_MODE", "debug") != "quiet";
+  c.dht_mode = env_or("DHT_MODE", c.dht_mode);
   std::string la = env_or("LISTEN_ADDRS", "");
   if (la == "none") {
     c.listen.clear();  // relay-only node
@@ -321,6 +322,10 @@ void Node::on_chat(StreamCtx& c) {
 void Node::start() {
   PrivateKey key = load_or_make_identity(cfg_);
   host_ = std::make_shared<Host>(key);
+  if (cfg_.dht_mode != "off") {
+    // created before any listener/dial so identify results feed the routing table
+    kad_ = std::make_unique<Kad>(host_, cfg_.dht_mode == "client" ? KadMode::Client : KadMode::Server);
+  }
   for (auto& l : cfg_.listen) host_->listen(Multiaddr::parse(l));
   relay_client_ = std::make_unique<RelayClient>(host_);
   host_->set_stream_handler(kChatProto, [this](StreamCtx& c) { on_chat(c); });
@@ -346,6 +351,7 @@ void Node::start() {
       if (id.empty()) throw NetError("invalid p2p multiaddr");
       host_->connect(id, {bare}, 10000);
       logf("✅ connected to bootstrap %s", id.to_base58().c_str());
+      if (kad_) kad_->add_peer(id, {bare});
     } catch (const std::exception& e) {
       logf("connect: %s (%s)", e.what(), b.c_str());
     }
@@ -380,6 +386,7 @@ void Node::stop() {
   http_.stop();
   if (refresher_.joinable()) refresher_.join();
   if (host_) host_->close();
+  kad_.reset();  // after close(): no identify/handler thread can reach it any more
 }
 
 static Json err(const std::string& e) {
@@ -632,6 +639,45 @@ void Node::install_routes() {
       arr.push(e);
     }
     res.json(200, arr);
+  });
+  // DHT (superset of the reference API): routing table and peer lookup
+  http_.route("GET", "/dht/peers", [this](const HttpRequest&, HttpResponse& res) {
+    Json arr = Json::array();
+    if (kad_) {
+      for (auto& p : kad_->closest(kad_key(host_->id().bytes()), 1 << 20)) {
+        Json e = Json::object();
+        e.set("peer_id", p.id.to_base58());
+        Json a = Json::array();
+        for (auto& x : p.addrs) a.push(x.str());
+        e.set("addrs", a);
+        arr.push(e);
+      }
+    }
+    res.json(200, arr);
+  });
+  http_.route("GET", "/dht/find", [this](const HttpRequest& req, HttpResponse& res) {
+    if (!kad_) {
+      res.json(503, err("dht disabled"));
+      return;
+    }
+    PeerId target;
+    try {
+      target = PeerId::decode(req.param("peer"));
+    } catch (...) {
+      res.json(400, err("bad peer id"));
+      return;
+    }
+    std::vector<Multiaddr> addrs;
+    if (!kad_->find_peer(target, &addrs, 5000)) {
+      res.json(404, err("peer not found"));
+      return;
+    }
+    Json j = Json::object();
+    j.set("peer_id", target.to_base58());
+    Json a = Json::array();
+    for (auto& x : addrs) a.push(x.str());
+    j.set("addrs", a);
+    res.json(200, j);
   });
   http_.route("GET", "/health", [](const HttpRequest&, HttpResponse& res) {
     Json j = Json::object();

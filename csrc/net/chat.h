@@ -15,6 +15,7 @@
 #include "host.h"
 #include "http.h"
 #include "json.h"
+#include "kad.h"
 #include "relay.h"
 
 namespace p2p {
@@ -93,7 +94,10 @@ struct NodeConfig {
   int register_interval_s = 0;   // 0 = register once (reference); >0 = refresh timer
   bool strict_sender = false;    // reject messages whose from_user != directory name of the peer
   bool access_log = true;
-  bool dht = true;
+  // Kademlia (`/ipfs/kad/1.0.0`): "auto"/"server" answer queries, "client" only
+  // queries, "off" disables.  The reference's dht.ModeAuto (main.go:151) is inert
+  // without AutoNAT; we serve by default (no AutoNAT here) -- documented deviation.
+  std::string dht_mode = "auto";
   static NodeConfig from_env();
 };
 
@@ -115,6 +119,7 @@ class Node {
   void set_generate_hook(GenerateHook h);
   Inbox& inbox() { return inbox_; }
   std::shared_ptr<Host> host() { return host_; }
+  Kad* kad() { return kad_.get(); }
   // POST /send semantics; returns (status, json body)
   std::pair<int, Json> send(const std::string& to, const std::string& content);
   Json metrics_json();
@@ -126,6 +131,7 @@ class Node {
   NodeConfig cfg_;
   std::shared_ptr<Host> host_;
   std::unique_ptr<RelayClient> relay_client_;
+  std::unique_ptr<Kad> kad_;
   std::unique_ptr<DirectoryClient> dir_;
   Inbox inbox_;
   HttpServer http_;

@@ -315,9 +315,14 @@ void Host::run_identify(const PeerId& p, SessionPtr s) {
       }
     }
     add_addrs(p, listen);
-    std::lock_guard<std::mutex> lk(mu_);
-    peer_protos_[p] = protos;
-    peer_agents_[p] = agent;
+    decltype(on_identified) cb;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      peer_protos_[p] = protos;
+      peer_agents_[p] = agent;
+      cb = on_identified;
+    }
+    if (cb) cb(p, protos, listen);
   } catch (...) {
   }
 }

@@ -78,6 +78,11 @@ class Host {
   std::vector<std::string> peer_protocols(const PeerId& p);
   std::string peer_agent(const PeerId& p);
 
+  // Called after identify completes for a peer (protocols, listen addrs); the
+  // DHT uses it to fill its routing table like go-libp2p-kad-dht does.
+  std::function<void(const PeerId&, const std::vector<std::string>&, const std::vector<Multiaddr>&)>
+      on_identified;
+
   // Relay dialer hook (installed by RelayClient).
   std::function<SessionPtr(const Multiaddr& relay, const PeerId& target, int timeout_ms)> relay_dialer;
 

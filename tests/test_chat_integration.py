@@ -227,3 +227,35 @@ def test_suggest_without_engine_is_503(procs):
     st, body, _ = http("POST", a + "/suggest", {"message": "hi"})
     assert st == 503 and "LLM unavailable" in json.loads(body)["error"]
     assert http("GET", a + "/metrics")[0] == 200
+
+
+def test_kad_dht_find_peer_through_bootstrap_chain(procs):
+    """A <- B <- C bootstrap chain: C never talked to A, yet finds A's addresses by
+    an iterative /ipfs/kad/1.0.0 FIND_NODE lookup through B."""
+    d = start_directory(procs)
+    a = start_node(procs, "A", d)
+    me_a = json.loads(http("GET", a + "/me")[1])
+    b = start_node(procs, "B", d, {"BOOTSTRAP_ADDRS": me_a["addrs"][0]})
+    me_b = json.loads(http("GET", b + "/me")[1])
+    c = start_node(procs, "C", d, {"BOOTSTRAP_ADDRS": me_b["addrs"][0]})
+    # routing tables fill from identify (peers advertising the kad protocol)
+    for _ in range(100):
+        pa = [p["peer_id"] for p in json.loads(http("GET", a + "/dht/peers")[1])]
+        pc = [p["peer_id"] for p in json.loads(http("GET", c + "/dht/peers")[1])]
+        if me_b["peer_id"] in pa and me_b["peer_id"] in pc:
+            break
+        time.sleep(0.05)
+    assert me_b["peer_id"] in pa and me_b["peer_id"] in pc
+    assert me_a["peer_id"] not in pc
+    st, body, _ = http("GET", c + "/dht/find?peer=" + me_a["peer_id"])
+    assert st == 200, body
+    found = json.loads(body)
+    assert found["peer_id"] == me_a["peer_id"] and found["addrs"]
+    assert any(x.split("/p2p/")[0] in found["addrs"] for x in me_a["addrs"])
+    # the lookup taught C about A
+    pc = [p["peer_id"] for p in json.loads(http("GET", c + "/dht/peers")[1])]
+    assert me_a["peer_id"] in pc
+    assert http("GET", c + "/dht/find?peer=notapeer")[0] == 400
+    # a node started with DHT_MODE=off serves no kad protocol
+    e = start_node(procs, "E", d, {"DHT_MODE": "off"})
+    assert http("GET", e + "/dht/find?peer=" + me_a["peer_id"])[0] == 503
