@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Continuous-batching serving benchmark (BASELINE config 4: concurrent peers ->
+batched decode), in-process through EngineServer + the native scheduler.
+
+``--peers`` clients each issue ``--requests`` suggest-reply requests back to back
+(closed loop: a peer sends its next request when the previous reply arrives),
+so the engine sees requests join and leave the running batch at arbitrary
+steps.  Prints one JSON line: aggregate generated tokens/s, TTFT p50/p99
+(submit -> first token, queueing included), mean batch occupancy.
+Per GPU; run one process per GPU (torchrun) for the 8-GPU number -- each rank
+serves its own peers (replica-per-GPU, dp).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import threading
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from p2p_llm_chat_go_amd.engine import Engine  # noqa: E402
+from p2p_llm_chat_go_amd.engine.sampling import SamplingParams  # noqa: E402
+from p2p_llm_chat_go_amd.engine.server import EngineServer  # noqa: E402
+from p2p_llm_chat_go_amd.engine.tokenizer import SAMPLE_MESSAGES, get_tokenizer, suggest_prompt  # noqa: E402
+from p2p_llm_chat_go_amd.models.config import get_config  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3.1-8b")
+    ap.add_argument("--peers", type=int, default=8)
+    ap.add_argument("--requests", type=int, default=4, help="requests per peer (timed)")
+    ap.add_argument("--new-tokens", type=int, default=64)
+    ap.add_argument("--jitter", type=int, default=16,
+                    help="reply lengths vary in [new-tokens - jitter, new-tokens]")
+    ap.add_argument("--device", default="cuda")
+    a = ap.parse_args()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device(a.device, local) if a.device == "cuda" else torch.device(a.device)
+    cfg = get_config(a.model)
+    tok = get_tokenizer(cfg)
+    eng = Engine(cfg, device=dev, seed=7, max_batch=max(a.peers, 1), max_prefill_tokens=1024)
+    eng.warmup(tuple(sorted({1, 2, 4, 8, a.peers} - {0})), ctx=256)
+    srv = EngineServer(eng, tok, max_batch=a.peers, decode_chunk=8)
+    prompts = [tok.chat_ids(suggest_prompt(SAMPLE_MESSAGES[i % len(SAMPLE_MESSAGES)]))
+               for i in range(a.peers)]
+
+    def params(i):
+        n = a.new_tokens - (i * 7919) % (a.jitter + 1)
+        return SamplingParams(max_tokens=max(1, n), stop_on_eos=False)
+
+    # warm pass (graphs for every batch bucket the mix will hit)
+    futs = [srv.submit(prompts[p], params(p)) for p in range(a.peers)]
+    [f.result(600) for f in futs]
+    results, lock = [], threading.Lock()
+
+    def peer(p):
+        for r in range(a.requests):
+            out = srv.generate(prompts[p], params(p * 31 + r))
+            with lock:
+                results.append(out)
+
+    occ0 = dict(srv.stats)
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=peer, args=(p,)) for p in range(a.peers)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    el = time.perf_counter() - t0
+    srv.close()
+    toks = sum(r["eval_count"] for r in results)
+    ttft = sorted(r["ttft_ns"] / 1e6 for r in results)
+    steps = srv.stats["decode_steps"] - occ0["decode_steps"]
+    print(json.dumps({
+        "metric": "suggest-reply tokens/sec (continuous batching)", "value": round(toks / el, 2),
+        "unit": "tokens/s", "model": cfg.name, "peers": a.peers, "requests": len(results),
+        "new_tokens": a.new_tokens, "elapsed_s": round(el, 3),
+        "ttft_p50_ms": round(statistics.median(ttft), 3),
+        "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
+        "mean_batch": round(toks / max(steps, 1), 2), "dtype": "bf16",
+        "data": "synthetic chat prompts, random-init weights"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
