@@ -1,0 +1,54 @@
+"""Prefill GEMM comparison at llama3.1-8B shapes: register-staged v1 vs the
+8-wave LDS-DMA v2 kernel (each tile) vs hipBLASLt (torch.matmul, plain GEMM
+without the fused epilogue).  One JSON line per (M, projection, variant)."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from p2p_llm_chat_go_amd import ops  # noqa: E402
+from p2p_llm_chat_go_amd.ops.gemm import tiled_config  # noqa: E402
+from p2p_llm_chat_go_amd.models.config import LLAMA31_8B  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kernel_bench import graph_time  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, nargs="*", default=[288, 512, 2048, 8192])
+    a = ap.parse_args()
+    H, F = LLAMA31_8B.hidden, LLAMA31_8B.ffn
+    variants = [("v1", (1, 0)), ("v2_auto", (2, 0)), ("v2_256x256", (2, 1)),
+                ("v2_128x256", (2, 2)), ("v2_128x128", (2, 3))]
+    for M in a.M:
+        x = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+        xf = torch.randn(M, F, device="cuda").to(torch.bfloat16)
+        h = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+        act = torch.zeros(M, F, device="cuda", dtype=torch.bfloat16)
+        o = torch.zeros(M, 6144, device="cuda", dtype=torch.bfloat16)
+        for name, N, K, fn in [
+            ("qkv", 6144, H, lambda W: ops.skinny_gemm(W, x, ops.EPI_STORE, norm=True, out=o)),
+            ("gate_up", 2 * F, H, lambda W: ops.skinny_gemm(W, x, ops.EPI_SILU, norm=True, out=act)),
+            ("down", H, F, lambda W: ops.skinny_gemm(W, xf, ops.EPI_RESID, out=h))]:
+            W = (torch.randn(N // 16, K // 32, 64, 8, device="cuda") * 0.02).to(torch.bfloat16)
+            flops = 2 * M * N * K
+            for vname, cfg in variants:
+                tiled_config(*cfg)
+                t = graph_time(lambda i: fn(W), n_inner=10)
+                print(json.dumps({"M": M, "gemm": name, "variant": vname, "us": round(t, 1),
+                                  "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1)}), flush=True)
+            tiled_config(2, 0)
+            Wb = torch.randn(K, N, device="cuda").to(torch.bfloat16)
+            xin = x if K == H else xf
+            t = graph_time(lambda i: torch.matmul(xin, Wb), n_inner=10)
+            print(json.dumps({"M": M, "gemm": name, "variant": "hipblaslt", "us": round(t, 1),
+                              "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1)}), flush=True)
+            del W, Wb
+
+
+if __name__ == "__main__":
+    main()

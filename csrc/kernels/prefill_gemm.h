@@ -1,0 +1,270 @@
+// Prefill GEMM v2: 8-wave MFMA GEMM with direct global->LDS (LDS-DMA) staging.
+//
+//   out[m, n] = epilogue( rstd[m] * sum_k X[m, k] * W[n, k] )   (gemm_epilogue.h)
+//
+// Tile BM x BN x 64 (BM, BN in {128, 256}), 512 threads = 8 waves in a 2 (M) x 4 (N)
+// grid; wave tile (BM/2) x (BN/4) of v_mfma_f32_16x16x32_bf16 accumulators.
+// Both operands are staged with `global_load_lds_dwordx4` (one wave-instruction
+// = one 1 KiB MFMA fragment block): the LDS image is fragment-major, so every
+// operand read is a lane-linear, conflict-free ds_read_b128 and no VGPRs or
+// VALU are spent on staging:
+//   * W is fragment-major in HBM already (ops.tile_weight): a block is 1 KiB
+//     contiguous;
+//   * X is row-major: lane l of a block fetches X[row0 + (l&15)][k0 + 8(l>>4) ..]
+//     (per-lane source address, lane-linear destination).
+// Two LDS stages (2 x (BM+BN) x 64 bf16 <= 128 KiB, one __shared__ array):
+// stage kt+1 is in flight while the MFMAs consume stage kt; one barrier per
+// k-tile.  Blocks sharing a weight n-tile are consecutive after the XCD remap.
+// NORM: the waves of column 0 also square the A fragments they read; a lane
+// sees 8 of every 32 k of one row, 3 shuffles finish the row's sum.
+#pragma once
+#include "gemm_epilogue.h"
+
+namespace pgemm {
+
+constexpr int BK = 64;
+constexpr int NT = 512;
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int BM, int BN, int EPI, bool NORM>
+__global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restrict__ Wt,
+                                                          const bf16* __restrict__ X, int ldx,
+                                                          int M, int K, int m_tiles, int n_tiles,
+                                                          int up_off, void* __restrict__ out,
+                                                          int ldo, float eps, EpiArgs ea) {
+  constexpr int FM = BM / 32;        // 16-row fragments per wave
+  constexpr int FN = BN / 64;        // 16-col groups per wave
+  constexpr int AB = BM / 16 * 2;    // A fragment blocks per stage (x 1 KiB)
+  constexpr int BB = BN / 16 * 2;    // B fragment blocks per stage
+  constexpr int STAGE = (AB + BB) * 64;  // bf16x8 per stage
+  constexpr int AI = AB / 8, BI = BB / 8;  // blocks per wave per stage
+  static_assert(AB % 8 == 0 && BB % 8 == 0, "tile");
+  __shared__ __attribute__((aligned(16))) bf16x8 lds[2 * STAGE];
+
+  const int nb = m_tiles * n_tiles;
+  const int b = xcd_remap(blockIdx.x, nb);
+  const int mt_i = b % m_tiles, nt_i = b / m_tiles;
+  const int m0 = mt_i * BM;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+  const int S = K >> 5;
+  const int nk = K / BK;
+
+  auto group_of = [&](int gi) -> int {  // LDS group slot -> global 16-col group
+    if constexpr (EPI == EPI_SILU) {
+      constexpr int H = BN / 32;
+      return gi < H ? nt_i * H + gi : nt_i * H + (gi - H) + up_off;
+    }
+    return nt_i * (BN / 16) + gi;
+  };
+
+  // ---- per-lane DMA sources (k offsets added per k-tile) ----
+  const bf16* asrc[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int blk = w + 8 * i;  // = mi * 2 + ks
+    const int mi = blk >> 1, ks = blk & 1;
+    int row = m0 + 16 * mi + (lane & 15);
+    row = row < M ? row : M - 1;
+    asrc[i] = X + (size_t)row * ldx + 32 * ks + 8 * (lane >> 4);
+  }
+  const bf16x8* bsrc[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int blk = w + 8 * i;  // = gi * 2 + ks
+    bsrc[i] = Wt + ((size_t)group_of(blk >> 1) * S + (blk & 1)) * 64 + lane;
+  }
+
+  auto issue = [&](int kt, int st) {
+    bf16x8* base = lds + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < AI; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + kt * BK),
+                                       (lds_ptr_t)(base + (w + 8 * i) * 64), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (size_t)kt * 2 * 64),
+                                       (lds_ptr_t)(base + (AB + w + 8 * i) * 64), 16, 0, 0);
+  };
+
+  int bgi[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    if constexpr (EPI == EPI_SILU) {
+      constexpr int H = FN / 2;
+      bgi[j] = j < H ? wn * H + j : BN / 32 + wn * H + (j - H);
+    } else {
+      bgi[j] = wn * FN + j;
+    }
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) ss[i] = 0.f;
+  const bool do_ss = NORM && wn == 0;
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const bf16x8* sa = lds + cur * STAGE;
+    const bf16x8* sb = sa + AB * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = sb[(bgi[j] * 2 + ks) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = sa[((wm * FM + i) * 2 + ks) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (do_ss) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = (float)af[i][e];
+            ss[i] = fmaf(v, v, ss[i]);
+          }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- row rstd (NORM): column-0 waves publish through LDS (stages are free now) ----
+  float* ss_row = reinterpret_cast<float*>(lds);
+  if constexpr (NORM) {
+    if (wn == 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        float v = ss[i];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16) ss_row[wm * (BM / 2) + 16 * i + lane] = v;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int rl = wm * (BM / 2) + 16 * i + 4 * q + jj;
+      const int m = m0 + rl;
+      const bool valid = m < M;
+      float scale = 1.f;
+      if constexpr (NORM) scale = rsqrtf(ss_row[rl] / (float)K + eps);
+      if constexpr (EPI == EPI_SILU) {
+        constexpr int H = FN / 2;
+#pragma unroll
+        for (int j = 0; j < H; ++j)
+          epi_store<EPI>(m, valid, nt_i * (BN / 32) + wn * H + j, r, acc[i][j][jj] * scale,
+                         acc[i][j + H][jj] * scale, out, ldo, ea);
+      } else if constexpr (EPI == EPI_QKV_ROPE) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int g = nt_i * (BN / 16) + bgi[j];
+          const int kk = g & 7;
+          const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+          float2 c = float2{1.f, 0.f};
+          int slot = -1;
+          if (valid) {
+            c = ea.cs[(size_t)ea.pos[m] * 64 + dd];
+            slot = ea.slots[m];
+          }
+          epi_store<EPI>(m, valid, g, r, acc[i][j][jj] * scale, 0.f, out, ldo, ea, c, slot);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          epi_store<EPI>(m, valid, nt_i * (BN / 16) + bgi[j], r, acc[i][j][jj] * scale, 0.f, out,
+                         ldo, ea);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int EPI, bool NORM>
+int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off, void* out,
+           int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
+  const int m_tiles = (M + BM - 1) / BM;
+  const int n_tiles = N / BN;
+  hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM>), dim3(m_tiles * n_tiles), dim3(NT),
+                     0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, m_tiles, n_tiles,
+                     up_off, out, ldo, eps, ea);
+  return (int)hipGetLastError();
+}
+
+template <int EPI, bool NORM>
+int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off,
+                void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
+  switch (tile) {
+    case 1: return launch<256, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 2: return launch<128, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 3: return launch<128, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// Largest tile that still gives about one block per CU; N must divide.
+int pick_tile(int M, int N) {
+  const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};
+  int best = 0;
+  for (auto& c : cand) {
+    if (N % c[2]) continue;
+    const long blocks = (long)((M + c[1] - 1) / c[1]) * (N / c[2]);
+    if (!best) best = c[0];
+    if (blocks >= 240) return c[0];
+    best = c[0];
+  }
+  return best;
+}
+
+}  // namespace pgemm
+
+static int g_prefill_tile = 0;  // 0 = heuristic (benchmarks can force 1..3)
+
+// Used by the p2p_tiled_gemm* entry points (tiled_gemm.hip).  Returns
+// hipErrorInvalidValue if the shape does not tile (caller falls back).
+static int prefill_dispatch(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
+                         int norm, void* out, int ldo, float eps, const EpiArgs& ea,
+                         hipStream_t st) {
+  using namespace pgemm;
+  if (M <= 0 || K % BK) return (int)hipErrorInvalidValue;
+  int tile = g_prefill_tile ? g_prefill_tile : pick_tile(M, N);
+  const int bn = tile == 3 ? 128 : 256;
+  if (!tile || N % bn) return (int)hipErrorInvalidValue;
+  const int up_off = (epi == EPI_SILU) ? N / 32 : 0;
+  switch (epi) {
+    case EPI_STORE:
+      return norm ? launch_tile<EPI_STORE, true>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st)
+                  : launch_tile<EPI_STORE, false>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case EPI_RESID:
+      return launch_tile<EPI_RESID, false>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case EPI_SILU:
+      return launch_tile<EPI_SILU, true>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case EPI_F32:
+      return norm ? launch_tile<EPI_F32, true>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st)
+                  : launch_tile<EPI_F32, false>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case EPI_QKV_ROPE:
+      return launch_tile<EPI_QKV_ROPE, true>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case EPI_ARGMAX:
+      return launch_tile<EPI_ARGMAX, true>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+  }
+  return (int)hipErrorInvalidValue;
+}

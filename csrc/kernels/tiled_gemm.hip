@@ -17,6 +17,7 @@
 // NORM: each thread always loads the same 4 rows at the same k offset, so it
 // accumulates their sum of squares on the fly; 3 xor-shuffles finish each row.
 #include "gemm_epilogue.h"
+#include "prefill_gemm.h"
 
 namespace {
 
@@ -200,9 +201,21 @@ int launch_tiled(const void* Wt, const void* X, int ldx, int M, int K, int n_til
 // Same contract as p2p_skinny_gemm (+ the fused qkv/argmax variants through `ea`
 // fields set by the wrappers below) for any M; requires K % 64 == 0 and N % 128 == 0
 // (SiLU: (N/2) % 64 == 0).  Returns hipErrorInvalidValue if the shape does not tile.
+static int g_tiled_version = 2;  // 2 = LDS-DMA 8-wave kernel (prefill_gemm.h), 1 = register-staged
+
+// Benchmarks / A-B tests: version 1|2, tile 0 (heuristic) or 1..3 (256x256, 128x256, 128x128).
+P2P_API void p2p_tiled_gemm_config(int version, int tile) {
+  if (version == 1 || version == 2) g_tiled_version = version;
+  g_prefill_tile = (tile >= 0 && tile <= 3) ? tile : 0;
+}
+
 static int tiled_dispatch(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
                           int norm, void* out, int ldo, float eps, const EpiArgs& ea,
                           hipStream_t st) {
+  if (g_tiled_version == 2) {
+    const int e = prefill_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, ea, st);
+    if (e != (int)hipErrorInvalidValue) return e;
+  }
   if (M <= 0 || K % BK != 0 || N % BN != 0) return (int)hipErrorInvalidValue;
   const int n_tiles = N / BN;
   const int up_off = (epi == EPI_SILU) ? N / 32 : 0;

@@ -373,9 +373,21 @@ def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
 
 
 # ------------------------------------------------------------ tiled (prefill) GEMM
+TILED_CFGS = [(2, 0), (2, 1), (2, 2), (2, 3), (1, 0)]
+
+
+@pytest.fixture(params=TILED_CFGS, ids=lambda c: "v%d_t%d" % c)
+def tiled_cfg(request):
+    from p2p_llm_chat_go_amd.ops.gemm import tiled_config
+
+    tiled_config(*request.param)
+    yield request.param
+    tiled_config(2, 0)
+
+
 @pytest.mark.parametrize("M", [65, 200, 513])
 @pytest.mark.parametrize("epi", ["store", "store_norm", "resid", "silu", "f32"])
-def test_tiled_gemm(M, epi):
+def test_tiled_gemm(M, epi, tiled_cfg):
     torch.manual_seed(M)
     K, N = 1024, 768
     W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
@@ -404,19 +416,20 @@ def test_tiled_gemm(M, epi):
     assert _rel(out.cpu(), ref) < 1e-2
 
 
-def test_tiled_qkv_rope_and_argmax():
+@pytest.mark.parametrize("M", [150, 300])
+def test_tiled_qkv_rope_and_argmax(M, tiled_cfg):
     from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
 
     torch.manual_seed(0)
-    M, Hq, Hkv, K = 150, 4, 2, 512
+    Hq, Hkv, K = 4, 2, 512
     W = (torch.randn((Hq + 2 * Hkv) * 128, K) * 0.05).to(torch.bfloat16)
     Wt = ops.tile_weight(W[ops.rope_row_perm(Hq + 2 * Hkv)])
     x = torch.randn(M, K).to(torch.bfloat16)
     cs = rope_table(LLAMA31_8B, max_pos=512)
     pos = torch.arange(M, dtype=torch.int32)
-    slots = torch.randperm(4 * 64)[:M].to(torch.int32)
+    slots = torch.randperm(6 * 64)[:M].to(torch.int32)
     q_ref = torch.zeros(M, Hq * 128, dtype=torch.bfloat16)
-    kr = torch.zeros(4, Hkv, 64, 128, dtype=torch.bfloat16)
+    kr = torch.zeros(6, Hkv, 64, 128, dtype=torch.bfloat16)
     vr = torch.zeros_like(kr)
     ops.qkv_rope_gemm(Wt, x, pos, slots, cs, Hq, Hkv, q_ref, kr, vr)  # CPU reference path
     qd = torch.zeros_like(q_ref).to(DEV)
