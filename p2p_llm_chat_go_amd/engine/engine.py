@@ -58,12 +58,13 @@ class Engine:
     def __init__(self, cfg: ModelConfig, weights: EngineWeights | None = None, device="cuda",
                  seed: int = 0, kv_pages: int | None = None, max_prefill_tokens: int = 1024,
                  max_batch: int = 64, use_graph: bool = True, comm=None, tp_rank: int = 0,
-                 tp_size: int = 1, kv_fraction: float = 0.85):
+                 tp_size: int = 1, kv_fraction: float = 0.85, ep_rank: int = 0,
+                 ep_size: int = 1, ep_mode: str = "allreduce"):
         self.cfg = cfg
         self.device = torch.device(device)
         if weights is None:
             weights = EngineWeights.random(cfg, self.device, seed=seed, tp_rank=tp_rank,
-                                           tp_size=tp_size)
+                                           tp_size=tp_size, ep_rank=ep_rank, ep_size=ep_size)
         self.weights = weights
         if kv_pages is None:
             self.kv = KVCache.from_free_memory(cfg, self.device, fraction=kv_fraction,
@@ -73,6 +74,9 @@ class Engine:
         if comm is not None and hasattr(comm, "setup"):
             comm.setup(self.device)
         self.model = LlamaModel(weights, self.kv, comm)
+        # MoE expert parallelism: "allreduce" (replicated h) or "a2a" (DP attention,
+        # tokens dispatched to expert owners; ranks must step in lockstep)
+        self.model.ep_mode = ep_mode
         self.max_prefill_tokens = max_prefill_tokens
         # prefill chunks with at least this many rows use the MFMA flash kernel
         # (0 = always the per-row paged kernel)

@@ -6,9 +6,17 @@ Per layer, for R rows (chunks of <= 64 rows, the grouped kernel's M tile):
     act[s] = silu(g) * u of expert(s)        grouped_gemm SILU | NORM
     o[s]   = w[s] * act[s] @ W2_e            grouped_gemm STORE (row-scaled)
     h     += sum_k o[r*K + k]                moe_combine (EP/TP: partial + all-reduce)
-Expert parallelism: rank r owns experts [r*E/ep, (r+1)*E/ep); every rank routes
-all rows, computes its experts' contributions, and the partial sums are
-all-reduced (decode-size messages; see parallel/comm.py).
+Expert parallelism, two modes:
+* ``allreduce`` (default; TP or replicated attention): rank r owns experts
+  [r*E/ep, (r+1)*E/ep); every rank routes all rows (h is replicated), computes
+  its experts' contributions, and the partial sums are all-reduced.
+* ``a2a`` (DP attention + EP, ``moe_forward_a2a``): every rank serves its own
+  sequences; each (token, expert) pair is dispatched to the expert's owner with
+  one all-to-all, the owner runs its grouped GEMMs on everything it received,
+  and a second all-to-all returns the weighted outputs (SURVEY §2C EP row,
+  BASELINE config 5 "expert all-to-all over xGMI").  Slots per destination are
+  a static capacity (rows x top_k), so ranks must step in lockstep with equal
+  row counts (bench / lockstep serving) and the path is hipGraph-capturable.
 """
 from __future__ import annotations
 
@@ -48,6 +56,8 @@ def router_tiled(lw):
 def moe_forward(model, lw, ws, R):
     cfg = model.cfg
     w = model.w
+    if w.ep_size > 1 and getattr(model, "ep_mode", "allreduce") == "a2a":
+        return moe_forward_a2a(model, lw, ws, R)
     e_local = cfg.n_experts // w.ep_size
     e_lo = w.ep_rank * e_local
     if ws.moe is None:
@@ -72,3 +82,60 @@ def moe_forward(model, lw, ws, R):
             part = ws.partial[r0:r0 + rc]
             moe_ops.moe_combine(m.o, m.topk_ids, rc, K, e_lo, e_local, part, accumulate=False)
             model.comm.allreduce_add_(h, part)
+
+
+def moe_forward_a2a(model, lw, ws, R):
+    """DP-attention + EP MoE layer for this rank's R rows (see module doc)."""
+    cfg, w, comm = model.cfg, model.w, model.comm
+    E, K, H = cfg.n_experts, cfg.top_k, cfg.hidden
+    W = w.ep_size
+    El = E // W
+    C = R * K  # static per-destination capacity
+    dev = model.device
+    h = ws.h[:R]
+    logits = torch.empty(R, 16, device=dev, dtype=torch.float32)
+    for r0 in range(0, R, CHUNK):
+        rc = min(CHUNK, R - r0)
+        ops.skinny_gemm(router_tiled(lw), h[r0:r0 + rc], ops.EPI_F32, norm=True,
+                        out=logits[r0:r0 + rc], eps=cfg.eps)
+    p = torch.softmax(logits[:, :E], dim=-1)
+    tw, tid = p.topk(K, dim=-1)
+    tw = tw / tw.sum(-1, keepdim=True)
+    flat = tid.reshape(-1)                                     # [R*K] expert ids
+    dest = torch.div(flat, El, rounding_mode="floor")
+    onehot = torch.nn.functional.one_hot(dest, W)
+    pos = (onehot.cumsum(0) - 1).gather(1, dest[:, None]).squeeze(1)
+    slot = dest * C + pos                                      # unique send slot per pair
+    send_x = torch.zeros(W * C, H, device=dev, dtype=torch.bfloat16)
+    send_x.index_copy_(0, slot, h.repeat_interleave(K, dim=0))
+    meta = torch.full((W * C, 2), -1, device=dev, dtype=torch.int32)
+    meta[:, 1] = 0
+    meta.index_copy_(0, slot, torch.stack([(flat % El).to(torch.int32),
+                                           tw.reshape(-1).float().view(torch.int32)], 1))
+    recv_x = torch.empty_like(send_x)
+    recv_meta = torch.empty_like(meta)
+    comm.all_to_all_(recv_x, send_x)
+    comm.all_to_all_(recv_meta, meta)
+    lexp = recv_meta[:, 0]
+    row_w = recv_meta[:, 1].contiguous().view(torch.float32)
+    # per-local-expert slot lists (invalid slots sort last)
+    key = torch.where(lexp < 0, torch.full_like(lexp, El), lexp).long()
+    order = torch.argsort(key, stable=True).to(torch.int32)
+    counts = torch.bincount(key, minlength=El + 1)[:El]
+    offs = counts.cumsum(0) - counts
+    n = W * C
+    idx = (offs[:, None] + torch.arange(n, device=dev)[None]).clamp(max=n - 1)
+    rows = order[idx].contiguous()                             # [El, n]
+    Fs = lw.w13.shape[1] * 16 // 2
+    act = torch.empty(n, Fs, device=dev, dtype=torch.bfloat16)
+    o = torch.zeros(n, H, device=dev, dtype=torch.bfloat16)
+    for c0 in range(0, n, CHUNK):
+        cnt = (counts - c0).clamp(0, CHUNK).to(torch.int32)
+        rc = rows[:, c0:c0 + CHUNK]
+        moe_ops.grouped_gemm(lw.w13, cnt, rc, recv_x, 1, CHUNK, ops.EPI_SILU, act, norm=True,
+                             eps=cfg.eps)
+        moe_ops.grouped_gemm(lw.w2, cnt, rc, act, 1, CHUNK, ops.EPI_STORE, o, row_w=row_w)
+    back = torch.empty_like(o)
+    comm.all_to_all_(back, o)
+    contrib = back.index_select(0, slot).float().view(R, K, H).sum(1)
+    h.copy_((h.float() + contrib).to(h.dtype))

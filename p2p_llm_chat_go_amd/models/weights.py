@@ -128,13 +128,17 @@ class EngineWeights:
                ep_rank=0, ep_size=1) -> "EngineWeights":
         """Random-init weights generated directly in the tiled layout (see module doc)."""
         dev = torch.device(device)
+        # shared (replicated) weights depend on the TP shard only, so every EP rank
+        # holds the same attention / router / embeddings; experts use their own stream
         gen = torch.Generator(device=dev)
-        gen.manual_seed(seed * 1000003 + tp_rank * 7919 + ep_rank * 104729)
+        gen.manual_seed(seed * 1000003 + tp_rank * 7919)
+        egen = torch.Generator(device=dev)
+        egen.manual_seed(seed * 1000003 + tp_rank * 7919 + (ep_rank + 1) * 104729)
         H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
 
-        def rnd_tiled(n, k, s=std, lead=()):
+        def rnd_tiled(n, k, s=std, lead=(), g=gen):
             t = torch.empty(*lead, n // 16, k // 32, 64, 8, device=dev, dtype=torch.bfloat16)
-            t.normal_(0.0, s, generator=gen)
+            t.normal_(0.0, s, generator=g)
             return t
 
         qkv_rows = (cfg.n_heads + 2 * cfg.n_kv_heads) // tp_size * D
@@ -147,8 +151,8 @@ class EngineWeights:
                 el = cfg.n_experts // ep_size
                 lw.router = torch.empty(cfg.n_experts, H, device=dev, dtype=torch.bfloat16).normal_(
                     0.0, 0.5, generator=gen)
-                lw.w13 = rnd_tiled(2 * Fs, H, lead=(el,))
-                lw.w2 = rnd_tiled(H, Fs, lead=(el,))
+                lw.w13 = rnd_tiled(2 * Fs, H, lead=(el,), g=egen)
+                lw.w2 = rnd_tiled(H, Fs, lead=(el,), g=egen)
             else:
                 lw.gate_up = rnd_tiled(2 * Fs, H)
                 lw.down = rnd_tiled(H, Fs)

@@ -89,6 +89,21 @@ class TPComm:
         out.copy_(I.gather(0, best[None])[0].to(out.dtype))
         return out
 
+    def all_to_all_(self, out: torch.Tensor, inp: torch.Tensor):
+        """Equal-split all-to-all along dim 0 (pure data movement: bf16 pairs travel as
+        int32, which every backend moves; gloo has no 16-bit types)."""
+        a, b = out, inp
+        if out.dtype == torch.bfloat16:
+            a, b = out.view(torch.int32), inp.view(torch.int32)
+        if out.device.type == "cuda" and self.backend != "nccl":
+            # gloo moves host memory only (virtual ranks on one GPU in tests)
+            ah = torch.empty_like(a, device="cpu")
+            dist.all_to_all_single(ah, b.cpu(), group=self.group)
+            a.copy_(ah)
+            return out
+        dist.all_to_all_single(a, b, group=self.group)
+        return out
+
     def all_gather_rows(self, t: torch.Tensor):
         parts = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(parts, t, group=self.group)

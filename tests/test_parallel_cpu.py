@@ -22,7 +22,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q, moe):
+def _worker(rank, world, port, q, moe, a2a=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -37,6 +37,8 @@ def _worker(rank, world, port, q, moe):
             cfg = TINY_MIXTRAL.replace(n_heads=4, n_kv_heads=4)
         sd = random_state_dict(cfg, seed=3)
         prompts = [[1, 2, 3, 4, 5], list(range(10, 50))]
+        if a2a:  # DP attention: every rank serves its own peers (equal lengths: lockstep)
+            prompts = [[1 + rank, 2, 3 + 2 * rank, 4, 5], list(range(10 + rank, 50 + rank))]
         full = Engine(cfg, weights=EngineWeights.from_state_dict(sd, cfg, "cpu"), device="cpu",
                       kv_pages=32)
         ref = [r.tokens for r in full.generate(prompts, 6, stop_on_eos=False)]
@@ -45,7 +47,8 @@ def _worker(rank, world, port, q, moe):
             kw = dict(ep_rank=rank, ep_size=world)
         w = EngineWeights.from_state_dict(sd, cfg, "cpu", **kw)
         eng = Engine(cfg, weights=w, device="cpu", kv_pages=32, comm=TPComm(),
-                     tp_rank=w.tp_rank, tp_size=w.tp_size)
+                     tp_rank=w.tp_rank, tp_size=w.tp_size,
+                     ep_mode="a2a" if a2a else "allreduce")
         got = [r.tokens for r in eng.generate(prompts, 6, stop_on_eos=False)]
         q.put((rank, got == ref, got, ref))
     except Exception as e:  # report instead of hanging the parent
@@ -55,11 +58,11 @@ def _worker(rank, world, port, q, moe):
         dist.destroy_process_group()
 
 
-def _run(world, moe=False):
+def _run(world, moe=False, a2a=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a)) for r in range(world)]
     [p.start() for p in ps]
     res = [q.get(timeout=300) for _ in range(world)]
     [p.join(timeout=60) for p in ps]
@@ -74,6 +77,12 @@ def test_tensor_parallel_matches_single(world):
 
 def test_expert_parallel_matches_single():
     _run(2, moe=True)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_expert_parallel_all_to_all_dp_attention(world):
+    """EP with token dispatch/return by all-to-all (DP attention, distinct prompts per rank)."""
+    _run(world, moe=True, a2a=True)
 
 
 def test_u64_max_allreduce_ordering():

@@ -21,7 +21,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q, moe):
+def _worker(rank, world, port, q, moe, a2a=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -35,13 +35,16 @@ def _worker(rank, world, port, q, moe):
         cfg = base.replace(n_heads=4, n_kv_heads=4, ffn=512 if not moe else 256)
         sd = random_state_dict(cfg, seed=3)
         prompts = [[1, 2, 3, 4, 5], list(range(10, 90))]
+        if a2a:
+            prompts = [[1 + rank, 2, 3 + 2 * rank, 4, 5], list(range(10 + rank, 90 + rank))]
         full = Engine(cfg, weights=EngineWeights.from_state_dict(sd, cfg, "cuda"), device="cuda",
                       kv_pages=32, use_graph=False)
         ref = [r.tokens for r in full.generate(prompts, 6, stop_on_eos=False)]
         kw = dict(ep_rank=rank, ep_size=world) if moe else dict(tp_rank=rank, tp_size=world)
         w = EngineWeights.from_state_dict(sd, cfg, "cuda", **kw)
         eng = Engine(cfg, weights=w, device="cuda", kv_pages=32, comm=TPComm(),
-                     tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=False)
+                     tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=False,
+                     ep_mode="a2a" if a2a else "allreduce")
         got = [r.tokens for r in eng.generate(prompts, 6, stop_on_eos=False)]
         q.put((rank, got == ref, got, ref))
     except Exception:
@@ -51,13 +54,13 @@ def _worker(rank, world, port, q, moe):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("moe", [False, True])
-def test_virtual_rank_parallel_gpu(moe):
+@pytest.mark.parametrize("moe,a2a", [(False, False), (True, False), (True, True)])
+def test_virtual_rank_parallel_gpu(moe, a2a):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     world = 2
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a)) for r in range(world)]
     [p.start() for p in ps]
     res = [q.get(timeout=600) for _ in range(world)]
     [p.join(timeout=60) for p in ps]
