@@ -22,8 +22,9 @@ def main():
     ap.add_argument("--M", type=int, nargs="*", default=[288, 512, 2048, 8192])
     a = ap.parse_args()
     H, F = LLAMA31_8B.hidden, LLAMA31_8B.ffn
-    variants = [("v1", (1, 0)), ("v2_auto", (2, 0)), ("v2_256x256", (2, 1)),
-                ("v2_128x256", (2, 2)), ("v2_128x128", (2, 3))]
+    variants = [("v1", (1, 0, 0)), ("v2_auto", (2, 0, 0)), ("v2_256x256", (2, 1, 1)),
+                ("v2_128x256", (2, 2, 1)), ("v2_128x128", (2, 3, 1)),
+                ("v2_128x128_s2", (2, 3, 2)), ("v2_128x128_s4", (2, 3, 4))]
     for M in a.M:
         x = torch.randn(M, H, device="cuda").to(torch.bfloat16)
         xf = torch.randn(M, F, device="cuda").to(torch.bfloat16)
@@ -41,7 +42,7 @@ def main():
                 t = graph_time(lambda i: fn(W), n_inner=10)
                 print(json.dumps({"M": M, "gemm": name, "variant": vname, "us": round(t, 1),
                                   "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1)}), flush=True)
-            tiled_config(2, 0)
+            tiled_config(2, 0, 0)
             Wb = torch.randn(K, N, device="cuda").to(torch.bfloat16)
             xin = x if K == H else xf
             t = graph_time(lambda i: torch.matmul(xin, Wb), n_inner=10)

@@ -18,6 +18,8 @@
 // NORM: the waves of column 0 also square the A fragments they read; a lane
 // sees 8 of every 32 k of one row, 3 shuffles finish the row's sum.
 #pragma once
+#include <algorithm>
+
 #include "gemm_epilogue.h"
 
 namespace pgemm {
@@ -27,12 +29,20 @@ constexpr int NT = 512;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int BM, int BN, int EPI, bool NORM>
+struct SplitArgs {
+  int splitk;          // K slices per output tile (1 = no split)
+  f32x4* slab;         // [tiles][splitk][FM*FN][NT] partial accumulators
+  float* ss_slab;      // [tiles][splitk][BM] partial row sums of squares
+  unsigned* counters;  // [tiles], zeroed before the launch
+};
+
+template <int BM, int BN, int EPI, bool NORM, bool SPLIT>
 __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restrict__ Wt,
                                                           const bf16* __restrict__ X, int ldx,
                                                           int M, int K, int m_tiles, int n_tiles,
                                                           int up_off, void* __restrict__ out,
-                                                          int ldo, float eps, EpiArgs ea) {
+                                                          int ldo, float eps, EpiArgs ea,
+                                                          SplitArgs sp) {
   constexpr int FM = BM / 32;        // 16-row fragments per wave
   constexpr int FN = BN / 64;        // 16-col groups per wave
   constexpr int AB = BM / 16 * 2;    // A fragment blocks per stage (x 1 KiB)
@@ -42,14 +52,18 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   static_assert(AB % 8 == 0 && BB % 8 == 0, "tile");
   __shared__ __attribute__((aligned(16))) bf16x8 lds[2 * STAGE];
 
-  const int nb = m_tiles * n_tiles;
+  const int splitk = SPLIT ? sp.splitk : 1;
+  const int nb = m_tiles * n_tiles * splitk;
   const int b = xcd_remap(blockIdx.x, nb);
-  const int mt_i = b % m_tiles, nt_i = b / m_tiles;
+  // a tile's K slices are consecutive (same XCD: the reducer reads them from its L2)
+  const int tile = b / splitk, split = b % splitk;
+  const int mt_i = tile % m_tiles, nt_i = tile / m_tiles;
   const int m0 = mt_i * BM;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;
   const int S = K >> 5;
-  const int nk = K / BK;
+  const int nk_all = K / BK;
+  const int kt0 = split * nk_all / splitk, kt1 = (split + 1) * nk_all / splitk;
 
   auto group_of = [&](int gi) -> int {  // LDS group slot -> global 16-col group
     if constexpr (EPI == EPI_SILU) {
@@ -109,12 +123,12 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   for (int i = 0; i < FM; ++i) ss[i] = 0.f;
   const bool do_ss = NORM && wn == 0;
 
-  issue(0, 0);
+  issue(kt0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    if (kt + 1 < kt1) issue(kt + 1, cur ^ 1);
     const bf16x8* sa = lds + cur * STAGE;
     const bf16x8* sb = sa + AB * 64;
 #pragma unroll
@@ -152,10 +166,61 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
         float v = ss[i];
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
-        if (lane < 16) ss_row[wm * (BM / 2) + 16 * i + lane] = v;
+        if (lane < 16) {
+          if constexpr (SPLIT)
+            sp.ss_slab[((size_t)tile * splitk + split) * BM + wm * (BM / 2) + 16 * i + lane] = v;
+          else
+            ss_row[wm * (BM / 2) + 16 * i + lane] = v;
+        }
       }
     }
+    if constexpr (!SPLIT) __syncthreads();
+  }
+  if constexpr (SPLIT) {
+    // split-K hand-off (agent-scope release/acquire through a per-tile ticket):
+    // every slice stores its fp32 partial tile, the last arriver reduces all
+    // slices in slice order (deterministic) and runs the epilogue.
+    f32x4* my = sp.slab + ((size_t)tile * splitk + split) * (FM * FN) * NT;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) my[(i * FN + j) * NT + tid] = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds) + BM;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(&sp.counters[tile], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (t == (unsigned)splitk - 1);
+    }
+    __syncthreads();
+    if (!*flag) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const f32x4* base = sp.slab + (size_t)tile * splitk * (FM * FN) * NT;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s2 = 0; s2 < splitk; ++s2) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += base[((size_t)s2 * FM * FN + i * FN + j) * NT + tid];
+    }
+    if constexpr (NORM) {
+      if (tid < BM) {
+        float t = 0.f;
+        for (int s2 = 0; s2 < splitk; ++s2) t += sp.ss_slab[((size_t)tile * splitk + s2) * BM + tid];
+        ss_row[tid] = t;
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue ----
@@ -199,14 +264,61 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   }
 }
 
+// split-K workspace (device, grown on demand outside graph capture)
+struct SplitWs {
+  void* buf = nullptr;
+  size_t bytes = 0;
+};
+static SplitWs g_split_ws;
+
+static bool split_ws(size_t bytes, hipStream_t st, char** out) {
+  if (g_split_ws.bytes < bytes) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) return false;  // cannot allocate while capturing
+    hipStreamSynchronize(st);
+    if (g_split_ws.buf) hipFree(g_split_ws.buf);
+    g_split_ws.buf = nullptr;
+    g_split_ws.bytes = 0;
+    if (hipMalloc(&g_split_ws.buf, bytes) != hipSuccess) return false;
+    g_split_ws.bytes = bytes;
+  }
+  *out = (char*)g_split_ws.buf;
+  return true;
+}
+
+static int g_splitk = 0;  // 0 = heuristic, 1 = never split, >1 = forced
+
 template <int BM, int BN, int EPI, bool NORM>
 int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off, void* out,
            int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   const int m_tiles = (M + BM - 1) / BM;
   const int n_tiles = N / BN;
-  hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM>), dim3(m_tiles * n_tiles), dim3(NT),
-                     0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, m_tiles, n_tiles,
-                     up_off, out, ldo, eps, ea);
+  const int tiles = m_tiles * n_tiles;
+  const int nk = K / BK;
+  // too few tiles to fill 256 CUs: split K so every CU gets work (>= 4 k-tiles per slice)
+  int splitk = g_splitk ? g_splitk : 1;
+  if (!g_splitk && tiles < 160) splitk = std::min(8, std::max(1, 256 / tiles));
+  splitk = std::max(1, std::min(splitk, nk / 4));
+  if (splitk > 1) {
+    constexpr int FM = BM / 32, FN = BN / 64;
+    const size_t slab = (size_t)tiles * splitk * FM * FN * NT * sizeof(f32x4);
+    const size_t ssb = (size_t)tiles * splitk * BM * sizeof(float);
+    const size_t cnt = (size_t)tiles * sizeof(unsigned);
+    char* ws = nullptr;
+    if (split_ws(slab + ssb + cnt, st, &ws)) {
+      SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), (unsigned*)(ws + slab + ssb)};
+      hipMemsetAsync(sp.counters, 0, cnt, st);
+      hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, true>),
+                         dim3(tiles * splitk), dim3(NT), 0, st, (const bf16x8*)Wt,
+                         (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, sp);
+      return (int)hipGetLastError();
+    }
+  }
+  SplitArgs none{1, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, false>), dim3(tiles), dim3(NT), 0,
+                     st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off,
+                     out, ldo, eps, ea, none);
   return (int)hipGetLastError();
 }
 

@@ -102,7 +102,7 @@ def lib():
             fn.restype = ctypes.c_size_t
         fn = getattr(L, "p2p_tiled_gemm_config", None)
         if fn is not None:
-            fn.argtypes = [c_int, c_int]
+            fn.argtypes = [c_int, c_int, c_int]
             fn.restype = None
         fn = getattr(L, "p2p_skinny_gemm_tune", None)
         if fn is not None:

@@ -44,10 +44,11 @@ def use_tiled(M, N, K, epi) -> bool:
     return (N // 2) % 64 == 0 if epi == EPI_SILU else N % 128 == 0
 
 
-def tiled_config(version: int = 2, tile: int = 0):
+def tiled_config(version: int = 2, tile: int = 0, splitk: int = 0):
     """Prefill GEMM selection: version 2 = 8-wave LDS-DMA kernel (tile 0 = heuristic,
-    1 = 256x256, 2 = 128x256, 3 = 128x128), version 1 = register-staged 128x128."""
-    _lib.lib().p2p_tiled_gemm_config(int(version), int(tile))
+    1 = 256x256, 2 = 128x256, 3 = 128x128; splitk 0 = heuristic, 1 = off, n = forced),
+    version 1 = register-staged 128x128."""
+    _lib.lib().p2p_tiled_gemm_config(int(version), int(tile), int(splitk))
 
 
 def _code(wt, M, epi, norm, waves):

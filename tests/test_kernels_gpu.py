@@ -373,16 +373,16 @@ def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
 
 
 # ------------------------------------------------------------ tiled (prefill) GEMM
-TILED_CFGS = [(2, 0), (2, 1), (2, 2), (2, 3), (1, 0)]
+TILED_CFGS = [(2, 0, 0), (2, 1, 1), (2, 2, 1), (2, 3, 1), (2, 3, 4), (2, 1, 3), (1, 0, 0)]
 
 
-@pytest.fixture(params=TILED_CFGS, ids=lambda c: "v%d_t%d" % c)
+@pytest.fixture(params=TILED_CFGS, ids=lambda c: "v%d_t%d_s%d" % c)
 def tiled_cfg(request):
     from p2p_llm_chat_go_amd.ops.gemm import tiled_config
 
     tiled_config(*request.param)
     yield request.param
-    tiled_config(2, 0)
+    tiled_config(2, 0, 0)
 
 
 @pytest.mark.parametrize("M", [65, 200, 513])
