@@ -10,7 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from p2p_llm_chat_go_amd import ops  # noqa: E402
-from p2p_llm_chat_go_amd.ops.gemm import tiled_config  # noqa: E402
+from p2p_llm_chat_go_amd.ops.gemm import set_tiled_min_m, tiled_config  # noqa: E402
 from p2p_llm_chat_go_amd.models.config import LLAMA31_8B  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -19,7 +19,7 @@ from kernel_bench import graph_time  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--M", type=int, nargs="*", default=[288, 512, 2048, 8192])
+    ap.add_argument("--M", type=int, nargs="*", default=[36, 64, 288, 512, 2048, 8192])
     a = ap.parse_args()
     H, F = LLAMA31_8B.hidden, LLAMA31_8B.ffn
     variants = [("v1", (1, 0, 0)), ("v2_auto", (2, 0, 0)), ("v2_256x256", (2, 1, 1)),
@@ -37,11 +37,19 @@ def main():
             ("down", H, F, lambda W: ops.skinny_gemm(W, xf, ops.EPI_RESID, out=h))]:
             W = (torch.randn(N // 16, K // 32, 64, 8, device="cuda") * 0.02).to(torch.bfloat16)
             flops = 2 * M * N * K
-            for vname, cfg in variants:
-                tiled_config(*cfg)
+            vs = variants
+            if M <= 64:  # decode-style skinny kernel vs the split-K tiled kernel
+                vs = [("skinny", None), ("v2_auto", (2, 0, 0)), ("v2_128x128_s4", (2, 3, 4)),
+                      ("v2_128x128_s8", (2, 3, 8)), ("v2_128x256_s8", (2, 2, 8))]
+            for vname, cfg in vs:
+                set_tiled_min_m(65 if cfg is None else 1)
+                if cfg is not None:
+                    tiled_config(*cfg)
                 t = graph_time(lambda i: fn(W), n_inner=10)
                 print(json.dumps({"M": M, "gemm": name, "variant": vname, "us": round(t, 1),
-                                  "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1)}), flush=True)
+                                  "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1),
+                                  "TBps": round(N * K * 2 / (t * 1e-6) / 1e12, 2)}), flush=True)
+            set_tiled_min_m(65)
             tiled_config(2, 0, 0)
             Wb = torch.randn(K, N, device="cuda").to(torch.bfloat16)
             xin = x if K == H else xf

@@ -297,8 +297,8 @@ int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_o
   const int tiles = m_tiles * n_tiles;
   const int nk = K / BK;
   // too few tiles to fill 256 CUs: split K so every CU gets work (>= 4 k-tiles per slice)
-  int splitk = g_splitk ? g_splitk : 1;
-  if (!g_splitk && tiles < 160) splitk = std::min(8, std::max(1, 256 / tiles));
+  // (measured on MI355X at 8B shapes: ~400 blocks is the sweet spot for long-K tiles)
+  int splitk = g_splitk ? g_splitk : std::min(8, std::max(1, 400 / tiles));
   splitk = std::max(1, std::min(splitk, nk / 4));
   if (splitk > 1) {
     constexpr int FM = BM / 32, FN = BN / 64;
@@ -341,7 +341,7 @@ int pick_tile(int M, int N) {
     if (N % c[2]) continue;
     const long blocks = (long)((M + c[1] - 1) / c[1]) * (N / c[2]);
     if (!best) best = c[0];
-    if (blocks >= 240) return c[0];
+    if (blocks >= 200) return c[0];
     best = c[0];
   }
   return best;

@@ -37,9 +37,17 @@ def set_tune(key, code: int):
     _TUNE[key] = int(code)
 
 
+TILED_MIN_M = SKINNY_MAX_M + 1  # rows from which the tiled kernel is used (bench override)
+
+
+def set_tiled_min_m(m: int):
+    global TILED_MIN_M
+    TILED_MIN_M = int(m)
+
+
 def use_tiled(M, N, K, epi) -> bool:
     """Prefill-sized M goes to the LDS-tiled MFMA kernel (compute-bound), decode to skinny."""
-    if M <= SKINNY_MAX_M or K % 64:
+    if M < TILED_MIN_M or K % 64:
         return False
     return (N // 2) % 64 == 0 if epi == EPI_SILU else N % 128 == 0
 
