@@ -213,6 +213,24 @@ PYBIND11_MODULE(_native, m) {
           return Json::parse(out);
         });
       })
+      .def("set_generate_stream_hook", [](Node& n, py::function fn) {
+        // fn(req_text, emit) -> final_text, emit(chunk_text) -> bool (called under the GIL)
+        auto holder = std::make_shared<py::function>(std::move(fn));
+        n.set_generate_stream_hook(
+            [holder](const Json& req, const std::function<bool(const Json&)>& emit) -> Json {
+              std::string out;
+              {
+                py::gil_scoped_acquire g;
+                py::cpp_function py_emit([&emit](const std::string& chunk) {
+                  Json c = Json::parse(chunk);
+                  py::gil_scoped_release rel;  // socket write without the GIL
+                  return emit(c);
+                });
+                out = py::str((*holder)(req.dump(), py_emit));
+              }
+              return Json::parse(out);
+            });
+      })
       .def("metrics", [](Node& n) { return n.metrics_json().dump(); });
 
   // ---- directory ----

@@ -276,6 +276,11 @@ Node::Node(NodeConfig cfg)
 
 Node::~Node() { stop(); }
 
+void Node::set_generate_stream_hook(GenerateStreamHook h) {
+  std::lock_guard<std::mutex> lk(hook_mu_);
+  stream_hook_ = std::move(h);
+}
+
 void Node::set_generate_hook(GenerateHook h) {
   std::lock_guard<std::mutex> lk(hook_mu_);
   hook_ = std::move(h);
@@ -529,6 +534,24 @@ void Node::install_routes() {
       return;
     }
     bool stream = j.get_bool("stream", true);  // Ollama default: streaming
+    GenerateStreamHook sh;
+    {
+      std::lock_guard<std::mutex> lk(hook_mu_);
+      sh = stream_hook_;
+    }
+    if (stream && sh) {  // token-by-token NDJSON from the in-process engine
+      n_suggest_++;
+      res.set_header("Content-Type", "application/x-ndjson");
+      res.stream = [sh, j](const std::function<bool(const std::string&)>& w) {
+        try {
+          Json fin = sh(j, [&](const Json& c) { return w(c.dump() + "\n"); });
+          w(fin.dump() + "\n");
+        } catch (const std::exception& e) {
+          w(err(e.what()).dump() + "\n");
+        }
+      };
+      return;
+    }
     Json out;
     try {
       out = generate(j);
@@ -558,6 +581,24 @@ void Node::install_routes() {
     try {
       j = Json::parse(req.body);
       j.set("endpoint", "chat");
+      GenerateStreamHook sh;
+      {
+        std::lock_guard<std::mutex> lk(hook_mu_);
+        sh = stream_hook_;
+      }
+      if (j.get_bool("stream", true) && sh) {
+        n_suggest_++;
+        res.set_header("Content-Type", "application/x-ndjson");
+        res.stream = [sh, j](const std::function<bool(const std::string&)>& w) {
+          try {
+            Json fin = sh(j, [&](const Json& c) { return w(c.dump() + "\n"); });
+            w(fin.dump() + "\n");
+          } catch (const std::exception& e) {
+            w(err(e.what()).dump() + "\n");
+          }
+        };
+        return;
+      }
       Json out = generate(j);
       res.json(200, out);
     } catch (const std::exception& e) {

@@ -103,6 +103,10 @@ struct NodeConfig {
 
 // Engine hook: Ollama /api/generate request JSON -> response JSON (in-process engine).
 using GenerateHook = std::function<Json(const Json& req)>;
+// Streaming engine hook: emit(chunk) per token batch (false = client gone); returns
+// the final `done: true` object.
+using GenerateStreamHook =
+    std::function<Json(const Json& req, const std::function<bool(const Json&)>& emit)>;
 
 class Node {
  public:
@@ -117,6 +121,7 @@ class Node {
   std::string peer_id() const { return host_ ? host_->id().to_base58() : ""; }
   std::vector<std::string> addrs() const { return addrs_; }
   void set_generate_hook(GenerateHook h);
+  void set_generate_stream_hook(GenerateStreamHook h);
   Inbox& inbox() { return inbox_; }
   std::shared_ptr<Host> host() { return host_; }
   Kad* kad() { return kad_.get(); }
@@ -138,6 +143,7 @@ class Node {
   std::vector<std::string> addrs_;
   std::mutex hook_mu_;
   GenerateHook hook_;
+  GenerateStreamHook stream_hook_;
   std::thread refresher_;
   std::atomic<bool> stopping_{false};
   std::atomic<long> n_sent_{0}, n_recv_{0}, n_suggest_{0}, n_send_fail_{0};

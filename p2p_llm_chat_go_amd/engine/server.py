@@ -57,10 +57,13 @@ class EngineServer:
         self._thread.start()
 
     # --------------------------------------------------------------- API
-    def submit(self, prompt_ids: list, params: SamplingParams) -> Future:
+    def submit(self, prompt_ids: list, params: SamplingParams, on_tokens=None) -> Future:
+        """Queue a request.  on_tokens(list[int]) is called from the engine thread with
+        every batch of newly generated tokens (streaming), before the future resolves."""
         fut = Future()
         with self._lock:
-            self._pending.append((list(prompt_ids), params, fut, time.perf_counter_ns()))
+            self._pending.append((list(prompt_ids), params, fut, time.perf_counter_ns(),
+                                  on_tokens))
             self._lock.notify()
         return fut
 
@@ -109,18 +112,96 @@ class EngineServer:
             out["context"] = []
         return json.dumps(out)
 
+    def handle_json_stream(self, req_text: str, emit) -> str:
+        """Ollama streaming (NDJSON): emit(chunk_json_text) -> bool per token batch;
+        returns the final ``done: true`` object (stats, empty response)."""
+        import queue
+
+        req = json.loads(req_text)
+        params = SamplingParams.from_ollama(req.get("options"), self.default_max_tokens)
+        chat = req.get("endpoint") == "chat"
+        if chat:
+            msgs = req.get("messages") or []
+            ids = self.tok.chat_ids("\n".join(m.get("content", "") for m in msgs
+                                               if m.get("role") != "system"))
+        elif req.get("raw"):
+            ids = self.tok.encode(req.get("prompt", ""), bos=True)
+        else:
+            ids = self.tok.chat_ids(req.get("prompt", ""))
+        q = queue.Queue()
+        fut = self.submit(ids, params, on_tokens=q.put)
+        model = req.get("model", self.model_name)
+        toks, text_sent, alive = [], "", True
+
+        def now():
+            return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime()) + ".000000Z"
+
+        def flush(final=False):
+            nonlocal text_sent, alive
+            text = self.tok.decode(toks)
+            if not final and text.endswith("\ufffd"):
+                return  # incomplete UTF-8 sequence: wait for the next token
+            delta = text[len(text_sent):] if text.startswith(text_sent) else text
+            text_sent = text
+            if not delta or not alive:
+                return
+            chunk = {"model": model, "created_at": now(), "done": False}
+            if chat:
+                chunk["message"] = {"role": "assistant", "content": delta}
+            else:
+                chunk["response"] = delta
+            alive = bool(emit(json.dumps(chunk)))
+
+        while True:
+            try:
+                toks += q.get(timeout=0.05)
+                flush()
+            except queue.Empty:
+                if fut.done() and q.empty():
+                    break
+        r = fut.result()
+        toks = r["tokens"]
+        flush(final=True)
+        out = {"model": model, "created_at": now(), "done": True,
+               "done_reason": r["done_reason"], "total_duration": r["total_duration"],
+               "load_duration": 0, "prompt_eval_count": r["prompt_eval_count"],
+               "prompt_eval_duration": r["prompt_eval_duration"], "eval_count": r["eval_count"],
+               "eval_duration": r["eval_duration"]}
+        if chat:
+            out["message"] = {"role": "assistant", "content": ""}
+        else:
+            out["response"] = ""
+            out["context"] = []
+        return json.dumps(out)
+
     # --------------------------------------------------------------- loop
     def _admit_pending(self):
         with self._lock:
             pend, self._pending = self._pending, []
-        for prompt, params, fut, t0 in pend:
+        for prompt, params, fut, t0, cb in pend:
             try:
                 rid = self.sched.add(len(prompt), params.max_tokens, params.stop_on_eos,
                                      list(self.engine.cfg.eos_ids))
             except Exception as e:  # too long / bad request
                 fut.set_exception(e)
                 continue
-            self._reqs[rid] = {"prompt": prompt, "params": params, "future": fut, "t_submit": t0}
+            self._reqs[rid] = {"prompt": prompt, "params": params, "future": fut, "t_submit": t0,
+                               "cb": cb, "streamed": 0}
+
+    def _stream(self, rids):
+        """Hand newly accepted tokens of streaming requests to their callbacks."""
+        for rid in rids:
+            r = self._reqs.get(rid)
+            if r is None or r["cb"] is None:
+                continue
+            toks = list(self.sched.get(rid).tokens)
+            if len(toks) > r["streamed"]:
+                new = toks[r["streamed"]:]
+                r["streamed"] = len(toks)
+                try:
+                    r["cb"](new)
+                except Exception:  # a broken consumer must not stop the engine
+                    r["cb"] = None
 
     def _loop(self):
         eng = self.engine
@@ -159,6 +240,7 @@ class EngineServer:
             for i, tkn in zip(plan.prefill, first):
                 self._reqs[i]["t_first"] = t1
                 self.sched.on_first_token(i, int(tkn))
+            self._stream(plan.prefill)
         running = [i for i in list(plan.decode) + list(plan.prefill)
                    if self.sched.get(i).state == 1]
         if running:
@@ -185,10 +267,12 @@ class EngineServer:
         hist = st.hist[:len(running), :k].cpu().tolist()
         self.stats["decode_steps"] += k
         self.sched.on_decode_tokens(running, hist)
+        self._stream(running)
 
     def _retire(self):
         now = time.perf_counter_ns()
         for rid in self.sched.take_finished():
+            self._stream([rid])
             r = self._reqs.pop(rid, None)
             sr = self.sched.get(rid)
             if r is not None and not r["future"].done():

@@ -70,6 +70,7 @@ def main(argv=None):
     if os.environ.get("ENGINE", "1") != "0":
         server = build_engine_server()
         node.set_generate_hook(server.handle_json)
+        node.set_generate_stream_hook(server.handle_json_stream)
     try:
         node.start()
     except Exception as e:  # log.Fatal("directory register failed:", err)

@@ -127,6 +127,7 @@ def test_nodes_with_inprocess_engine():
                         "listen": ["/ip4/127.0.0.1/tcp/0"]})
             if name == "B":
                 n.set_generate_hook(srv.handle_json)
+                n.set_generate_stream_hook(srv.handle_json_stream)
             n.start()
             nodes.append(n)
         a = "http://127.0.0.1:%d" % nodes[0].http_port
@@ -147,11 +148,22 @@ def test_nodes_with_inprocess_engine():
                       "following message:\n\nHey! How's it going?\n\nReply:"}, timeout=60)
         g = json.loads(body)
         assert st == 200 and g["done"] and "response" in g and g["eval_count"] > 0
-        # streaming NDJSON (Ollama default)
-        st, body, hdr = http("POST", b + "/api/generate", {"prompt": "x", "options": {"num_predict": 3}},
-                             timeout=60)
+        # streaming NDJSON (Ollama default): token-by-token chunks, then the stats object;
+        # the concatenated stream equals the non-streamed greedy reply
+        req = {"prompt": "x", "options": {"num_predict": 12}}
+        st, body, hdr = http("POST", b + "/api/generate", req, timeout=60)
         lines = [json.loads(x) for x in body.strip().split("\n")]
-        assert st == 200 and lines[-1]["done"] is True and lines[0]["done"] is False
+        assert st == 200 and hdr["Content-Type"].startswith("application/x-ndjson")
+        assert lines[-1]["done"] is True and lines[-1]["eval_count"] > 0
+        assert len(lines) >= 3 and all(x["done"] is False for x in lines[:-1])
+        streamed = "".join(x["response"] for x in lines[:-1])
+        full = json.loads(http("POST", b + "/api/generate", dict(req, stream=False),
+                               timeout=60)[1])["response"]
+        assert streamed == full
+        st, body, _ = http("POST", b + "/api/chat", {"messages": [{"role": "user", "content": "x"}],
+                                                     "options": {"num_predict": 6}}, timeout=60)
+        chunks = [json.loads(x) for x in body.strip().split("\n")]
+        assert chunks[-1]["done"] is True and chunks[0]["message"]["role"] == "assistant"
         # one-click suggest + send back to the original sender
         st, body, _ = http("POST", b + "/suggest", {"id": mid, "send": True,
                                                     "options": {"num_predict": 5}}, timeout=60)
