@@ -39,8 +39,10 @@ def main():
             flops = 2 * M * N * K
             vs = variants
             if M <= 64:  # decode-style skinny kernel vs the split-K tiled kernel
-                vs = [("skinny", None), ("v2_auto", (2, 0, 0)), ("v2_128x128_s4", (2, 3, 4)),
-                      ("v2_128x128_s8", (2, 3, 8)), ("v2_128x256_s8", (2, 2, 8))]
+                vs = [("skinny", None), ("v2_auto", (2, 0, 0)), ("v2_64x128", (2, 4, 1)),
+                      ("v2_64x128_s2", (2, 4, 2)), ("v2_64x128_s4", (2, 4, 4)),
+                      ("v2_64x128_s8", (2, 4, 8)), ("v2_64x256", (2, 5, 1)),
+                      ("v2_64x256_s2", (2, 5, 2)), ("v2_128x128_s4", (2, 3, 4))]
             for vname, cfg in vs:
                 set_tiled_min_m(65 if cfg is None else 1)
                 if cfg is not None:

@@ -36,21 +36,40 @@ struct SplitArgs {
   unsigned* counters;  // [tiles], zeroed before the launch
 };
 
-template <int BM, int BN, int EPI, bool NORM, bool SPLIT>
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Waits until at most `pending` x L of this thread's LDS-DMA loads are in flight.
+template <int L, int STAGES>
+__device__ __forceinline__ void wait_tiles(int pending) {
+  if constexpr (STAGES >= 4) {
+    if (pending >= 2) { wait_vmcnt<2 * L>(); return; }
+  }
+  if constexpr (STAGES >= 3) {
+    if (pending >= 1) { wait_vmcnt<L>(); return; }
+  }
+  wait_vmcnt<0>();
+}
+
+template <int BM, int BN, int EPI, bool NORM, bool SPLIT, int STAGES>
 __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restrict__ Wt,
                                                           const bf16* __restrict__ X, int ldx,
                                                           int M, int K, int m_tiles, int n_tiles,
                                                           int up_off, void* __restrict__ out,
                                                           int ldo, float eps, EpiArgs ea,
                                                           SplitArgs sp) {
-  constexpr int FM = BM / 32;        // 16-row fragments per wave
+  constexpr int FM = BM / 32;        // 16-row fragments per wave (2 x 4 wave grid)
   constexpr int FN = BN / 64;        // 16-col groups per wave
   constexpr int AB = BM / 16 * 2;    // A fragment blocks per stage (x 1 KiB)
   constexpr int BB = BN / 16 * 2;    // B fragment blocks per stage
   constexpr int STAGE = (AB + BB) * 64;  // bf16x8 per stage
   constexpr int AI = AB / 8, BI = BB / 8;  // blocks per wave per stage
+  constexpr int L = AI + BI;               // LDS-DMA instructions per thread per stage
   static_assert(AB % 8 == 0 && BB % 8 == 0, "tile");
-  __shared__ __attribute__((aligned(16))) bf16x8 lds[2 * STAGE];
+  static_assert(FM >= 1 && FN >= 2, "tile");
+  __shared__ __attribute__((aligned(16))) bf16x8 lds[STAGES * STAGE];
 
   const int splitk = SPLIT ? sp.splitk : 1;
   const int nb = m_tiles * n_tiles * splitk;
@@ -64,6 +83,7 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   const int S = K >> 5;
   const int nk_all = K / BK;
   const int kt0 = split * nk_all / splitk, kt1 = (split + 1) * nk_all / splitk;
+  const int n = kt1 - kt0;
 
   auto group_of = [&](int gi) -> int {  // LDS group slot -> global 16-col group
     if constexpr (EPI == EPI_SILU) {
@@ -123,13 +143,17 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   for (int i = 0; i < FM; ++i) ss[i] = 0.f;
   const bool do_ss = NORM && wn == 0;
 
-  issue(kt0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    if (kt + 1 < kt1) issue(kt + 1, cur ^ 1);
-    const bf16x8* sa = lds + cur * STAGE;
+  // ---- STAGES-deep LDS-DMA pipeline: counted vmcnt + raw barriers, so the
+  // younger stages stay in flight across the barrier (no vmcnt(0) drain) ----
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t)
+    if (t < n) issue(kt0 + t, t);
+  for (int t = 0; t < n; ++t) {
+    wait_tiles<L, STAGES>(min(STAGES - 2, n - 1 - t));  // tile t landed (this thread's part)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                       // ... and every other wave's part
+    if (t + STAGES - 1 < n) issue(kt0 + t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    const bf16x8* sa = lds + (t % STAGES) * STAGE;
     const bf16x8* sb = sa + AB * 64;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -153,9 +177,9 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
           }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  wait_vmcnt<0>();
+  __syncthreads();  // every wave done reading the stages before LDS is reused below
 
   // ---- row rstd (NORM): column-0 waves publish through LDS (stages are free now) ----
   float* ss_row = reinterpret_cast<float*>(lds);
@@ -274,10 +298,10 @@ static SplitWs g_split_ws;
 static bool split_ws(size_t bytes, hipStream_t st, char** out) {
   if (g_split_ws.bytes < bytes) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    hipStreamIsCapturing(st, &cs);
+    (void)hipStreamIsCapturing(st, &cs);
     if (cs != hipStreamCaptureStatusNone) return false;  // cannot allocate while capturing
-    hipStreamSynchronize(st);
-    if (g_split_ws.buf) hipFree(g_split_ws.buf);
+    (void)hipStreamSynchronize(st);
+    if (g_split_ws.buf) (void)hipFree(g_split_ws.buf);
     g_split_ws.buf = nullptr;
     g_split_ws.bytes = 0;
     if (hipMalloc(&g_split_ws.buf, bytes) != hipSuccess) return false;
@@ -289,9 +313,18 @@ static bool split_ws(size_t bytes, hipStream_t st, char** out) {
 
 static int g_splitk = 0;  // 0 = heuristic, 1 = never split, >1 = forced
 
+// LDS stages per tile shape (<= 160 KiB of LDS per CU): deeper pipelines where a stage is small
+template <int BM, int BN>
+constexpr int stages_for() {
+  constexpr int stage_kb = (BM + BN) * BK * 2 / 1024;
+  constexpr int fit = 160 / stage_kb;
+  return fit >= 4 ? 4 : (fit >= 2 ? fit : 2);
+}
+
 template <int BM, int BN, int EPI, bool NORM>
 int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off, void* out,
            int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
+  constexpr int STAGES = stages_for<BM, BN>();
   const int m_tiles = (M + BM - 1) / BM;
   const int n_tiles = N / BN;
   const int tiles = m_tiles * n_tiles;
@@ -308,15 +341,15 @@ int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_o
     char* ws = nullptr;
     if (split_ws(slab + ssb + cnt, st, &ws)) {
       SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), (unsigned*)(ws + slab + ssb)};
-      hipMemsetAsync(sp.counters, 0, cnt, st);
-      hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, true>),
+      (void)hipMemsetAsync(sp.counters, 0, cnt, st);
+      hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, true, STAGES>),
                          dim3(tiles * splitk), dim3(NT), 0, st, (const bf16x8*)Wt,
                          (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, sp);
       return (int)hipGetLastError();
     }
   }
   SplitArgs none{1, nullptr, nullptr, nullptr};
-  hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, false>), dim3(tiles), dim3(NT), 0,
+  hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, false, STAGES>), dim3(tiles), dim3(NT), 0,
                      st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off,
                      out, ldo, eps, ea, none);
   return (int)hipGetLastError();
@@ -329,12 +362,16 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
     case 1: return launch<256, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 2: return launch<128, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 3: return launch<128, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 4: return launch<64, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 5: return launch<64, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
   }
   return (int)hipErrorInvalidValue;
 }
 
-// Largest tile that still gives about one block per CU; N must divide.
+// Largest tile that still gives about one block per CU; N must divide.  M <= 64
+// uses the 64-row tiles (no MFMA work or DMA on padding rows beyond one tile).
 int pick_tile(int M, int N) {
+  if (M <= 64) return N % 256 == 0 && N / 256 >= 200 ? 5 : (N % 128 == 0 ? 4 : 0);
   const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};
   int best = 0;
   for (auto& c : cand) {
@@ -359,7 +396,7 @@ static int prefill_dispatch(const void* Wt, const void* X, int ldx, int M, int K
   using namespace pgemm;
   if (M <= 0 || K % BK) return (int)hipErrorInvalidValue;
   int tile = g_prefill_tile ? g_prefill_tile : pick_tile(M, N);
-  const int bn = tile == 3 ? 128 : 256;
+  const int bn = (tile == 3 || tile == 4) ? 128 : 256;
   if (!tile || N % bn) return (int)hipErrorInvalidValue;
   const int up_off = (epi == EPI_SILU) ? N / 32 : 0;
   switch (epi) {

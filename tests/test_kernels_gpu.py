@@ -373,19 +373,22 @@ def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
 
 
 # ------------------------------------------------------------ tiled (prefill) GEMM
-TILED_CFGS = [(2, 0, 0), (2, 1, 1), (2, 2, 1), (2, 3, 1), (2, 3, 4), (2, 1, 3), (1, 0, 0)]
+TILED_CFGS = [(2, 0, 0), (2, 1, 1), (2, 2, 1), (2, 3, 1), (2, 3, 4), (2, 1, 3), (2, 4, 1),
+              (2, 4, 3), (2, 5, 2), (1, 0, 0)]
 
 
 @pytest.fixture(params=TILED_CFGS, ids=lambda c: "v%d_t%d_s%d" % c)
 def tiled_cfg(request):
-    from p2p_llm_chat_go_amd.ops.gemm import tiled_config
+    from p2p_llm_chat_go_amd.ops.gemm import set_tiled_min_m, tiled_config
 
     tiled_config(*request.param)
+    set_tiled_min_m(1)  # small M goes through the tiled kernel too
     yield request.param
+    set_tiled_min_m(65)
     tiled_config(2, 0, 0)
 
 
-@pytest.mark.parametrize("M", [65, 200, 513])
+@pytest.mark.parametrize("M", [7, 65, 200, 513])
 @pytest.mark.parametrize("epi", ["store", "store_norm", "resid", "silu", "f32"])
 def test_tiled_gemm(M, epi, tiled_cfg):
     torch.manual_seed(M)
