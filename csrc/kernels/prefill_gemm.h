@@ -313,12 +313,13 @@ static bool split_ws(size_t bytes, hipStream_t st, char** out) {
 
 static int g_splitk = 0;  // 0 = heuristic, 1 = never split, >1 = forced
 
-// LDS stages per tile shape (<= 160 KiB of LDS per CU): deeper pipelines where a stage is small
+// LDS stages per tile shape.  Measured on MI355X (bench/prefill_gemm_bench.py): the
+// 64-row tiles are latency-bound streams and want 3-4 stages in flight; the 128/256-row
+// tiles are MFMA-bound and lose more to 1-block/CU occupancy than they gain from depth.
 template <int BM, int BN>
 constexpr int stages_for() {
-  constexpr int stage_kb = (BM + BN) * BK * 2 / 1024;
-  constexpr int fit = 160 / stage_kb;
-  return fit >= 4 ? 4 : (fit >= 2 ? fit : 2);
+  if constexpr (BM >= 128) return 2;
+  return BN <= 128 ? 4 : 3;
 }
 
 template <int BM, int BN, int EPI, bool NORM>
@@ -330,8 +331,8 @@ int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_o
   const int tiles = m_tiles * n_tiles;
   const int nk = K / BK;
   // too few tiles to fill 256 CUs: split K so every CU gets work (>= 4 k-tiles per slice)
-  // (measured on MI355X at 8B shapes: ~400 blocks is the sweet spot for long-K tiles)
-  int splitk = g_splitk ? g_splitk : std::min(8, std::max(1, 400 / tiles));
+  // (measured on MI355X at 8B shapes: ~400 blocks, >= 16 k-tiles per slice)
+  int splitk = g_splitk ? g_splitk : std::min(8, std::max(1, std::min(400 / tiles, nk / 16)));
   splitk = std::max(1, std::min(splitk, nk / 4));
   if (splitk > 1) {
     constexpr int FM = BM / 32, FN = BN / 64;
@@ -371,7 +372,7 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
 // Largest tile that still gives about one block per CU; N must divide.  M <= 64
 // uses the 64-row tiles (no MFMA work or DMA on padding rows beyond one tile).
 int pick_tile(int M, int N) {
-  if (M <= 64) return N % 256 == 0 && N / 256 >= 200 ? 5 : (N % 128 == 0 ? 4 : 0);
+  if (M <= 64) return N % 128 == 0 ? 4 : 0;
   const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};
   int best = 0;
   for (auto& c : cand) {

@@ -40,9 +40,10 @@ def _graph_time(fn, reps=3):
     return best
 
 
-def _configs(K, M=1):
-    """Launch codes: waves | U << 8 | NG << 16 (NG = column groups per block, M > 16)."""
-    out = []
+def _configs(K, M=1, tiled=False):
+    """Launch codes: waves | U << 8 | NG << 16 (NG = column groups per block, M > 16);
+    G.TILED_FLAG = the split-K LDS-DMA tiled kernel (M > 16, tileable shapes)."""
+    out = [G.TILED_FLAG] if (tiled and M > 16) else []
     for ng in ((1,) if M <= 16 else (1, 2)):
         for u in ((4, 8) if M <= 16 else (2, 4)):
             for w in (1, 2, 4, 8):
@@ -52,6 +53,8 @@ def _configs(K, M=1):
 
 
 def describe(code: int) -> str:
+    if code & G.TILED_FLAG:
+        return "tiled"
     ng = (code >> 16) & 0xff
     return "w%d/U%d%s" % (code & 0xff, (code >> 8) & 0xff, "/NG%d" % ng if ng > 1 else "")
 
@@ -90,9 +93,9 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
         jobs.append(("lm_head", [w.lm_head], G.EPI_ARGMAX,
                      lambda wt, c: ops.lm_head_argmax(wt, x, keys, waves=c)))
         for name, wts, epi, fn in jobs:
-            K = G.tiled_shape(wts[0])[1]
+            N, K = G.tiled_shape(wts[0])
             times = {}
-            for code in _configs(K, M):
+            for code in _configs(K, M, G.tiled_ok(N, K, epi)):
                 times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
             best = min(times, key=times.get)
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)

@@ -45,11 +45,28 @@ def set_tiled_min_m(m: int):
     TILED_MIN_M = int(m)
 
 
-def use_tiled(M, N, K, epi) -> bool:
-    """Prefill-sized M goes to the LDS-tiled MFMA kernel (compute-bound), decode to skinny."""
-    if M < TILED_MIN_M or K % 64:
+def tiled_ok(N, K, epi) -> bool:
+    if K % 64:
         return False
     return (N // 2) % 64 == 0 if epi == EPI_SILU else N % 128 == 0
+
+
+def use_tiled(M, N, K, epi) -> bool:
+    """Prefill-sized M goes to the LDS-tiled MFMA kernel (compute-bound), decode to skinny."""
+    return M >= TILED_MIN_M and tiled_ok(N, K, epi)
+
+
+# launch-code bit: run this (shape, M tile) on the tiled LDS-DMA kernel (autotuned for
+# 16 < M <= 64, where the split-K tiled kernel can beat the skinny one)
+TILED_FLAG = 1 << 24
+
+
+def _want_tiled(wt, M, N, K, epi, norm, waves) -> bool:
+    if use_tiled(M, N, K, epi):
+        return True
+    if M > SKINNY_MAX_M or not tiled_ok(N, K, epi):
+        return False
+    return bool(_code(wt, M, epi, norm, waves) & TILED_FLAG)
 
 
 def tiled_config(version: int = 2, tile: int = 0, splitk: int = 0):
@@ -128,7 +145,7 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
     assert x.stride(1) == 1 and out.stride(1) == 1
     L = _lib.lib()
     s = _lib.stream_ptr(x.device)
-    if use_tiled(M, N, K, epi):
+    if _want_tiled(wt, M, N, K, epi, norm, waves):
         _lib.check(L.p2p_tiled_gemm(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N, epi,
                                     int(norm), out.data_ptr(), out.stride(0), float(eps), s),
                    "tiled_gemm")
@@ -175,7 +192,7 @@ def qkv_rope_gemm(wt, x, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_c
         return rope_cache_ref(qkv, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_cache)
     L = _lib.lib()
     s = _lib.stream_ptr(x.device)
-    if use_tiled(M, N, K, EPI_QKV_ROPE):
+    if _want_tiled(wt, M, N, K, EPI_QKV_ROPE, True, waves):
         _lib.check(L.p2p_tiled_gemm_qkv_rope(
             wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, n_heads, n_kv, pos.data_ptr(),
             slots.data_ptr(), cos_sin.data_ptr(), q_out.data_ptr(), q_out.stride(0),
@@ -219,7 +236,7 @@ def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: i
         keys[:M, 0] = torch.where((k ^ sign) > (cur ^ sign), k, cur)
         return keys
     L = _lib.lib()
-    if use_tiled(M, N, K, EPI_ARGMAX):
+    if _want_tiled(wt, M, N, K, EPI_ARGMAX, True, waves):
         _lib.check(L.p2p_tiled_gemm_argmax(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N,
                                            keys.data_ptr(), int(col_offset), float(eps),
                                            _lib.stream_ptr(x.device)), "tiled_gemm_argmax")
