@@ -162,11 +162,14 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
       for (int j = 0; j < FN; ++j) bfr[j] = sb[(bgi[j] * 2 + ks) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[i] = sa[((wm * FM + i) * 2 + ks) * 64 + lane];
+      // keep the MFMA cluster together against the co-resident wave (guide T5)
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
       if (do_ss) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
