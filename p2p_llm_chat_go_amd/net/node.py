@@ -55,9 +55,40 @@ def build_engine_server(model: str | None = None, device: str | None = None):
                         default_max_tokens=int(os.environ.get("ENGINE_MAX_TOKENS", "128")))
 
 
+# CLI flags mirror the environment (SURVEY §5 "Config / flag system"): a flag wins
+# over the variable of the same meaning.
+FLAGS = [
+    ("--username", "MYNAMEIS"), ("--http-addr", "HTTP_ADDR"), ("--directory-url", "DIRECTORY_URL"),
+    ("--bootstrap", "BOOTSTRAP_ADDRS"), ("--relays", "RELAY_ADDRS"), ("--listen", "LISTEN_ADDRS"),
+    ("--key-type", "KEY_TYPE"), ("--identity-file", "IDENTITY_FILE"), ("--inbox-file", "INBOX_FILE"),
+    ("--register-interval", "REGISTER_INTERVAL"), ("--dht-mode", "DHT_MODE"),
+    ("--llm-model", "LLM_MODEL"), ("--ui-file", "UI_FILE"), ("--engine", "ENGINE"),
+    ("--engine-model", "ENGINE_MODEL"), ("--engine-device", "ENGINE_DEVICE"),
+    ("--engine-checkpoint", "ENGINE_CHECKPOINT"), ("--engine-max-batch", "ENGINE_MAX_BATCH"),
+    ("--engine-max-tokens", "ENGINE_MAX_TOKENS"), ("--tokenizer", "TOKENIZER_PATH"),
+    ("--engine-url", "ENGINE_URL"),
+]
+
+
+def parse_flags(argv=None):
+    import argparse
+
+    ap = argparse.ArgumentParser(prog="python -m p2p_llm_chat_go_amd.net.node",
+                                 description="P2P chat node with the in-process engine")
+    for flag, env in FLAGS:
+        ap.add_argument(flag, dest=env, default=None, help="(env %s)" % env)
+    a = ap.parse_args(argv)
+    for _flag, env in FLAGS:
+        v = getattr(a, env)
+        if v is not None:
+            os.environ[env] = v
+    return a
+
+
 def main(argv=None):
     from ..native import load
 
+    parse_flags(argv)
     N = load()
     cfg = {}
     ui = os.environ.get("UI_FILE") or os.path.join(

@@ -259,3 +259,24 @@ def test_kad_dht_find_peer_through_bootstrap_chain(procs):
     # a node started with DHT_MODE=off serves no kad protocol
     e = start_node(procs, "E", d, {"DHT_MODE": "off"})
     assert http("GET", e + "/dht/find?peer=" + me_a["peer_id"])[0] == 503
+
+
+def test_python_node_cli_flags(procs):
+    """`python -m p2p_llm_chat_go_amd.net.node` flags mirror the env vars (flag wins)."""
+    import subprocess
+    import sys
+
+    d = start_directory(procs)
+    port = free_port()
+    env = dict(os.environ, MYNAMEIS="from-env", PYTHONPATH=os.path.dirname(BIN))
+    p = subprocess.Popen([sys.executable, "-m", "p2p_llm_chat_go_amd.net.node", "--username",
+                          "from-flag", "--http-addr", "127.0.0.1:%d" % port, "--directory-url", d,
+                          "--engine", "0", "--key-type", "ed25519", "--listen",
+                          "/ip4/127.0.0.1/tcp/0"], env=env, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL)
+    procs.procs.append(p)
+    url = "http://127.0.0.1:%d" % port
+    wait_http(url + "/me", timeout=60)
+    me = json.loads(http("GET", url + "/me")[1])
+    assert me["username"] == "from-flag" and me["peer_id"].startswith("12D3KooW")
+    assert json.loads(http("GET", d + "/lookup?username=from-flag")[1])["peer_id"] == me["peer_id"]
