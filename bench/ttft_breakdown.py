@@ -1,0 +1,55 @@
+"""TTFT anatomy for one suggest-reply prompt: wall time of Engine.prefill (host
+prep + all layers + LM head + first-token sync) vs GPU time, for profiling
+under rocprofv3 (`--kernel-trace --stats`) to get the per-kernel split."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from p2p_llm_chat_go_amd.engine import Engine  # noqa: E402
+from p2p_llm_chat_go_amd.engine.tokenizer import SAMPLE_MESSAGES, get_tokenizer, suggest_prompt  # noqa: E402
+from p2p_llm_chat_go_amd.models.config import get_config  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3.1-8b")
+    ap.add_argument("--peers", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    cfg = get_config(a.model)
+    tok = get_tokenizer(cfg)
+    eng = Engine(cfg, device="cuda", kv_pages=256, max_batch=max(8, a.peers))
+    eng.warmup((a.peers,), ctx=128)
+    prompts = [tok.chat_ids(suggest_prompt(SAMPLE_MESSAGES[i % len(SAMPLE_MESSAGES)]))
+               for i in range(a.peers)]
+    pages = [eng.kv.allocator.alloc(1) for _ in prompts]
+    for _ in range(3):
+        eng.prefill(prompts, pages).cpu()
+    torch.cuda.synchronize()
+    walls, gpus = [], []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(a.iters):
+        t0 = time.perf_counter()
+        e0.record()
+        first = eng.prefill(prompts, pages)
+        e1.record()
+        first.cpu()
+        walls.append((time.perf_counter() - t0) * 1e3)
+        torch.cuda.synchronize()
+        gpus.append(e0.elapsed_time(e1))
+    walls.sort()
+    gpus.sort()
+    print(json.dumps({"model": cfg.name, "peers": a.peers, "prompt_tokens": len(prompts[0]),
+                      "prefill_wall_ms_p50": round(walls[len(walls) // 2], 3),
+                      "prefill_gpu_event_ms_p50": round(gpus[len(gpus) // 2], 3),
+                      "tuning": {"%s@M%d" % k: "%s %.1fus" % v for k, v in eng.tuning.items()}}),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
