@@ -248,6 +248,9 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
       }
       __syncthreads();
     }
+    // every slice has arrived: re-arm the ticket for the next launch (the workspace
+    // counters are zeroed once at allocation, so no per-launch memset node is needed)
+    if (tid == 0) sp.counters[tile] = 0;
   }
 
   // ---- epilogue ----
@@ -298,7 +301,12 @@ struct SplitWs {
 };
 static SplitWs g_split_ws;
 
+// ticket counters: a fixed region at the end of the workspace, zeroed when the
+// workspace is (re)allocated and re-armed by each tile's last arriver
+constexpr size_t kCounterBytes = 64 * 1024;  // 16384 tiles
+
 static bool split_ws(size_t bytes, hipStream_t st, char** out) {
+  bytes += kCounterBytes;
   if (g_split_ws.bytes < bytes) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(st, &cs);
@@ -308,6 +316,7 @@ static bool split_ws(size_t bytes, hipStream_t st, char** out) {
     g_split_ws.buf = nullptr;
     g_split_ws.bytes = 0;
     if (hipMalloc(&g_split_ws.buf, bytes) != hipSuccess) return false;
+    if (hipMemset(g_split_ws.buf, 0, bytes) != hipSuccess) return false;
     g_split_ws.bytes = bytes;
   }
   *out = (char*)g_split_ws.buf;
@@ -337,15 +346,16 @@ int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_o
   // (measured on MI355X at 8B shapes: ~400 blocks, >= 16 k-tiles per slice)
   int splitk = g_splitk ? g_splitk : std::min(8, std::max(1, std::min(400 / tiles, nk / 16)));
   splitk = std::max(1, std::min(splitk, nk / 4));
-  if (splitk > 1) {
+  if (splitk > 1 && (size_t)tiles * sizeof(unsigned) <= kCounterBytes) {
     constexpr int FM = BM / 32, FN = BN / 64;
     const size_t slab = (size_t)tiles * splitk * FM * FN * NT * sizeof(f32x4);
     const size_t ssb = (size_t)tiles * splitk * BM * sizeof(float);
-    const size_t cnt = (size_t)tiles * sizeof(unsigned);
     char* ws = nullptr;
-    if (split_ws(slab + ssb + cnt, st, &ws)) {
-      SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), (unsigned*)(ws + slab + ssb)};
-      (void)hipMemsetAsync(sp.counters, 0, cnt, st);
+    if (split_ws(slab + ssb, st, &ws)) {
+      // counters live at the END of the workspace at a fixed offset from the end so a
+      // grown workspace keeps them zeroed; see split_ws
+      SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab),
+                   (unsigned*)(ws + g_split_ws.bytes - kCounterBytes)};
       hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, true, STAGES>),
                          dim3(tiles * splitk), dim3(NT), 0, st, (const bf16x8*)Wt,
                          (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, sp);
