@@ -49,6 +49,7 @@ class EngineServer:
         self._lock = threading.Condition()
         self._reqs = {}      # id -> dict(prompt, params, future, t_submit, t_admit, t_first)
         self._pending = []   # (prompt_ids, params, future, t_submit) waiting to enter the scheduler
+        self._cancels = set()  # futures whose requests should stop
         self._stop = False
         self._gen = torch.Generator(device=engine.device)
         self.stats = {"requests": 0, "tokens": 0, "prefill_tokens": 0, "decode_steps": 0,
@@ -66,6 +67,14 @@ class EngineServer:
                                   on_tokens))
             self._lock.notify()
         return fut
+
+    def cancel(self, fut: Future):
+        """Stop a request early (e.g. its streaming client went away); its KV pages are
+        freed at the next engine step and the future resolves with done_reason
+        "cancelled"."""
+        with self._lock:
+            self._cancels.add(fut)
+            self._lock.notify()
 
     def generate(self, prompt_ids, params: SamplingParams, timeout: float = 600.0) -> dict:
         return self.submit(prompt_ids, params).result(timeout)
@@ -151,6 +160,8 @@ class EngineServer:
             else:
                 chunk["response"] = delta
             alive = bool(emit(json.dumps(chunk)))
+            if not alive:  # client disconnected: stop generating for it
+                self.cancel(fut)
 
         while True:
             try:
@@ -224,8 +235,18 @@ class EngineServer:
                 self._reqs.clear()
             self.stats["busy_s"] += time.perf_counter() - t_busy
 
+    def _apply_cancels(self):
+        with self._lock:
+            cancels, self._cancels = self._cancels, set()
+        if not cancels:
+            return
+        for rid, r in list(self._reqs.items()):
+            if r["future"] in cancels:
+                self.sched.cancel(rid)
+
     def _step(self, eng: Engine):
         self._admit_pending()
+        self._apply_cancels()
         plan = self.sched.schedule()
         if plan.prefill:
             prompts = [self._reqs[i]["prompt"] for i in plan.prefill]

@@ -215,3 +215,33 @@ def test_server_gpu_graphs_batched():
             assert r["tokens"] == ref.generate([p], n, stop_on_eos=False)[0].tokens
     finally:
         srv.close()
+
+
+def test_server_cancel_and_stream_disconnect():
+    """A cancelled request (or a streaming client that goes away) stops early and
+    frees its KV pages."""
+    srv, _, _ = make_server()
+    try:
+        free0 = srv.sched.free_pages
+        p = SamplingParams(max_tokens=400, stop_on_eos=False)
+        fut = srv.submit([1, 2, 3], p)
+        srv.cancel(fut)
+        r = fut.result(60)
+        assert r["done_reason"] == "cancelled" and r["eval_count"] < 400
+        # streaming consumer that refuses the first chunk
+        calls = []
+
+        def emit(chunk):
+            calls.append(chunk)
+            return False
+        out = json.loads(srv.handle_json_stream(json.dumps(
+            {"prompt": "x", "options": {"num_predict": 400}}), emit))
+        assert out["done"] is True and out["done_reason"] == "cancelled"
+        assert len(calls) == 1 and out["eval_count"] < 400
+        for _ in range(100):
+            if srv.sched.free_pages == free0:
+                break
+            time.sleep(0.02)
+        assert srv.sched.free_pages == free0
+    finally:
+        srv.close()
