@@ -62,6 +62,94 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict_
   for (int i = threadIdx.x; i < e_local; i += blockDim.x) cnt[i] = s_cnt[i];
 }
 
+// Fused router + route for decode/prefill chunks (R <= 64 rows): one wave per row
+// computes rstd(h) and the E router logits (norm gain folded into Wr) with 16-byte
+// loads and wave reductions, then softmax / top-k / renormalisation in registers
+// (no scratch arrays), and the per-local-expert slot lists through LDS atomics.
+// Replaces the padded router GEMM + moe_route pair (two dependent launches).
+template <int E>
+__global__ __launch_bounds__(512) void moe_router_route_kernel(
+    const bf16* __restrict__ h, int ldh, int R, int H, const bf16* __restrict__ wr, float eps,
+    int K, int e_lo, int e_local, int* __restrict__ topk_ids, float* __restrict__ topk_w,
+    int* __restrict__ cnt, int* __restrict__ rows, int rows_stride) {
+  __shared__ int s_cnt[E];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (threadIdx.x < E) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (int r = w; r < R; r += nw) {
+    const bf16x8* hp = reinterpret_cast<const bf16x8*>(h + (size_t)r * ldh);
+    float acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+    float ss = 0.f;
+    for (int c = lane; c < H / 8; c += 64) {
+      const bf16x8 x = hp[c];
+      float xf[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xf[j] = (float)x[j];
+        ss = fmaf(xf[j], xf[j], ss);
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const bf16x8 wv = reinterpret_cast<const bf16x8*>(wr + (size_t)e * H)[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[e] = fmaf(xf[j], (float)wv[j], acc[e]);
+      }
+    }
+    ss = wave_sum(ss);
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = wave_sum(acc[e]);
+    const float rstd = rsqrtf(ss / (float)H + eps);
+    float m = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      acc[e] *= rstd;
+      m = fmaxf(m, acc[e]);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      acc[e] = __expf(acc[e] - m);
+      sum += acc[e];
+    }
+    // top-k by repeated arg-max over a taken mask (all indices compile-time)
+    unsigned taken = 0;
+    float wsum = 0.f;
+    int sel[MAX_K];
+    float wk[MAX_K];
+    for (int k = 0; k < K; ++k) {
+      int best = 0;
+      float bv = -1.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (!(taken >> e & 1u) && acc[e] > bv) {
+          bv = acc[e];
+          best = e;
+        }
+      }
+      taken |= 1u << best;
+      sel[k] = best;
+      wk[k] = bv / sum;
+      wsum += wk[k];
+    }
+    if (lane == 0) {
+      for (int k = 0; k < K; ++k) {
+        const int slot = r * K + k;
+        topk_ids[slot] = sel[k];
+        topk_w[slot] = wk[k] / wsum;
+        const int le = sel[k] - e_lo;
+        if (le >= 0 && le < e_local) {
+          const int pos = atomicAdd(&s_cnt[le], 1);
+          rows[(size_t)le * rows_stride + pos] = slot;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < e_local) cnt[threadIdx.x] = s_cnt[threadIdx.x];
+}
+
 // accumulate=1: h[r] += sum_k o[r*K+k] over local experts;  0: out[r] = that sum.
 __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict__ o, int ldo_,
                                                           const int* __restrict__ topk_ids, int K,
@@ -101,6 +189,28 @@ P2P_API int p2p_moe_route(const float* logits, int ldl, int R, int E, int K, int
   hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(256), 0, st, logits, ldl, R, E, K, e_lo,
                      e_local, topk_ids, topk_w, cnt, rows, rows_stride);
   return (int)hipGetLastError();
+}
+
+// h: [R, H] bf16 residual rows (raw); wr: [E, H] bf16 router with the RMSNorm gain folded.
+P2P_API int p2p_moe_router_route(const void* h, int ldh, int R, int H, const void* wr, float eps,
+                                 int E, int K, int e_lo, int e_local, int* topk_ids, float* topk_w,
+                                 int* cnt, int* rows, int rows_stride, hipStream_t st) {
+  if (K > MAX_K || K > E || R <= 0 || R > 64 || H % 8 || rows_stride < R || e_local > E)
+    return (int)hipErrorInvalidValue;
+  const auto* hb = (const bf16*)h;
+  const auto* wb = (const bf16*)wr;
+#define P2P_ROUTER_CASE(EE)                                                                      \
+  case EE:                                                                                      \
+    hipLaunchKernelGGL(moe_router_route_kernel<EE>, dim3(1), dim3(512), 0, st, hb, ldh, R, H, wb, \
+                       eps, K, e_lo, e_local, topk_ids, topk_w, cnt, rows, rows_stride);         \
+    return (int)hipGetLastError();
+  switch (E) {
+    P2P_ROUTER_CASE(4)
+    P2P_ROUTER_CASE(8)
+    P2P_ROUTER_CASE(16)
+  }
+#undef P2P_ROUTER_CASE
+  return (int)hipErrorInvalidValue;
 }
 
 P2P_API int p2p_moe_combine(const void* o, int ldo_, const int* topk_ids, int R, int K, int e_lo,

@@ -1,8 +1,7 @@
 """Mixtral sparse-MoE FFN on the engine kernels (replaces the dense SwiGLU MLP).
 
 Per layer, for R rows (chunks of <= 64 rows, the grouped kernel's M tile):
-    logits = rstd(h) * h @ Wrouter'          skinny_gemm (router padded to 16 rows)
-    ids, w = top_k(softmax(logits))          moe_route  (+ per-expert slot lists)
+    ids, w = top_k(softmax(rstd(h) h Wr'))   moe_router_route (+ per-expert slot lists)
     act[s] = silu(g) * u of expert(s)        grouped_gemm SILU | NORM
     o[s]   = w[s] * act[s] @ W2_e            grouped_gemm STORE (row-scaled)
     h     += sum_k o[r*K + k]                moe_combine (EP/TP: partial + all-reduce)
@@ -68,10 +67,9 @@ def moe_forward(model, lw, ws, R):
     for r0 in range(0, R, CHUNK):
         rc = min(CHUNK, R - r0)
         h = ws.h[r0:r0 + rc]
-        logits = m.logits[:rc]
-        ops.skinny_gemm(router_tiled(lw), h, ops.EPI_F32, norm=True, out=logits, eps=cfg.eps)
-        moe_ops.moe_route(logits, cfg.n_experts, K, e_lo, e_local, m.topk_ids, m.topk_w, m.cnt,
-                          m.rows)
+        # router GEMM + softmax/top-k + per-expert slot lists in one kernel
+        moe_ops.moe_router_route(h, lw.router, cfg.n_experts, K, e_lo, e_local, m.topk_ids,
+                                 m.topk_w, m.cnt, m.rows, eps=cfg.eps)
         moe_ops.grouped_gemm(lw.w13, m.cnt, m.rows, h, K, rc, ops.EPI_SILU, m.act, norm=True,
                              eps=cfg.eps)
         moe_ops.grouped_gemm(lw.w2, m.cnt, m.rows, m.act, 1, rc, ops.EPI_STORE, m.o,

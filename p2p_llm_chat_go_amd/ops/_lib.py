@@ -70,6 +70,8 @@ _SIGS = {
                          c_int, c_float, c_int, c_void_p],
     "p2p_moe_route": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                       c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_moe_router_route": [c_void_p, c_int, c_int, c_int, c_void_p, c_float, c_int, c_int, c_int,
+                             c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "p2p_moe_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p],
 }

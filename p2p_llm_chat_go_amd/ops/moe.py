@@ -37,6 +37,22 @@ def moe_route(logits, E, K, e_lo, e_local, topk_ids, topk_w, cnt, rows):
                "moe_route")
 
 
+def moe_router_route(h, wr, E, K, e_lo, e_local, topk_ids, topk_w, cnt, rows, eps=1e-5):
+    """Fused router (rstd(h) * h @ Wr^T, RMSNorm gain folded into wr) + moe_route for
+    R <= 64 rows: topk ids/weights [R*K], cnt [e_local], rows [e_local, >=R]."""
+    R, H = h.shape
+    if h.device.type != "cuda":
+        hf = h.float()
+        logits = (hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps)) @ wr.float().t()
+        return moe_route(logits, E, K, e_lo, e_local, topk_ids, topk_w, cnt, rows)
+    L = _lib.lib()
+    _lib.check(L.p2p_moe_router_route(h.data_ptr(), h.stride(0), R, H, wr.data_ptr(), float(eps),
+                                      E, K, e_lo, e_local, topk_ids.data_ptr(), topk_w.data_ptr(),
+                                      cnt.data_ptr(), rows.data_ptr(), rows.stride(0),
+                                      _lib.stream_ptr(h.device)), "moe_router_route")
+    return topk_ids, topk_w
+
+
 def grouped_gemm(wt, cnt, rows, x, x_div, max_rows, epi, out, norm=False, row_w=None, eps=1e-5):
     """Per local expert e: out[slot] = epi(x[slot // x_div] @ W_e^T) for its routed slots.
 

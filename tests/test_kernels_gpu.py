@@ -340,6 +340,32 @@ def test_lm_head_argmax(M, offset):
 
 
 # ------------------------------------------------------------ MoE
+@pytest.mark.parametrize("R,E,K,e_lo,e_local", [(1, 8, 2, 0, 8), (37, 8, 2, 4, 4), (64, 4, 2, 0, 4),
+                                                 (5, 16, 4, 8, 8)])
+def test_moe_router_route_fused(R, E, K, e_lo, e_local):
+    """Fused router+route kernel vs the fp32 router logits -> reference routing."""
+    from p2p_llm_chat_go_amd.ops import moe as Mo
+
+    torch.manual_seed(R * 31 + E)
+    H = 4096
+    h = torch.randn(R, H).to(torch.bfloat16)
+    wr = (torch.randn(E, H) * 0.05).to(torch.bfloat16)
+    ref = [torch.zeros(R * K, dtype=torch.int32), torch.zeros(R * K), torch.zeros(e_local, dtype=torch.int32),
+           torch.zeros(e_local, 64, dtype=torch.int32)]
+    Mo.moe_router_route(h, wr, E, K, e_lo, e_local, *ref)
+    got = [torch.zeros_like(t).to(DEV) for t in ref]
+    Mo.moe_router_route(h.to(DEV), wr.to(DEV), E, K, e_lo, e_local, *got)
+    torch.cuda.synchronize()
+    ids, tw, cnt, rows = [t.cpu() for t in got]
+    assert torch.equal(ids, ref[0])
+    assert torch.allclose(tw, ref[1], atol=2e-3)
+    assert torch.equal(cnt, ref[2])
+    for e in range(e_local):  # slot lists: same sets (atomic order may differ)
+        c = int(cnt[e])
+        assert sorted(rows[e, :c].tolist()) == sorted(ref[3][e, :c].tolist())
+
+
+
 @pytest.mark.parametrize("R,E,K,e_lo,e_local", [(1, 8, 2, 0, 8), (13, 8, 2, 0, 8), (64, 8, 2, 4, 4)])
 def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
     from p2p_llm_chat_go_amd.ops import moe as M
