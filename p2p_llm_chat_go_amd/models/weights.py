@@ -180,7 +180,9 @@ def config_from_hf(path: str, base: ModelConfig | None = None) -> ModelConfig:
     """Build a ModelConfig from an HF ``config.json`` (Llama / Mixtral)."""
     with open(os.path.join(path, "config.json")) as f:
         c = json.load(f)
-    rs = c.get("rope_scaling") or None
+    # transformers < 5: rope_theta + rope_scaling; >= 5: rope_parameters (theta inside)
+    rs = c.get("rope_scaling") or c.get("rope_parameters") or None
+    theta = c.get("rope_theta", (rs or {}).get("rope_theta", 10000.0))
     llama3 = None
     if rs and rs.get("rope_type", rs.get("type")) == "llama3":
         llama3 = (float(rs["factor"]), float(rs["low_freq_factor"]), float(rs["high_freq_factor"]),
@@ -194,7 +196,7 @@ def config_from_hf(path: str, base: ModelConfig | None = None) -> ModelConfig:
                                                            c["num_attention_heads"]),
         ffn=c["intermediate_size"], vocab=c["vocab_size"],
         head_dim=c.get("head_dim", c["hidden_size"] // c["num_attention_heads"]),
-        rope_theta=float(c.get("rope_theta", 10000.0)), rope_llama3=llama3,
+        rope_theta=float(theta), rope_llama3=llama3,
         eps=float(c.get("rms_norm_eps", 1e-5)), max_pos=int(c.get("max_position_embeddings", 8192)),
         n_experts=int(c.get("num_local_experts", 0)), top_k=int(c.get("num_experts_per_tok", 0)),
         tie_embeddings=bool(c.get("tie_word_embeddings", False)),
