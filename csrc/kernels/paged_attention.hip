@@ -38,10 +38,14 @@ __global__ __launch_bounds__(WAVES * 64) void paged_attn_kernel(
     const int* __restrict__ ctx_lens, int Hkv, float scale, int n_chunks, bf16* __restrict__ out,
     int ldo, float* __restrict__ part_o, float* __restrict__ part_ml) {
   const int c = blockIdx.x, h = blockIdx.y, r = blockIdx.z;
-  const int ctx = ctx_lens[r];
-  if (c * CHUNK >= ctx) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int t = lane >> 2, quarter = lane & 3;
+  // The context length, the block-table row and q are independent loads: issue them
+  // together, and issue the K/V loads before looking at ctx (keys past the context
+  // read the zero-initialised block-table tail = null page 0, always mapped), so the
+  // kernel's dependent-latency chain is row_bt -> page -> K/V, not ctx -> ... -> K/V.
+  const int ctx = ctx_lens[r];
+  const int rb = row_bt[r];
 
   constexpr int VS = HD + 8;
   __shared__ bf16x2 qs[G][HD / 2];
@@ -51,14 +55,13 @@ __global__ __launch_bounds__(WAVES * 64) void paged_attn_kernel(
   __shared__ float so[WAVES][G][HD];
 
   const int key0 = c * CHUNK + w * KPW;  // first key of this wave
-  const int n_valid = min(max(ctx - key0, 0), KPW);
-  const bool mine = t < n_valid;
 
   // 1) all global loads first: 32 dims (4 x 16 B) of K and V row `t` per lane
   bf16x8 kr[4], vr[4];
-  if (mine) {
+  {
     const int key = key0 + t;
-    const int page = bt[(size_t)row_bt[r] * bt_stride + key / PAGE];
+    const int pcol = min(key / PAGE, bt_stride - 1);
+    const int page = bt[(size_t)rb * bt_stride + pcol];
     const size_t off = (((size_t)page * Hkv + h) * PAGE + (key % PAGE)) * HD + quarter * 32;
     const bf16x8* kp = reinterpret_cast<const bf16x8*>(kc + off);
     const bf16x8* vp = reinterpret_cast<const bf16x8*>(vc + off);
@@ -69,6 +72,9 @@ __global__ __launch_bounds__(WAVES * 64) void paged_attn_kernel(
   }
   const bf16x2* qrow = reinterpret_cast<const bf16x2*>(q + (size_t)r * ldq + (size_t)h * G * HD);
   for (int i = tid; i < G * HD / 2; i += WAVES * 64) qs[i / (HD / 2)][i % (HD / 2)] = qrow[i];
+  if (c * CHUNK >= ctx) return;  // block-uniform: the whole chunk is past the context
+  const int n_valid = min(max(ctx - key0, 0), KPW);
+  const bool mine = t < n_valid;
   __syncthreads();
 
   float o[G][2];
