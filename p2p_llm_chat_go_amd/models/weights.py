@@ -99,7 +99,8 @@ class EngineWeights:
                 E = cfg.n_experts
                 assert E % ep_size == 0
                 el = E // ep_size
-                lw.router = ops.fold_norm(get(p + "block_sparse_moe.gate.weight"), g_post).contiguous()
+                lw.router = ops.fold_norm(get(p + "block_sparse_moe.gate.weight"), g_post).to(
+                    torch.bfloat16).contiguous()
                 w13, w2 = [], []
                 Fs = F // tp_size
                 for e in range(ep_rank * el, (ep_rank + 1) * el):

@@ -45,6 +45,8 @@ def moe_router_route(h, wr, E, K, e_lo, e_local, topk_ids, topk_w, cnt, rows, ep
         hf = h.float()
         logits = (hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps)) @ wr.float().t()
         return moe_route(logits, E, K, e_lo, e_local, topk_ids, topk_w, cnt, rows)
+    if h.dtype != torch.bfloat16 or wr.dtype != torch.bfloat16 or not wr.is_contiguous():
+        raise TypeError("moe_router_route: h and wr must be bf16 (wr contiguous)")
     L = _lib.lib()
     _lib.check(L.p2p_moe_router_route(h.data_ptr(), h.stride(0), R, H, wr.data_ptr(), float(eps),
                                       E, K, e_lo, e_local, topk_ids.data_ptr(), topk_w.data_ptr(),
