@@ -220,6 +220,7 @@ class Engine:
                         if all(done):
                             break
                 hist = st.hist[:B, :steps_run].cpu()
+                self.model.check_faults(st.ws)
                 for b in range(B):
                     out[b] += [int(t) for t in hist[b]]
             else:

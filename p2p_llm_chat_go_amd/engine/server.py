@@ -286,6 +286,7 @@ class EngineServer:
                 for _ in range(k):
                     g.step_sampled(params, self._gen)
         hist = st.hist[:len(running), :k].cpu().tolist()
+        eng.model.check_faults(st.ws)
         self.stats["decode_steps"] += k
         self.sched.on_decode_tokens(running, hist)
         self._stream(running)

@@ -22,6 +22,8 @@ captured in a hipGraph (``engine.graph``).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
@@ -52,6 +54,9 @@ class Workspace:
         self.keys = ops.new_argmax_keys(mo, dev)
         self.attn_ws = ops.attn_workspace(max_rows, nq, max_ctx, dev)
         self.moe = None  # lazily sized by models.moe
+        # fused attention + o_proj hand-off counters (re-armed by the kernel) + fault flag
+        self.sync = torch.zeros(2, device=dev, dtype=torch.int32)
+        self.err = torch.zeros(1, device=dev, dtype=torch.int32)
 
 
 class LlamaModel:
@@ -66,6 +71,8 @@ class LlamaModel:
         self.nkv = self.cfg.n_kv_heads // self.tp
         max_pos = min(self.cfg.max_pos, 1 << 17)
         self.rope = rope_table(self.cfg, max_pos=max_pos, device=self.device)
+        # decode: attention and o_proj in one launch (ops.attn_oproj) where it applies
+        self.fuse_attn_oproj = os.environ.get("P2P_FUSED_ATTN_OPROJ", "1") == "1"
 
     def new_workspace(self, max_rows, max_ctx, max_out_rows=None) -> Workspace:
         return Workspace(self.cfg, max_rows, max_ctx, self.device, self.tp, max_out_rows)
@@ -107,17 +114,25 @@ class LlamaModel:
         h = ws.h[:R]
         ops.gather_rows(self.w.embed, ids[:R], out=h)
         q, attn = ws.q[:R], ws.attn[:R]
+        fused = (self.fuse_attn_oproj and tiles is None and self.tp == 1
+                 and self.device.type == "cuda"
+                 and ops.attn_oproj_ok(R, self.nq, self.nkv, max_ctx, cfg.hidden))
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)
             ops.qkv_rope_gemm(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc,
                               vc, eps=cfg.eps)
-            if tiles is not None:
-                ops.flash_prefill(q, kc, vc, block_tables, tiles, self.nq, self.nkv, out=attn,
-                                  tiles_host=tiles_host)
+            if fused:
+                ops.attn_oproj(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R], self.nq,
+                               self.nkv, max_ctx, lw.o, h, attn, ws.sync, ws.err)
             else:
-                ops.paged_attention(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R], self.nq,
-                                    self.nkv, max_ctx, out=attn, workspace=ws.attn_ws)
-            self._row_parallel(lw.o, attn, h, ws, R)
+                if tiles is not None:
+                    ops.flash_prefill(q, kc, vc, block_tables, tiles, self.nq, self.nkv, out=attn,
+                                      tiles_host=tiles_host)
+                else:
+                    ops.paged_attention(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R],
+                                        self.nq, self.nkv, max_ctx, out=attn,
+                                        workspace=ws.attn_ws)
+                self._row_parallel(lw.o, attn, h, ws, R)
             self._mlp(lw, ws, R)
         if n_out == 0:
             return None
@@ -133,6 +148,13 @@ class LlamaModel:
         logits = ws.logits[:n]
         ops.skinny_gemm(self.w.lm_head, x, ops.EPI_F32, norm=True, out=logits, eps=cfg.eps)
         return logits
+
+    def check_faults(self, ws: Workspace):
+        """Raise if a fused kernel's bounded cross-workgroup wait timed out (its results
+        would be wrong); costs one small device read, call where the host syncs anyway."""
+        if self.device.type == "cuda" and int(ws.err.item()) != 0:
+            ws.err.zero_()
+            raise RuntimeError("fused attention/o_proj hand-off timed out (results invalid)")
 
     def finalize_greedy(self, ws: Workspace, n: int, out=None):
         """keys -> token ids (TP: all-reduce MAX of the keys across vocab shards first)."""

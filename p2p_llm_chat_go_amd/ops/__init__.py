@@ -8,8 +8,8 @@ never a fallback for GPU tensors.
 from .gemm import (EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, argmax_finalize, fold_norm,
                    lm_head_argmax, new_argmax_keys, qkv_rope_gemm, rope_row_perm, skinny_gemm, tile_weight,
                    tiled_shape, untile_weight)
-from .attention import (PAGE, HEAD_DIM, attn_workspace, flash_prefill, paged_attention,
-                        prefill_tiles, rope_cache)
+from .attention import (PAGE, HEAD_DIM, attn_oproj, attn_oproj_ok, attn_workspace,
+                        flash_prefill, paged_attention, prefill_tiles, rope_cache)
 from .elementwise import advance, argmax, gather_rows
 from ._lib import available as kernels_available, lib as kernel_lib, lib_path as kernel_lib_path
 
@@ -17,6 +17,7 @@ __all__ = [
     "EPI_F32", "EPI_RESID", "EPI_SILU", "EPI_STORE", "fold_norm", "skinny_gemm", "tile_weight",
     "tiled_shape", "untile_weight", "argmax_finalize", "lm_head_argmax", "new_argmax_keys", "qkv_rope_gemm",
     "rope_row_perm", "PAGE", "HEAD_DIM", "attn_workspace", "paged_attention", "flash_prefill", "prefill_tiles",
+    "attn_oproj", "attn_oproj_ok",
     "rope_cache", "advance", "argmax", "gather_rows", "kernels_available", "kernel_lib",
     "kernel_lib_path",
 ]

@@ -46,6 +46,9 @@ _SIGS = {
     "p2p_car_handle_size": [],
     "p2p_car_allreduce_add": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p, c_int,
                               c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_attn_oproj": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                       c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_void_p,
+                       c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "p2p_gather_rows": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
     "p2p_rope_cache": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_void_p, c_int, c_void_p, c_void_p, c_void_p],

@@ -80,6 +80,43 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return out
 
 
+FUSED_MAX_ROWS = 16
+FUSED_MAX_CTX = 256
+
+
+def attn_oproj_ok(R: int, n_heads: int, n_kv: int, max_ctx: int, N: int) -> bool:
+    """Shapes the fused attention + o_proj kernel handles (else run the two ops)."""
+    G = n_heads // n_kv
+    S = n_heads * HEAD_DIM // 32
+    return (R <= FUSED_MAX_ROWS and max_ctx <= FUSED_MAX_CTX and G in (1, 2, 4) and S % 16 == 0
+            and S // 16 in (1, 2, 4, 8, 16) and N % 16 == 0)
+
+
+def attn_oproj(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_kv, max_ctx, wo,
+               h, attn, sync, err, scale=None):
+    """h += attention(q) @ Wo^T in ONE launch (decode, R <= 16 rows, ctx <= 256):
+    the o_proj blocks stream their weights while the attention blocks run.
+    attn: [R, n_heads*128] scratch; sync: int32 [2] zeros; err: int32 [1]."""
+    from .gemm import EPI_RESID, skinny_gemm, tiled_shape
+
+    R = q.shape[0]
+    if scale is None:
+        scale = 1.0 / math.sqrt(HEAD_DIM)
+    N, K = tiled_shape(wo)
+    if q.device.type != "cuda":
+        paged_attention(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_kv,
+                        max_ctx, out=attn, scale=scale)
+        return skinny_gemm(wo, attn, EPI_RESID, out=h)
+    L = _lib.lib()
+    _lib.check(L.p2p_attn_oproj(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                block_tables.data_ptr(), block_tables.stride(0), row_bt.data_ptr(),
+                                ctx_lens.data_ptr(), R, n_heads, n_kv, HEAD_DIM, float(scale),
+                                int(max_ctx), attn.data_ptr(), attn.stride(0), wo.data_ptr(), N,
+                                h.data_ptr(), h.stride(0), sync.data_ptr(), err.data_ptr(),
+                                _lib.stream_ptr(q.device)), "attn_oproj")
+    return h
+
+
 QTILE = 16
 
 

@@ -192,6 +192,62 @@ def test_paged_attention_spike_forces_rescale():
     assert _rel(out.cpu(), ref) < 1e-2
 
 
+# ------------------------------------------- fused decode attention + o_proj
+@pytest.mark.parametrize("R,Hkv,G,ctxs", [(1, 8, 4, [100]), (3, 2, 2, [1, 17, 256]),
+                                          (16, 1, 4, list(range(5, 245, 15))), (2, 4, 1, [64, 65])])
+def test_attn_oproj_fused(R, Hkv, G, ctxs):
+    """One launch (attention blocks + o_proj blocks with a cross-workgroup hand-off)
+    == paged_attention followed by the o_proj+residual GEMM; repeated launches and
+    hipGraph replays exercise the counter re-arming."""
+    torch.manual_seed(R * 100 + Hkv * 10 + G)
+    Hq = Hkv * G
+    K = Hq * 128
+    N = 256 if K < 4096 else 4096
+    npg = 4
+    P = 1 + R * npg
+    k, v = _make_cache(P, Hkv, seed=R + G)
+    bt = (torch.randperm(P - 1)[:R * npg] + 1).view(R, npg).to(torch.int32)
+    q = torch.randn(R, Hq * 128).to(torch.bfloat16)
+    ctx = torch.tensor(ctxs, dtype=torch.int32)
+    row_bt = torch.arange(R, dtype=torch.int32)
+    Wo = (torch.randn(N, K) * 0.02).to(torch.bfloat16)
+    h0 = torch.randn(R, N).to(torch.bfloat16)
+    a_ref = A.paged_attention_ref(q, k, v, bt, row_bt, ctx, Hq, Hkv, 1 / math.sqrt(128),
+                                  torch.empty(R, Hq * 128, dtype=torch.float32))
+    ref = h0.float() + a_ref.to(torch.bfloat16).float() @ Wo.float().t()
+    assert ops.attn_oproj_ok(R, Hq, Hkv, 256, N)
+    d = {n: t.to(DEV) for n, t in dict(q=q, k=k, v=v, bt=bt, ctx=ctx, rb=row_bt).items()}
+    wt = ops.tile_weight(Wo).to(DEV)
+    attn = torch.zeros(R, Hq * 128, dtype=torch.bfloat16, device=DEV)
+    sync = torch.zeros(2, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for _ in range(3):  # back-to-back launches: the kernel re-arms its counters
+        h = h0.to(DEV)
+        ops.attn_oproj(d["q"], d["k"], d["v"], d["bt"], d["rb"], d["ctx"], Hq, Hkv, 256, wt, h,
+                       attn, sync, err)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0 and sync.abs().sum().item() == 0
+        assert _rel(attn.cpu(), a_ref) < 1e-2
+        assert _rel(h.cpu(), ref) < 1e-2
+    # captured and replayed
+    h = h0.to(DEV)
+    hs = h.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            ops.attn_oproj(d["q"], d["k"], d["v"], d["bt"], d["rb"], d["ctx"], Hq, Hkv, 256, wt,
+                           h, attn, sync, err)
+    torch.cuda.synchronize()
+    for i in range(4):
+        h.copy_(hs)
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        assert _rel(h.cpu(), ref) < 1e-2, i
+
+
 # ------------------------------------------------------- flash prefill (MFMA)
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
 @pytest.mark.parametrize("lens", [[(0, 5)], [(0, 37), (0, 16)], [(100, 70), (0, 300), (3, 1)]])
