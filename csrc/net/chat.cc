@@ -229,6 +229,7 @@ NodeConfig NodeConfig::from_env() {
   c.strict_sender = env_or("STRICT_SENDER", "0") == "1";
   c.access_log = env_or("GIN_MODE", "debug") != "quiet";
   c.dht_mode = env_or("DHT_MODE", c.dht_mode);
+  c.nat_pmp = env_or("NAT_PMP", c.nat_pmp);
   std::string la = env_or("LISTEN_ADDRS", "");
   if (la == "none") {
     c.listen.clear();  // relay-only node
@@ -332,6 +333,7 @@ void Node::start() {
     kad_ = std::make_unique<Kad>(host_, cfg_.dht_mode == "client" ? KadMode::Client : KadMode::Server);
   }
   for (auto& l : cfg_.listen) host_->listen(Multiaddr::parse(l));
+  if (cfg_.nat_pmp != "off" && !cfg_.nat_pmp.empty()) setup_nat();
   relay_client_ = std::make_unique<RelayClient>(host_);
   host_->set_stream_handler(kChatProto, [this](StreamCtx& c) { on_chat(c); });
   for (auto& r : split_csv(cfg_.relays)) {
@@ -386,9 +388,40 @@ void Node::start() {
 
 void Node::wait() { http_.serve_forever(); }
 
+void Node::setup_nat() {
+  nat_ = std::make_unique<NatPmp>(cfg_.nat_pmp == "on" ? "" : cfg_.nat_pmp, 1000);
+  if (!nat_->ok()) {
+    logf("NAT-PMP: no default gateway");
+    return;
+  }
+  const std::string ext = nat_->external_address();
+  if (ext.empty()) {
+    logf("NAT-PMP: gateway %s did not answer", nat_->gateway().c_str());
+    return;
+  }
+  std::vector<NatMapping> maps;
+  for (auto& a : host_->addrs()) {
+    std::string h;
+    int port = 0;
+    if (!a.tcp_host_port(&h, &port) || a.has(MA_P2P_CIRCUIT)) continue;
+    bool dup = false;
+    for (auto& m : maps) dup |= m.internal_port == port;
+    if (dup) continue;
+    NatMapping m;
+    if (nat_->map_tcp(port, port, 3600, &m)) {
+      maps.push_back(m);
+      host_->add_advertised_addr(
+          Multiaddr::parse("/ip4/" + ext + "/tcp/" + std::to_string(m.external_port)));
+      logf("NAT-PMP: mapped tcp %d -> %s:%d", port, ext.c_str(), m.external_port);
+    }
+  }
+  nat_->keep_alive(maps);
+}
+
 void Node::stop() {
   if (stopping_.exchange(true)) return;
   http_.stop();
+  if (nat_) nat_->stop();
   if (refresher_.joinable()) refresher_.join();
   if (host_) host_->close();
   kad_.reset();  // after close(): no identify/handler thread can reach it any more

@@ -16,6 +16,7 @@
 #include "http.h"
 #include "json.h"
 #include "kad.h"
+#include "natpmp.h"
 #include "relay.h"
 
 namespace p2p {
@@ -98,6 +99,9 @@ struct NodeConfig {
   // queries, "off" disables.  The reference's dht.ModeAuto (main.go:151) is inert
   // without AutoNAT; we serve by default (no AutoNAT here) -- documented deviation.
   std::string dht_mode = "auto";
+  // NAT port mapping (reference: libp2p.NATPortMap(), main.go:143): "off" (default here:
+  // loopback tests/CI), "on" (default gateway) or an explicit "ip[:port]" NAT-PMP gateway
+  std::string nat_pmp = "off";
   static NodeConfig from_env();
 };
 
@@ -131,12 +135,14 @@ class Node {
 
  private:
   void on_chat(StreamCtx& c);
+  void setup_nat();
   void install_routes();
   Json generate(const Json& req);
   NodeConfig cfg_;
   std::shared_ptr<Host> host_;
   std::unique_ptr<RelayClient> relay_client_;
   std::unique_ptr<Kad> kad_;
+  std::unique_ptr<NatPmp> nat_;
   std::unique_ptr<DirectoryClient> dir_;
   Inbox inbox_;
   HttpServer http_;

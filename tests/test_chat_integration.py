@@ -280,3 +280,51 @@ def test_python_node_cli_flags(procs):
     me = json.loads(http("GET", url + "/me")[1])
     assert me["username"] == "from-flag" and me["peer_id"].startswith("12D3KooW")
     assert json.loads(http("GET", d + "/lookup?username=from-flag")[1])["peer_id"] == me["peer_id"]
+
+
+def test_nat_pmp_port_mapping(procs):
+    """NAT_PMP=<gateway>: the node maps its TCP port on the gateway (RFC 6886) and
+    advertises the external address (reference: libp2p.NATPortMap()); SIGTERM deletes
+    the mapping.  The gateway is a fake NAT-PMP responder on loopback."""
+    import socket
+    import struct
+    import threading
+
+    srv = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    srv.bind(("127.0.0.1", 0))
+    srv.settimeout(0.2)
+    log = []
+    stop = threading.Event()
+
+    def serve():
+        while not stop.is_set():
+            try:
+                data, addr = srv.recvfrom(64)
+            except socket.timeout:
+                continue
+            if data[:2] == b"\x00\x00":
+                srv.sendto(struct.pack(">BBHI4B", 0, 128, 0, 1, 203, 0, 113, 7), addr)
+            elif data[1] == 2:
+                _v, _op, _r, iport, eport, life = struct.unpack(">BBHHHI", data[:12])
+                log.append((iport, eport, life))
+                srv.sendto(struct.pack(">BBHIHHI", 0, 130, 0, 1, iport,
+                                       (iport + 10000) % 65536 if life else 0, life), addr)
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    try:
+        d = start_directory(procs)
+        a = start_node(procs, "A", d, {"NAT_PMP": "127.0.0.1:%d" % srv.getsockname()[1]})
+        me = json.loads(http("GET", a + "/me")[1])
+        iport = int(me["addrs"][0].split("/tcp/")[1].split("/")[0])
+        ext = "/ip4/203.0.113.7/tcp/%d/p2p/%s" % ((iport + 10000) % 65536, me["peer_id"])
+        assert ext in me["addrs"], me["addrs"]
+        assert (iport, iport, 3600) in log
+        assert ext in json.loads(http("GET", d + "/lookup?username=A")[1])["addrs"]
+        node = procs.procs[-1]
+        node.terminate()
+        node.wait(timeout=10)
+        assert any(x[0] == iport and x[2] == 0 for x in log), log  # unmapped on shutdown
+    finally:
+        stop.set()
+        t.join(timeout=2)
+        srv.close()
