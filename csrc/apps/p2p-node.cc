@@ -35,5 +35,6 @@ int main() {
     node.stop();
   }).detach();
   node.wait();
+  node.stop();  // blocks until a signal-driven stop() in flight has finished
   return 0;
 }

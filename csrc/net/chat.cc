@@ -419,9 +419,10 @@ void Node::setup_nat() {
 }
 
 void Node::stop() {
+  std::lock_guard<std::mutex> lk(stop_mu_);
   if (stopping_.exchange(true)) return;
+  if (nat_) nat_->stop();  // before http_.stop(): that releases wait() and main may exit
   http_.stop();
-  if (nat_) nat_->stop();
   if (refresher_.joinable()) refresher_.join();
   if (host_) host_->close();
   kad_.reset();  // after close(): no identify/handler thread can reach it any more

@@ -152,6 +152,7 @@ class Node {
   GenerateStreamHook stream_hook_;
   std::thread refresher_;
   std::atomic<bool> stopping_{false};
+  std::mutex stop_mu_;  // a second stop() caller blocks until the first finished
   std::atomic<long> n_sent_{0}, n_recv_{0}, n_suggest_{0}, n_send_fail_{0};
 };
 

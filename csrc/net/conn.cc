@@ -77,12 +77,15 @@ void write_frame(Conn& c, const Bytes& payload) {
 }
 
 // ================================================================ TCP
-TcpConn::TcpConn(int fd, std::string remote) : fd_(fd), remote_(std::move(remote)) {
+TcpConn::TcpConn(int fd, std::string remote) : fd_(fd), own_fd_(fd), remote_(std::move(remote)) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
 }
 
-TcpConn::~TcpConn() { close(); }
+TcpConn::~TcpConn() {
+  close();
+  if (own_fd_ >= 0) ::close(own_fd_);
+}
 
 static std::string sockaddr_str(const sockaddr* sa) {
   char host[INET6_ADDRSTRLEN] = {0};
@@ -180,12 +183,12 @@ void TcpConn::close_write() {
   if (fd >= 0) shutdown(fd, SHUT_WR);
 }
 
+// shutdown() wakes a thread blocked in recv/send on this socket; the descriptor
+// itself stays open until the destructor, so it cannot be reused by another
+// socket while that thread still holds the old number.
 void TcpConn::close() {
   int fd = fd_.exchange(-1);
-  if (fd >= 0) {
-    shutdown(fd, SHUT_RDWR);
-    ::close(fd);
-  }
+  if (fd >= 0) shutdown(fd, SHUT_RDWR);
 }
 
 TcpListener::TcpListener(const std::string& host, int port) : fd_(-1), host_(host) {
@@ -215,10 +218,14 @@ TcpListener::TcpListener(const std::string& host, int port) : fd_(-1), host_(hos
   getsockname(fd, (sockaddr*)&ss, &sl);
   port_ = ss.ss_family == AF_INET ? ntohs(((sockaddr_in*)&ss)->sin_port)
                                   : ntohs(((sockaddr_in6*)&ss)->sin6_port);
+  own_fd_ = fd;
   fd_ = fd;
 }
 
-TcpListener::~TcpListener() { close(); }
+TcpListener::~TcpListener() {
+  close();
+  if (own_fd_ >= 0) ::close(own_fd_);
+}
 
 std::shared_ptr<TcpConn> TcpListener::accept() {
   while (true) {
@@ -235,10 +242,7 @@ std::shared_ptr<TcpConn> TcpListener::accept() {
 
 void TcpListener::close() {
   int fd = fd_.exchange(-1);
-  if (fd >= 0) {
-    shutdown(fd, SHUT_RDWR);
-    ::close(fd);
-  }
+  if (fd >= 0) shutdown(fd, SHUT_RDWR);  // wakes accept(); the fd is closed by the destructor
 }
 
 std::vector<std::string> local_ipv4_addrs(bool include_loopback) {

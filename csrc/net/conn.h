@@ -81,7 +81,8 @@ class TcpConn : public Conn {
   int fd() const { return fd_; }
 
  private:
-  std::atomic<int> fd_;
+  std::atomic<int> fd_;  // -1 once close() ran; readers/writers check it
+  int own_fd_;           // released only by the destructor: no fd reuse under a reader
   int timeout_ms_ = 0;
   std::string remote_;
   std::mutex wmu_;
@@ -98,6 +99,7 @@ class TcpListener {
 
  private:
   std::atomic<int> fd_;
+  int own_fd_ = -1;  // released by the destructor (close() only shuts it down)
   int port_ = 0;
   std::string host_;
 };

@@ -167,12 +167,17 @@ int HttpServer::start(const std::string& addr) {
         active_--;
       }).detach();
     }
+    std::lock_guard<std::mutex> lk(mu_);
+    accept_exited_ = true;
+    exit_cv_.notify_all();
   });
   return port_;
 }
 
 void HttpServer::serve_forever() {
-  if (accept_thread_.joinable()) accept_thread_.join();
+  if (!listener_) return;  // never started
+  std::unique_lock<std::mutex> lk(mu_);
+  exit_cv_.wait(lk, [this] { return accept_exited_; });
 }
 
 void HttpServer::stop() {

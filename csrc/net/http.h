@@ -9,6 +9,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -73,6 +74,10 @@ class HttpServer {
   bool access_log_ = true;
   std::mutex mu_;
   std::vector<std::weak_ptr<TcpConn>> conns_;
+  // serve_forever() waits on this instead of joining: stop() is the only joiner of
+  // accept_thread_ (two concurrent joins of one std::thread are undefined behaviour)
+  std::condition_variable exit_cv_;
+  bool accept_exited_ = false;
 };
 
 struct HttpResult {

@@ -213,7 +213,10 @@ def test_identity_and_inbox_persistence(procs, tmp_path):
     b = start_node(procs, "B", d, {"IDENTITY_FILE": idf, "INBOX_FILE": ibf})
     pid1 = json.loads(http("GET", b + "/me")[1])["peer_id"]
     assert http("POST", a + "/send", {"to_username": "B", "content": "persist me"})[0] == 200
-    time.sleep(0.3)
+    for _ in range(200):  # "sent" = bytes written; the receiver pushes asynchronously
+        if json.loads(http("GET", b + "/inbox")[1]):
+            break
+        time.sleep(0.05)
     procs.procs[-1].terminate()
     procs.procs[-1].wait()
     b2 = start_node(procs, "B", d, {"IDENTITY_FILE": idf, "INBOX_FILE": ibf})
