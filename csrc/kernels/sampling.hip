@@ -1,0 +1,290 @@
+// Ollama-style stochastic sampling on the GPU: temperature -> top-k ->
+// top-p -> multinomial draw, one workgroup per row, graph-capturable (all
+// per-row parameters live in device memory; the random stream is a counter-based
+// hash of (seed, position, token id), so a replayed graph draws fresh numbers
+// every step without host state).
+//
+// Per row (1024 threads = 16 waves, the logits row stays L2-resident across passes):
+//   1. top-k threshold by an MSB-first radix select over the order-preserving
+//      32-bit keys of the fp32 logits: 4 passes of 8 bits, per-wave LDS histograms
+//      (16 x 256 bins) summed, wave 0 finds the bin holding the k-th largest by a
+//      shuffle suffix-scan.  The k-th largest key T is exact after 4 passes.
+//   2. collect the k candidates: every key > T, then the keys == T with the lowest
+//      ids (a second radix select over ~id, only when the k-th value is tied).
+//   3. bitonic sort of the (<= 128) candidates in LDS, descending value, ascending id.
+//   4. softmax(v / temperature) over them, inclusive cumsum; keep the smallest
+//      prefix whose mass reaches top_p (drop i when cum_i - p_i > top_p).
+//   5. exponential race: token = argmax_i p_i / E_i with E_i ~ Exp(1) -- exactly a
+//      draw from the renormalised kept distribution.
+// temperature <= 0 rows are greedy (argmax, lowest id on ties, like torch).
+// The same semantics as engine/sampling.py (the CPU reference and the test oracle).
+#include "common.h"
+
+namespace {
+
+constexpr int THREADS = 1024;
+constexpr int NWAVES = THREADS / 64;
+constexpr int KMAX = 128;
+
+__device__ __forceinline__ unsigned ord_key(float v) {
+  unsigned u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// splitmix64 finaliser: a well-mixed 64-bit hash of the draw's coordinates
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// uniform in (0, 1) from (seed, pos, token): 24 random bits, centred in their cell
+__device__ __forceinline__ float uniform01(unsigned long long seed, int pos, int tok) {
+  const unsigned long long h =
+      mix64(seed ^ mix64(((unsigned long long)(unsigned)pos << 32) | (unsigned)tok));
+  return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+template <typename F>
+__device__ __forceinline__ void for_each_key(const float* __restrict__ row, int V, bool vec, F f) {
+  if (vec) {
+    const float4* r4 = reinterpret_cast<const float4*>(row);
+    for (int i = threadIdx.x; i < (V >> 2); i += THREADS) {
+      const float4 x = r4[i];
+      f(4 * i + 0, x.x);
+      f(4 * i + 1, x.y);
+      f(4 * i + 2, x.z);
+      f(4 * i + 3, x.w);
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += THREADS) f(i, row[i]);
+  }
+}
+
+__global__ __launch_bounds__(THREADS) void sample_kernel(
+    const float* __restrict__ logits, int ld, int V, const float* __restrict__ temp,
+    const int* __restrict__ topk, const float* __restrict__ topp,
+    const unsigned long long* __restrict__ seeds, const int* __restrict__ pos,
+    int* __restrict__ out) {
+  const int r = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* row = logits + (size_t)r * ld;
+  const bool vec = ((ld | V) & 3) == 0;
+  const float T = temp[r];
+
+  __shared__ int hist[NWAVES][256];
+  __shared__ float cv[KMAX];
+  __shared__ int ci[KMAX];
+  __shared__ int s_bin, s_kr, s_cnt, s_ngt, s_ntie;
+  __shared__ float s_bestv[NWAVES];
+  __shared__ int s_besti[NWAVES];
+
+  if (!(T > 0.f)) {  // greedy
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for_each_key(row, V, vec, [&](int i, float x) {
+      if (x > bv || (x == bv && i < bi)) { bv = x; bi = i; }
+    });
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { s_bestv[w] = bv; s_besti[w] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int i = 1; i < NWAVES; ++i)
+        if (s_bestv[i] > bv || (s_bestv[i] == bv && s_besti[i] < bi)) { bv = s_bestv[i]; bi = s_besti[i]; }
+      out[r] = bi == 0x7fffffff ? 0 : bi;
+    }
+    return;
+  }
+
+  int k = topk[r];
+  if (k <= 0 || k > KMAX) k = KMAX;
+  if (k > V) k = V;
+
+  // ---- 1. radix select of the k-th largest (value, -id) pair ----
+  // One MSB-first 8-bit digit per pass over keys that match the prefix so far.
+  // Phase A selects on the value key; if the k-th value is tied with more keys than
+  // remain to be taken, phase B selects among those ties on ~id (ascending ids win),
+  // so the candidate set is exact and deterministic.
+  auto radix_pass = [&](int shift, auto&& digit_of) {  // returns via s_bin / s_kr / s_cnt
+    for (int i = lane; i < 256; i += 64) hist[w][i] = 0;
+    __syncthreads();
+    for_each_key(row, V, vec, [&](int i, float x) {
+      unsigned d;
+      if (digit_of(i, x, &d)) atomicAdd(&hist[w][d], 1);
+    });
+    __syncthreads();
+    if (w == 0) {
+      int c[4];
+      int s = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int t = 0;
+#pragma unroll
+        for (int ww = 0; ww < NWAVES; ++ww) t += hist[ww][4 * lane + j];
+        c[j] = t;
+        s += t;
+      }
+      // suf = sum of lane totals at lanes >= this lane (bins >= 4*lane)
+      int suf = s;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_down(suf, o, 64);
+        if (lane + o < 64) suf += t;
+      }
+      int above = suf - s;  // keys in bins > 4*lane+3
+      const int kr0 = s_kr;
+      if (above < kr0 && suf >= kr0) {  // the kr-th largest lies in this lane's 4 bins
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+          if (above + c[j] >= kr0) {
+            s_bin = 4 * lane + j;
+            s_cnt = c[j];
+            s_kr = kr0 - above;
+            break;
+          }
+          above += c[j];
+        }
+      }
+    }
+    __syncthreads();
+  };
+  if (tid == 0) s_kr = k;
+  unsigned prefix = 0u, mask = 0u;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    radix_pass(shift, [&](int, float x, unsigned* d) {
+      const unsigned u = ord_key(x);
+      *d = (u >> shift) & 255u;
+      return (u & mask) == prefix;
+    });
+    prefix |= (unsigned)s_bin << shift;
+    mask |= 255u << shift;
+  }
+  // prefix = value key of the k-th largest; s_kr of its s_cnt equal keys are taken
+  const int kr = s_kr;
+  const int n_gt = k - kr;
+  unsigned idthr = 0u;  // ties taken: ~id >= idthr (all of them when idthr == 0)
+  if (s_cnt > kr) {
+    unsigned ip = 0u, im = 0u;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      radix_pass(shift, [&](int i, float x, unsigned* d) {
+        const unsigned u = ~(unsigned)i;
+        *d = (u >> shift) & 255u;
+        return ord_key(x) == prefix && (u & im) == ip;
+      });
+      ip |= (unsigned)s_bin << shift;
+      im |= 255u << shift;
+    }
+    idthr = ip;
+  }
+
+  // ---- 2. collect the k candidates ----
+  if (tid == 0) {
+    s_ngt = 0;
+    s_ntie = 0;
+  }
+  __syncthreads();
+  for_each_key(row, V, vec, [&](int i, float x) {
+    const unsigned u = ord_key(x);
+    if (u > prefix) {
+      const int sidx = atomicAdd(&s_ngt, 1);
+      if (sidx < KMAX) { cv[sidx] = x; ci[sidx] = i; }
+    } else if (u == prefix && ~(unsigned)i >= idthr) {
+      const int sidx = atomicAdd(&s_ntie, 1);
+      if (sidx < kr) { cv[n_gt + sidx] = x; ci[n_gt + sidx] = i; }
+    }
+  });
+  __syncthreads();
+
+  // ---- 3. bitonic sort (descending value, ascending id), KMAX slots padded ----
+  if (tid < KMAX && tid >= k) {
+    cv[tid] = -INFINITY;
+    ci[tid] = 0x7fffffff;
+  }
+  __syncthreads();
+  for (int size = 2; size <= KMAX; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (tid < KMAX) {
+        const int j = tid ^ stride;
+        if (j > tid) {
+          const bool desc = (tid & size) == 0;  // descending overall
+          const float a = cv[tid], b = cv[j];
+          const int ia = ci[tid], ib = ci[j];
+          // "a before b" in the final (descending value, ascending id) order
+          const bool a_first = a > b || (a == b && ia < ib);
+          if (desc != a_first) {
+            cv[tid] = b; cv[j] = a;
+            ci[tid] = ib; ci[j] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- 4 + 5. softmax / top-p / exponential race, wave 0 (2 slots per lane) ----
+  if (w == 0) {
+    const float vmax = cv[0];
+    const float invT = 1.f / T;
+    float p[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = 2 * lane + j;
+      p[j] = i < k ? __expf((cv[i] - vmax) * invT) : 0.f;
+    }
+    const float tot = wave_sum(p[0] + p[1]);
+    p[0] /= tot;
+    p[1] /= tot;
+    // inclusive prefix sum over slots 0..127 (lane-major: slot 2*lane + j)
+    float ls = p[0] + p[1];
+    float inc = ls;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    const float base = inc - ls;  // mass of slots before 2*lane
+    const float cum0 = base + p[0], cum1 = cum0 + p[1];
+    const float top_p = topp[r];
+    const bool keep0 = 2 * lane < k && (cum0 - p[0]) <= top_p;
+    const bool keep1 = 2 * lane + 1 < k && (cum1 - p[1]) <= top_p;
+    const unsigned long long seed = seeds[r];
+    const int ps = pos[r];
+    float best = -1.f;
+    int bid = 0x7fffffff;
+    if (keep0) {
+      best = p[0] / -__logf(uniform01(seed, ps, ci[2 * lane]));
+      bid = ci[2 * lane];
+    }
+    if (keep1) {
+      const float sc = p[1] / -__logf(uniform01(seed, ps, ci[2 * lane + 1]));
+      if (sc > best) { best = sc; bid = ci[2 * lane + 1]; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bid, o, 64);
+      if (ob > best || (ob == best && oi < bid)) { best = ob; bid = oi; }
+    }
+    if (lane == 0) out[r] = bid == 0x7fffffff ? ci[0] : bid;
+  }
+}
+
+}  // namespace
+
+// ids[r] <- a draw from row r of logits [B, V] (row stride ld) with per-row
+// temperature (<= 0: greedy), top_k (<= 0 or > 128: 128), top_p, and a random
+// stream keyed by (seeds[r], pos[r], token id).
+P2P_API int p2p_sample(const float* logits, int ld, int B, int V, const float* temp,
+                       const int* topk, const float* topp, const unsigned long long* seeds,
+                       const int* pos, int* ids, hipStream_t st) {
+  if (B <= 0 || V <= 0 || ld < V) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(THREADS), 0, st, logits, ld, V, temp, topk, topp,
+                     seeds, pos, ids);
+  return (int)hipGetLastError();
+}

@@ -124,12 +124,16 @@ class Engine:
             self.decode_graph(b, ctx)
 
     # -------------------------------------------------------------- prefill
-    def prefill(self, prompts: list, block_tables: list, return_logits: bool = False):
+    def prefill(self, prompts: list, block_tables: list, return_logits: bool = False,
+                sampling: list | None = None):
         """Run all prompts (flat rows, chunked at max_prefill_tokens).
 
         Returns int32 first tokens [B] on the device (and, with return_logits,
         the fp32 last-position logits [B, V_local] of every sequence).
+        sampling: one SamplingParams per prompt; non-greedy ones draw their first
+        token with ops.sample (else every first token is the fused greedy argmax).
         """
+        sampled = sampling is not None and not all(p.greedy for p in sampling)
         dev = self.device
         B = len(prompts)
         max_ctx = max(len(p) for p in prompts)
@@ -164,7 +168,7 @@ class Engine:
             dev_t = host.to(dev, non_blocking=True)
             seq_d, pos_d, ids_d, slots_d, ctx_d = dev_t[0], dev_t[1], dev_t[2], dev_t[3], dev_t[4]
             out_rows = torch.tensor(outs or [0], dtype=torch.int32).to(dev, non_blocking=True)
-            greedy = all_logits is None
+            greedy = all_logits is None and not sampled
             tiles = tiles_h = None
             if self.flash_prefill_min and R >= self.flash_prefill_min:
                 tiles_h = ops.prefill_tiles(seq.tolist(), pos.tolist())
@@ -176,6 +180,12 @@ class Engine:
                 continue
             if greedy:
                 toks = self.model.finalize_greedy(ws, len(outs))
+            elif sampled:
+                from .sampling import sample
+
+                full = res if self.model.tp == 1 else self.model.comm.all_gather_cols(res)
+                toks = sample(full, [sampling[b] for b in out_seq],
+                              [len(prompts[b]) - 1 for b in out_seq])
             else:
                 toks = self.model.sample_greedy(ws, res)
             sel = torch.tensor(out_seq, dtype=torch.long).to(dev, non_blocking=True)

@@ -38,6 +38,9 @@ class DecodeState:
         self.hist = torch.zeros(B, max_steps, device=dev, dtype=i32)
         self.step = torch.zeros(1, device=dev, dtype=i32)
         self.ws = model.new_workspace(B, max_ctx)
+        from .sampling import SamplerSlots
+
+        self.samp = SamplerSlots(B, dev)  # sampled graphs read these (ops.sample)
 
     def reset_dummy(self):
         self.ids.zero_()
@@ -75,6 +78,18 @@ class DecodeState:
     def advance(self):
         ops.advance(self.ids, self.pos, self.ctx, self.slots, self.bt, self.hist, self.step)
 
+    def body_sampled(self):
+        """Forward + on-device sampling (ops.sample, per-row params in self.samp) +
+        advance: a sampled decode step as one graph replay."""
+        self.body_logits()
+        logits = self.ws.logits[:self.B]
+        m = self.model
+        if m.tp > 1:  # vocab-parallel LM head: every rank samples the full row identically
+            logits = m.comm.all_gather_cols(logits)
+        sp = self.samp
+        ops.sample(logits, sp.temp, sp.topk, sp.topp, sp.seeds, self.pos, out=self.ids)
+        self.advance()
+
     def body(self):
         m = self.model
         keys = m.forward(self.ws, self.ids, self.pos, self.slots, self.bt, self.row_bt, self.ctx,
@@ -100,7 +115,7 @@ class DecodeGraph:
         if self.greedy:
             self.state.body()
         else:
-            self.state.body_logits()
+            self.state.body_sampled()
 
     def capture(self, warmup: int = 2):
         st = self.state
@@ -140,16 +155,14 @@ class DecodeGraph:
             else:
                 self.state.body()
 
-    def step_sampled(self, params: list, generator=None):
-        """One decode step with per-row SamplingParams (non-greedy rows sample)."""
-        from .sampling import sample
-
-        st = self.state
-        if self.graph is not None:
-            self.graph.replay()
-        else:
-            st.body_logits()
-        ids = sample(st.ws.logits[:st.B], list(params) + [params[-1]] * (st.B - len(params)),
-                     generator)
-        st.ids.copy_(ids)
-        st.advance()
+    def step_sampled(self, params: list, n: int = 1):
+        """n decode steps with per-row SamplingParams (temperature <= 0 rows stay greedy):
+        the parameters are loaded into device slots (only when they change), then each
+        step is one replay -- forward, ops.sample and advance are all in the graph."""
+        assert not self.greedy
+        self.state.samp.load(params)
+        for _ in range(n):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self.state.body_sampled()

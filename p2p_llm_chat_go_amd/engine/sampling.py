@@ -3,15 +3,18 @@ and Ollama-style temperature / top-k / top-p sampling for requests that ask for
 it (``options`` of ``/api/generate``; Ollama's defaults are temperature 0.8,
 top_k 40, top_p 0.9).
 
-The stochastic path runs on the logits of a graph-captured forward: top-k is
-taken first (k <= 128, so the full-vocab softmax is never materialised), then
-top-p over the k survivors, then an exponential-race draw (argmax of
-p / Exp(1)), which is equivalent to multinomial sampling and needs one random
-tensor per step.  Rows with temperature <= 0 are greedy.
+The stochastic path is ``ops.sample`` (csrc/kernels/sampling.hip), captured in
+the decode graph right after the LM head: top-k first (k <= 128, radix select,
+so the full-vocab softmax is never materialised), then top-p over the k
+survivors, then an exponential-race draw (argmax of p / Exp(1)), equivalent to
+multinomial sampling.  The random stream is keyed by (request seed, position,
+token id), so replays draw fresh numbers with no host state and a given seed
+reproduces a reply.  Rows with temperature <= 0 are greedy.
 """
 from __future__ import annotations
 
 import dataclasses
+import random
 
 import torch
 
@@ -29,6 +32,12 @@ class SamplingParams:
     def greedy(self) -> bool:
         return self.temperature <= 0.0
 
+    def resolved_seed(self) -> int:
+        """The request's random-stream key: ``seed`` if given, else drawn once per request."""
+        if self.seed is None:
+            self.seed = random.getrandbits(62)
+        return int(self.seed) & ((1 << 63) - 1)
+
     @classmethod
     def from_ollama(cls, options: dict | None, default_max: int = 128) -> "SamplingParams":
         o = options or {}
@@ -39,30 +48,43 @@ class SamplingParams:
                    top_p=float(o.get("top_p", 0.9)), seed=o.get("seed"), max_tokens=max(1, n))
 
 
-def sample(logits: torch.Tensor, params: list, generator: torch.Generator | None = None):
-    """logits [B, V] fp32 -> int32 token ids [B] (one SamplingParams per row)."""
+class SamplerSlots:
+    """Per-row sampling parameters of a decode batch as device tensors, read by the
+    graph-captured ``ops.sample`` launch (so a sampled decode step replays like a
+    greedy one).  ``load`` copies only when the batch's parameters change."""
+
+    def __init__(self, B: int, device):
+        self.B = B
+        self.temp = torch.zeros(B, device=device, dtype=torch.float32)
+        self.topk = torch.full((B,), 40, device=device, dtype=torch.int32)
+        self.topp = torch.full((B,), 0.9, device=device, dtype=torch.float32)
+        self.seeds = torch.zeros(B, device=device, dtype=torch.int64)
+        self._key = None
+
+    def load(self, params: list):
+        params = list(params[:self.B]) + [SamplingParams()] * (self.B - len(params))
+        key = tuple((p.temperature, p.top_k, p.top_p, p.resolved_seed()) for p in params)
+        if key == self._key:
+            return
+        self.temp.copy_(torch.tensor([k[0] for k in key], dtype=torch.float32))
+        self.topk.copy_(torch.tensor([k[1] for k in key], dtype=torch.int32))
+        self.topp.copy_(torch.tensor([k[2] for k in key], dtype=torch.float32))
+        self.seeds.copy_(torch.tensor([k[3] for k in key], dtype=torch.int64))
+        self._key = key
+
+
+def sample(logits: torch.Tensor, params: list, pos) -> torch.Tensor:
+    """logits [B, V] fp32 -> int32 token ids [B] (one SamplingParams per row; pos =
+    the position each row's token is drawn for).  Runs ops.sample (the GPU kernel,
+    or its PyTorch reference on CPU tensors)."""
+    from .. import ops
+
     B = logits.shape[0]
-    out = logits.argmax(-1).to(torch.int32)
-    rows = [i for i, p in enumerate(params[:B]) if not p.greedy]
-    if not rows:
-        return out
-    idx = torch.tensor(rows, device=logits.device)
-    lg = logits.index_select(0, idx)
-    temps = torch.tensor([params[i].temperature for i in rows], device=logits.device)
-    ks = [max(1, min(int(params[i].top_k) if params[i].top_k > 0 else 128, 128)) for i in rows]
-    kmax = max(ks)
-    vals, ids = lg.topk(kmax, dim=-1)
-    kmask = torch.arange(kmax, device=logits.device)[None, :] >= torch.tensor(
-        ks, device=logits.device)[:, None]
-    vals = vals / temps[:, None]
-    vals = vals.masked_fill(kmask, float("-inf"))
-    probs = torch.softmax(vals, dim=-1)
-    tps = torch.tensor([params[i].top_p for i in rows], device=logits.device)
-    cum = probs.cumsum(-1)
-    drop = (cum - probs) > tps[:, None]  # keep the smallest prefix with mass >= top_p
-    probs = probs.masked_fill(drop, 0.0)
-    probs = probs / probs.sum(-1, keepdim=True)
-    e = torch.empty_like(probs).exponential_(1.0, generator=generator)
-    choice = (probs / e).argmax(-1)
-    out[idx] = ids.gather(1, choice[:, None])[:, 0].to(torch.int32)
-    return out
+    params = list(params[:B]) + [SamplingParams()] * (B - len(params))
+    dev = logits.device
+    temp = torch.tensor([p.temperature for p in params], dtype=torch.float32).to(dev)
+    topk = torch.tensor([p.top_k for p in params], dtype=torch.int32).to(dev)
+    topp = torch.tensor([p.top_p for p in params], dtype=torch.float32).to(dev)
+    seeds = torch.tensor([p.resolved_seed() for p in params], dtype=torch.int64).to(dev)
+    pos = torch.as_tensor(pos, dtype=torch.int32).to(dev)
+    return ops.sample(logits, temp, topk, topp, seeds, pos)

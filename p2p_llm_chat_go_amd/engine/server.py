@@ -51,7 +51,6 @@ class EngineServer:
         self._pending = []   # (prompt_ids, params, future, t_submit) waiting to enter the scheduler
         self._cancels = set()  # futures whose requests should stop
         self._stop = False
-        self._gen = torch.Generator(device=engine.device)
         self.stats = {"requests": 0, "tokens": 0, "prefill_tokens": 0, "decode_steps": 0,
                       "busy_s": 0.0}
         self._thread = threading.Thread(target=self._loop, name="engine-loop", daemon=True)
@@ -255,7 +254,8 @@ class EngineServer:
             for i in plan.prefill:
                 self._reqs[i]["t_admit"] = t0
             with span("server.prefill", batch=len(prompts)):
-                first = eng.prefill(prompts, pages).cpu().tolist()
+                first = eng.prefill(prompts, pages, sampling=[self._reqs[i]["params"]
+                                                              for i in plan.prefill]).cpu().tolist()
             t1 = time.perf_counter_ns()
             self.stats["prefill_tokens"] += sum(len(p) for p in prompts)
             for i, tkn in zip(plan.prefill, first):
@@ -283,8 +283,7 @@ class EngineServer:
             if greedy:
                 g.replay(k)
             else:
-                for _ in range(k):
-                    g.step_sampled(params, self._gen)
+                g.step_sampled(params, k)
         hist = st.hist[:len(running), :k].cpu().tolist()
         eng.model.check_faults(st.ws)
         self.stats["decode_steps"] += k

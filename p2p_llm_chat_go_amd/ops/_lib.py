@@ -61,6 +61,8 @@ _SIGS = {
     "p2p_skinny_gemm_qkv_rope": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float,
                                  c_int, c_void_p],
+    "p2p_sample": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                   c_void_p, c_void_p],
     "p2p_tiled_gemm": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                        c_int, c_float, c_void_p],
     "p2p_tiled_gemm_qkv_rope": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,

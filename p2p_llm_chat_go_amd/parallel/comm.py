@@ -104,6 +104,12 @@ class TPComm:
         dist.all_to_all_single(a, b, group=self.group)
         return out
 
+    def all_gather_cols(self, t: torch.Tensor):
+        """[B, n] per rank -> [B, world * n] (rank-major columns: vocab-parallel logits)."""
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.cat(parts, 1)
+
     def all_gather_rows(self, t: torch.Tensor):
         parts = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(parts, t, group=self.group)

@@ -122,3 +122,35 @@ def test_tiny_mixtral(dev):
     res = eng.generate(prompts, max_new_tokens=6, stop_on_eos=False)
     for p, r in zip(prompts, res):
         _greedy_ok(sd, cfg, p, r.tokens)
+
+
+@pytest.mark.gpu
+def test_sampled_decode_graph_gpu():
+    """Sampled decode steps are one graph replay each (forward + ops.sample + advance):
+    temperature 0 rows reproduce the greedy graph exactly; a fixed seed reproduces a
+    sampled continuation, graph == eager."""
+    from p2p_llm_chat_go_amd.engine.sampling import SamplingParams
+
+    cfg = TINY_LLAMA.replace(n_layers=2)
+    w = EngineWeights.random(cfg, "cuda", seed=9)
+    prompts = [[1, 2, 3, 4, 5], [7] * 40]
+
+    def run(greedy, params, use_graph=True, n=12):
+        eng = Engine(cfg, weights=w, device="cuda", kv_pages=32, max_batch=2,
+                     use_graph=use_graph)
+        pages = [eng.kv.allocator.alloc(2) for _ in prompts]
+        first = eng.prefill(prompts, pages).cpu().tolist()
+        g = eng.decode_graph(2, 128, greedy=greedy)
+        g.state.load(first, [len(p) for p in prompts], pages)
+        if greedy:
+            g.replay(n)
+        else:
+            g.step_sampled(params, n)
+        return g.state.hist[:2, :n].cpu().tolist()
+
+    ref = run(True, None)
+    assert run(False, [SamplingParams(temperature=0.0)] * 2) == ref
+    hot = [SamplingParams(temperature=1.3, top_k=64, top_p=0.95, seed=s) for s in (5, 6)]
+    a = run(False, hot)
+    assert a == run(False, hot) == run(False, hot, use_graph=False)
+    assert a != ref

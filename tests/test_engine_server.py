@@ -245,3 +245,59 @@ def test_server_cancel_and_stream_disconnect():
         assert srv.sched.free_pages == free0
     finally:
         srv.close()
+
+
+def test_sampling_reference_semantics():
+    """ops.sample's reference (the GPU kernel's oracle): top-k then top-p keep set,
+    greedy rows, reproducible draws per (seed, position), and draws that follow the
+    kept distribution."""
+    import torch
+
+    from p2p_llm_chat_go_amd import ops
+    from p2p_llm_chat_go_amd.ops import sampling as S
+
+    torch.manual_seed(0)
+    lg = torch.randn(3, 500) * 2
+    ids, p = S.keep_set(lg[0], 0.7, 5, 1.0)
+    assert len(ids) == 5 and torch.equal(ids, lg[0].topk(5).indices)
+    assert abs(float(p.sum()) - 1) < 1e-6 and bool((p[:-1] >= p[1:]).all())
+    ids2, _ = S.keep_set(lg[0], 0.7, 40, 0.5)
+    q = torch.softmax(lg[0].topk(40).values / 0.7, -1)
+    n_keep = int(((q.cumsum(-1) - q) <= 0.5).sum())
+    assert len(ids2) == n_keep and 1 <= n_keep < 40
+    args = (torch.tensor([0.0, 0.8, 0.8]), torch.tensor([40, 40, 40], dtype=torch.int32),
+            torch.tensor([0.9, 0.9, 0.9]), torch.tensor([1, 2, 2]))
+    a = ops.sample(lg, *args, torch.tensor([7, 7, 7], dtype=torch.int32))
+    b = ops.sample(lg, *args, torch.tensor([7, 7, 7], dtype=torch.int32))
+    assert torch.equal(a, b) and int(a[0]) == int(lg[0].argmax())
+    # empirical frequencies over positions (fresh draws) match the kept distribution
+    row = torch.tensor([[4.0, 3.5, 3.0, 0.0, -1.0] + [-9.0] * 20])
+    ids, p = S.keep_set(row[0], 1.0, 3, 1.0)
+    cnt = torch.zeros(3)
+    n = 3000
+    for t in range(n):
+        tok = int(ops.sample(row, torch.tensor([1.0]), torch.tensor([3], dtype=torch.int32),
+                             torch.tensor([1.0]), torch.tensor([11]),
+                             torch.tensor([t], dtype=torch.int32))[0])
+        assert tok in (0, 1, 2)
+        cnt[tok] += 1
+    assert (cnt / n - p[torch.argsort(ids)]).abs().max() < 0.03
+
+
+def test_server_sampled_requests_reproducible_with_seed():
+    """/api/generate with options.seed: the same seed replays the same reply (draws are
+    keyed by (seed, position, token)); the first token is sampled too."""
+    srv, _, _ = make_server()
+    try:
+        def gen(seed):
+            req = {"model": "m", "prompt": "hello there", "stream": False,
+                   "options": {"temperature": 1.5, "top_k": 50, "top_p": 0.95,
+                               "num_predict": 8, "seed": seed}}
+            return json.loads(srv.handle_json(json.dumps(req)))["response"]
+
+        a, b = gen(123), gen(123)
+        assert a == b
+        outs = {gen(s) for s in range(6)}
+        assert len(outs) > 1  # different seeds draw different replies
+    finally:
+        srv.close()
