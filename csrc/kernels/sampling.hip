@@ -8,7 +8,9 @@
 //   1. top-k threshold by an MSB-first radix select over the order-preserving
 //      32-bit keys of the fp32 logits: 4 passes of 8 bits, per-wave LDS histograms
 //      (16 x 256 bins) summed, wave 0 finds the bin holding the k-th largest by a
-//      shuffle suffix-scan.  The k-th largest key T is exact after 4 passes.
+//      shuffle suffix-scan.  The k-th largest key T is exact after 4 passes.  A
+//      prefilter first bounds T from below by the k-th largest per-thread maximum,
+//      so the passes run over a few hundred LDS-resident entries, not the row.
 //   2. collect the k candidates: every key > T, then the keys == T with the lowest
 //      ids (a second radix select over ~id, only when the k-th value is tied).
 //   3. bitonic sort of the (<= 128) candidates in LDS, descending value, ascending id.
@@ -25,10 +27,15 @@ namespace {
 constexpr int THREADS = 1024;
 constexpr int NWAVES = THREADS / 64;
 constexpr int KMAX = 128;
+constexpr int CAP = 4096;  // prefiltered candidates held in LDS
 
 __device__ __forceinline__ unsigned ord_key(float v) {
   unsigned u = __float_as_uint(v);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ float key_float(unsigned u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
 // splitmix64 finaliser: a well-mixed 64-bit hash of the draw's coordinates
@@ -76,7 +83,10 @@ __global__ __launch_bounds__(THREADS) void sample_kernel(
   __shared__ int hist[NWAVES][256];
   __shared__ float cv[KMAX];
   __shared__ int ci[KMAX];
-  __shared__ int s_bin, s_kr, s_cnt, s_ngt, s_ntie;
+  __shared__ int s_bin, s_kr, s_cnt, s_ngt, s_ntie, s_nc;
+  __shared__ unsigned s_tmk[THREADS];  // per-thread max keys (prefilter)
+  __shared__ unsigned s_ck[CAP];       // prefiltered candidates: key, id
+  __shared__ int s_ci[CAP];
   __shared__ float s_bestv[NWAVES];
   __shared__ int s_besti[NWAVES];
 
@@ -107,16 +117,17 @@ __global__ __launch_bounds__(THREADS) void sample_kernel(
   if (k > V) k = V;
 
   // ---- 1. radix select of the k-th largest (value, -id) pair ----
-  // One MSB-first 8-bit digit per pass over keys that match the prefix so far.
-  // Phase A selects on the value key; if the k-th value is tied with more keys than
-  // remain to be taken, phase B selects among those ties on ~id (ascending ids win),
-  // so the candidate set is exact and deterministic.
-  auto radix_pass = [&](int shift, auto&& digit_of) {  // returns via s_bin / s_kr / s_cnt
+  // One MSB-first 8-bit digit per pass over the keys that match the prefix so far
+  // (per-wave LDS histograms; wave 0 finds the bin by a shuffle suffix-scan).  Phase
+  // A selects on the value key; if the k-th value is tied with more keys than remain
+  // to be taken, phase B selects among those ties on ~id (ascending ids win), so the
+  // candidate set is exact and deterministic.  `each(f)` enumerates (id, key) pairs.
+  auto radix_pass = [&](auto&& each, auto&& digit_of) {  // -> s_bin / s_kr / s_cnt
     for (int i = lane; i < 256; i += 64) hist[w][i] = 0;
     __syncthreads();
-    for_each_key(row, V, vec, [&](int i, float x) {
+    each([&](int i, unsigned key) {
       unsigned d;
-      if (digit_of(i, x, &d)) atomicAdd(&hist[w][d], 1);
+      if (digit_of(i, key, &d)) atomicAdd(&hist[w][d], 1);
     });
     __syncthreads();
     if (w == 0) {
@@ -130,8 +141,7 @@ __global__ __launch_bounds__(THREADS) void sample_kernel(
         c[j] = t;
         s += t;
       }
-      // suf = sum of lane totals at lanes >= this lane (bins >= 4*lane)
-      int suf = s;
+      int suf = s;  // keys in bins >= 4*lane
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const int t = __shfl_down(suf, o, 64);
@@ -154,34 +164,76 @@ __global__ __launch_bounds__(THREADS) void sample_kernel(
     }
     __syncthreads();
   };
-  if (tid == 0) s_kr = k;
-  unsigned prefix = 0u, mask = 0u;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    radix_pass(shift, [&](int, float x, unsigned* d) {
-      const unsigned u = ord_key(x);
-      *d = (u >> shift) & 255u;
-      return (u & mask) == prefix;
-    });
-    prefix |= (unsigned)s_bin << shift;
-    mask |= 255u << shift;
-  }
-  // prefix = value key of the k-th largest; s_kr of its s_cnt equal keys are taken
-  const int kr = s_kr;
-  const int n_gt = k - kr;
-  unsigned idthr = 0u;  // ties taken: ~id >= idthr (all of them when idthr == 0)
-  if (s_cnt > kr) {
-    unsigned ip = 0u, im = 0u;
+  // k-th largest (value key, ~id) among `each`'s pairs: returns (value key, ties taken,
+  // id threshold: ties with ~id >= thr are in)
+  auto select = [&](auto&& each, int kk, unsigned* vkey, int* kr_out, unsigned* idthr) {
+    if (tid == 0) s_kr = kk;
+    unsigned prefix = 0u, mask = 0u;
     for (int shift = 24; shift >= 0; shift -= 8) {
-      radix_pass(shift, [&](int i, float x, unsigned* d) {
-        const unsigned u = ~(unsigned)i;
+      radix_pass(each, [&](int, unsigned u, unsigned* d) {
         *d = (u >> shift) & 255u;
-        return ord_key(x) == prefix && (u & im) == ip;
+        return (u & mask) == prefix;
       });
-      ip |= (unsigned)s_bin << shift;
-      im |= 255u << shift;
+      prefix |= (unsigned)s_bin << shift;
+      mask |= 255u << shift;
     }
-    idthr = ip;
+    const int kr = s_kr;
+    unsigned thr = 0u;
+    if (s_cnt > kr) {
+      unsigned ip = 0u, im = 0u;
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        radix_pass(each, [&](int i, unsigned u, unsigned* d) {
+          const unsigned ni = ~(unsigned)i;
+          *d = (ni >> shift) & 255u;
+          return u == prefix && (ni & im) == ip;
+        });
+        ip |= (unsigned)s_bin << shift;
+        im |= 255u << shift;
+      }
+      thr = ip;
+    }
+    *vkey = prefix;
+    *kr_out = kr;
+    *idthr = thr;
+  };
+  auto each_row = [&](auto&& f) {
+    for_each_key(row, V, vec, [&](int i, float x) { f(i, ord_key(x)); });
+  };
+
+  // Prefilter: the k-th largest of the 1024 per-thread maxima is a key with at least
+  // k row entries at or above it, so only those entries (typically a few hundred)
+  // can be in the top k.  They are gathered to LDS and selected there; a row with
+  // more than CAP such entries (massive ties) is selected over the whole row instead.
+  float tmax = -INFINITY;
+  for_each_key(row, V, vec, [&](int, float x) { tmax = fmaxf(tmax, x); });
+  s_tmk[tid] = ord_key(tmax);
+  unsigned t0key;
+  {
+    int kr_;
+    unsigned thr_;
+    select([&](auto&& f) { f(tid, s_tmk[tid]); }, min(k, THREADS), &t0key, &kr_, &thr_);
   }
+  if (tid == 0) s_nc = 0;
+  __syncthreads();
+  each_row([&](int i, unsigned u) {
+    if (u >= t0key) {
+      const int sidx = atomicAdd(&s_nc, 1);
+      if (sidx < CAP) { s_ck[sidx] = u; s_ci[sidx] = i; }
+    }
+  });
+  __syncthreads();
+  const int nc = s_nc;
+  const bool small = nc <= CAP;
+  auto each_cand = [&](auto&& f) {
+    for (int j = tid; j < nc; j += THREADS) f(s_ci[j], s_ck[j]);
+  };
+  unsigned prefix, idthr;
+  int kr;
+  if (small)
+    select(each_cand, k, &prefix, &kr, &idthr);
+  else
+    select(each_row, k, &prefix, &kr, &idthr);
+  const int n_gt = k - kr;
 
   // ---- 2. collect the k candidates ----
   if (tid == 0) {
@@ -189,16 +241,19 @@ __global__ __launch_bounds__(THREADS) void sample_kernel(
     s_ntie = 0;
   }
   __syncthreads();
-  for_each_key(row, V, vec, [&](int i, float x) {
-    const unsigned u = ord_key(x);
+  auto take = [&](int i, unsigned u) {
     if (u > prefix) {
       const int sidx = atomicAdd(&s_ngt, 1);
-      if (sidx < KMAX) { cv[sidx] = x; ci[sidx] = i; }
+      if (sidx < KMAX) { cv[sidx] = key_float(u); ci[sidx] = i; }
     } else if (u == prefix && ~(unsigned)i >= idthr) {
       const int sidx = atomicAdd(&s_ntie, 1);
-      if (sidx < kr) { cv[n_gt + sidx] = x; ci[n_gt + sidx] = i; }
+      if (sidx < kr) { cv[n_gt + sidx] = key_float(u); ci[n_gt + sidx] = i; }
     }
-  });
+  };
+  if (small)
+    each_cand(take);
+  else
+    each_row(take);
   __syncthreads();
 
   // ---- 3. bitonic sort (descending value, ascending id), KMAX slots padded ----
