@@ -75,6 +75,11 @@ class LlamaModel:
         # MI355X it is 16.5 us vs 14.0 us for the two kernels at 8B / batch 1
         # (profiles/r1_fused_attn_oproj_vs_separate.jsonl), so the two-kernel path stays default.
         self.fuse_attn_oproj = os.environ.get("P2P_FUSED_ATTN_OPROJ", "0") == "1"
+        # TP prefill: row-parallel GEMMs of >= this many rows overlap their all-reduce
+        # (chunked, separate communication stream); decode-size sums use the one-shot AR
+        self.overlap_min_rows = int(os.environ.get("P2P_TP_OVERLAP_MIN_ROWS", "256"))
+        self.overlap_chunks = int(os.environ.get("P2P_TP_OVERLAP_CHUNKS", "4"))
+        self._comm_stream = None
 
     def new_workspace(self, max_rows, max_ctx, max_out_rows=None) -> Workspace:
         return Workspace(self.cfg, max_rows, max_ctx, self.device, self.tp, max_out_rows)
@@ -84,10 +89,35 @@ class LlamaModel:
         """h += x @ W (row-parallel across TP ranks)."""
         if self.tp == 1:
             ops.skinny_gemm(wt, x, ops.EPI_RESID, out=h)
-        else:
-            part = ws.partial[:R]
-            ops.skinny_gemm(wt, x, ops.EPI_STORE, out=part)
-            self.comm.allreduce_add_(h, part)
+            return
+        part = ws.partial[:R]
+        if R >= self.overlap_min_rows and h.device.type == "cuda":
+            return self._row_parallel_overlapped(wt, x, h, part, R)
+        ops.skinny_gemm(wt, x, ops.EPI_STORE, out=part)
+        self.comm.allreduce_add_(h, part)
+
+    def _row_parallel_overlapped(self, wt, x, h, part, R):
+        """Prefill-size row-parallel sum with the all-reduce overlapped with the GEMM:
+        the rows are cut into chunks; chunk i's all-reduce (RCCL over xGMI) + residual
+        add run on a communication stream while the compute stream runs chunk i+1's
+        GEMM (BASELINE north star: "RCCL all-reduce over xGMI overlapped with GEMMs")."""
+        cur = torch.cuda.current_stream(h.device)
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(h.device)
+        cs = self._comm_stream
+        n = max(1, min(self.overlap_chunks, R // 64))
+        step = -(-R // n)
+        step = -(-step // 16) * 16  # whole 16-row MFMA tiles per chunk
+        for a in range(0, R, step):
+            b = min(R, a + step)
+            ops.skinny_gemm(wt, x[a:b], ops.EPI_STORE, out=part[a:b])
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            with torch.cuda.stream(cs):
+                cs.wait_event(ev)
+                self.comm.allreduce_add_(h[a:b], part[a:b])
+        cur.wait_stream(cs)
+        return h
 
     def _mlp(self, lw, ws, R):
         h = ws.h[:R]

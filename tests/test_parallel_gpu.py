@@ -21,8 +21,10 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q, moe, a2a=False):
+def _worker(rank, world, port, q, moe, a2a=False, overlap=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if overlap:  # prefill row-parallel sums chunked onto a communication stream
+        os.environ["P2P_TP_OVERLAP_MIN_ROWS"] = "16"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from p2p_llm_chat_go_amd.engine import Engine
@@ -54,13 +56,15 @@ def _worker(rank, world, port, q, moe, a2a=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("moe,a2a", [(False, False), (True, False), (True, True)])
-def test_virtual_rank_parallel_gpu(moe, a2a):
+@pytest.mark.parametrize("moe,a2a,overlap", [(False, False, False), (False, False, True),
+                                              (True, False, False), (True, True, False)])
+def test_virtual_rank_parallel_gpu(moe, a2a, overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     world = 2
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a, overlap))
+          for r in range(world)]
     [p.start() for p in ps]
     res = [q.get(timeout=600) for _ in range(world)]
     [p.join(timeout=60) for p in ps]
