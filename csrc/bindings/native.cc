@@ -9,6 +9,7 @@
 #include <thread>
 
 #include "net/chat.h"
+#include "net/tls.h"
 #include "net/relay.h"
 #include "runtime/scheduler.h"
 
@@ -36,6 +37,7 @@ NodeConfig cfg_from_dict(const py::dict& d) {
   S("bootstrap", &c.bootstrap);
   S("relays", &c.relays);
   S("key_type", &c.key_type);
+  S("security", &c.security);
   S("identity_file", &c.identity_file);
   S("inbox_file", &c.inbox_file);
   S("engine_url", &c.engine_url);
@@ -49,7 +51,10 @@ NodeConfig cfg_from_dict(const py::dict& d) {
 }
 
 // Noise + yamux self-test over a socketpair: returns the echoed payload.
-std::string secure_echo(const std::string& key_type, const std::string& payload) {
+std::string secure_echo(const std::string& key_type, const std::string& payload,
+                        const std::string& security) {
+  const bool tls = security == "tls";
+  std::string early;  // TLS ALPN muxer agreed by the client side
   int sv[2];
   if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) throw NetError("socketpair");
   KeyType kt = key_type == "rsa" ? KeyType::RSA : KeyType::Ed25519;
@@ -62,10 +67,17 @@ std::string secure_echo(const std::string& key_type, const std::string& payload)
   std::thread srv([&] {
     try {
       auto b1 = std::make_shared<BufConn>(cb);
-      ms_handle(*b1, {"/noise"});
-      auto sec = NoiseConn::handshake(b1, kb, false);
+      ConnPtr sec;
+      bool early_mux = false;
+      if (ms_handle(*b1, {"/noise", kTlsProto}) == kTlsProto) {
+        auto t = TlsConn::handshake(b1, kb, false);
+        early_mux = !t->early_muxer().empty();
+        sec = t;
+      } else {
+        sec = NoiseConn::handshake(b1, kb, false);
+      }
       auto b2 = std::make_shared<BufConn>(sec);
-      ms_handle(*b2, {"/yamux/1.0.0"});
+      if (!early_mux) ms_handle(*b2, {"/yamux/1.0.0"});
       auto sess = std::make_shared<YamuxSession>(b2, false);
       std::mutex m;
       std::condition_variable cv;
@@ -91,10 +103,18 @@ std::string secure_echo(const std::string& key_type, const std::string& payload)
   Bytes got;
   try {
     auto b1 = std::make_shared<BufConn>(ca);
-    ms_select(*b1, "/noise");
-    auto sec = NoiseConn::handshake(b1, ka, true, idb);
+    ConnPtr sec;
+    if (tls) {
+      ms_select(*b1, kTlsProto);
+      auto t = TlsConn::handshake(b1, ka, true, idb);
+      early = t->early_muxer();
+      sec = t;
+    } else {
+      ms_select(*b1, "/noise");
+      sec = NoiseConn::handshake(b1, ka, true, idb);
+    }
     auto b2 = std::make_shared<BufConn>(sec);
-    ms_select(*b2, "/yamux/1.0.0");
+    if (early.empty()) ms_select(*b2, "/yamux/1.0.0");
     auto sess = std::make_shared<YamuxSession>(b2, true);
     sess->start(nullptr);
     StreamPtr s = sess->open_stream();
@@ -112,7 +132,9 @@ std::string secure_echo(const std::string& key_type, const std::string& payload)
   }
   srv.join();
   if (!err.empty()) throw NetError("server: " + err);
-  return std::string(got.begin(), got.end());
+  std::string res(got.begin(), got.end());
+  if (tls && early != "yamux/1.0.0") throw NetError("tls: ALPN did not select the early muxer");
+  return res;
 }
 
 }  // namespace
@@ -157,14 +179,15 @@ PYBIND11_MODULE(_native, m) {
   m.def("parse_rfc3339", &parse_rfc3339);
   m.def("rfc3339_now", &rfc3339_now_local);
   m.def("uuid4", &uuid4);
-  m.def("secure_echo", [](const std::string& kt, const py::bytes& payload) {
+  m.def("secure_echo", [](const std::string& kt, const py::bytes& payload,
+                          const std::string& security) {
     std::string in = payload, out;
     {
       py::gil_scoped_release rel;
-      out = secure_echo(kt, in);
+      out = secure_echo(kt, in, security);
     }
     return py::bytes(out);
-  });
+  }, py::arg("key_type"), py::arg("payload"), py::arg("security") = "noise");
   m.def("chat_message_from_json", [](const std::string& s) {
     return ChatMessage::from_json(Json::parse(s)).to_json().dump();
   });

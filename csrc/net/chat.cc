@@ -230,6 +230,7 @@ NodeConfig NodeConfig::from_env() {
   c.access_log = env_or("GIN_MODE", "debug") != "quiet";
   c.dht_mode = env_or("DHT_MODE", c.dht_mode);
   c.nat_pmp = env_or("NAT_PMP", c.nat_pmp);
+  c.security = env_or("SECURITY", c.security);
   std::string la = env_or("LISTEN_ADDRS", "");
   if (la == "none") {
     c.listen.clear();  // relay-only node
@@ -328,6 +329,7 @@ void Node::on_chat(StreamCtx& c) {
 void Node::start() {
   PrivateKey key = load_or_make_identity(cfg_);
   host_ = std::make_shared<Host>(key);
+  host_->set_security(split_csv(cfg_.security));
   if (cfg_.dht_mode != "off") {
     // created before any listener/dial so identify results feed the routing table
     kad_ = std::make_unique<Kad>(host_, cfg_.dht_mode == "client" ? KadMode::Client : KadMode::Server);

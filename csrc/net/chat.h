@@ -102,6 +102,9 @@ struct NodeConfig {
   // NAT port mapping (reference: libp2p.NATPortMap(), main.go:143): "off" (default here:
   // loopback tests/CI), "on" (default gateway) or an explicit "ip[:port]" NAT-PMP gateway
   std::string nat_pmp = "off";
+  // Secure channels, outbound preference order ("noise", "tls" = /tls/1.0.0); inbound
+  // accepts every listed one.  go-libp2p's default host offers both (TLS first).
+  std::string security = "noise,tls";
   static NodeConfig from_env();
 };
 

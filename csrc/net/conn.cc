@@ -290,6 +290,24 @@ void ms_select(BufConn& c, const std::string& proto) {
   throw NetError("multistream: unexpected response " + r);
 }
 
+std::string ms_select_any(BufConn& c, const std::vector<std::string>& protos) {
+  if (protos.empty()) throw NetError("multistream: nothing to propose");
+  Bytes out = uvarint(strlen(kMultistreamProto) + 1);
+  append(out, std::string(kMultistreamProto) + "\n");
+  put_uvarint(out, protos[0].size() + 1);
+  append(out, protos[0] + "\n");
+  c.write_all(out);
+  std::string h = ms_read(c);
+  if (h != kMultistreamProto) throw NetError("multistream: bad header " + h);
+  for (size_t i = 0;;) {
+    std::string r = ms_read(c);
+    if (r == protos[i]) return r;
+    if (r != "na") throw NetError("multistream: unexpected response " + r);
+    if (++i == protos.size()) throw NetError("protocol not supported: " + protos[0]);
+    ms_write(c, protos[i]);
+  }
+}
+
 std::string ms_handle(BufConn& c, const std::set<std::string>& protos) {
   std::string h = ms_read(c);
   if (h != kMultistreamProto) throw NetError("multistream: bad header " + h);

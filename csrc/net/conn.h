@@ -9,6 +9,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <vector>
 
 #include "crypto.h"
 #include "util.h"
@@ -111,6 +112,8 @@ std::vector<std::string> local_ipv4_addrs(bool include_loopback = true);
 extern const char* kMultistreamProto;  // "/multistream/1.0.0"
 // Initiator: propose `proto`; throws NetError("protocol not supported") on "na".
 void ms_select(BufConn& c, const std::string& proto);
+// Proposes protos in order (falling through on "na"); returns the accepted one.
+std::string ms_select_any(BufConn& c, const std::vector<std::string>& protos);
 // Responder: returns the agreed protocol; throws if the peer gives up.
 std::string ms_handle(BufConn& c, const std::set<std::string>& protos);
 

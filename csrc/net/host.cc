@@ -1,4 +1,5 @@
 #include "host.h"
+#include "tls.h"
 
 #include <string.h>
 
@@ -161,29 +162,59 @@ std::string Host::peer_agent(const PeerId& p) {
 }
 
 // ------------------------------------------------------------ upgrade
+// The secured connection of an upgrade: a Noise or TLS channel, its peer, and the
+// muxer TLS already agreed on through ALPN ("" = negotiate it with multistream).
+struct Secured {
+  ConnPtr conn;
+  PeerId peer;
+  std::string early_muxer;
+};
+
+static Secured secure(const std::string& proto, std::shared_ptr<BufConn> b, const PrivateKey& key,
+                      bool initiator, const PeerId& expected) {
+  if (proto == kTlsProto) {
+    auto t = TlsConn::handshake(b, key, initiator, expected);
+    return {t, t->remote_peer(), t->early_muxer()};
+  }
+  auto n = NoiseConn::handshake(b, key, initiator, expected);
+  return {n, n->remote_peer(), ""};
+}
+
+void Host::set_security(const std::vector<std::string>& order) {
+  std::vector<std::string> ids;
+  for (auto& n : order) {
+    if (n == "noise" || n == kNoiseProto) ids.push_back(kNoiseProto);
+    else if (n == "tls" || n == kTlsProto) ids.push_back(kTlsProto);
+    else throw NetError("unknown security transport: " + n);
+  }
+  if (ids.empty()) throw NetError("no security transport configured");
+  security_ = ids;
+}
+
 SessionPtr Host::upgrade_outbound(ConnPtr raw, const PeerId& expected, bool relayed) {
   raw->set_read_timeout(kUpgradeTimeoutMs);
   auto b1 = std::make_shared<BufConn>(raw);
-  ms_select(*b1, kNoiseProto);
-  auto sec = NoiseConn::handshake(b1, key_, true, expected);
-  auto b2 = std::make_shared<BufConn>(sec);
-  ms_select(*b2, kYamuxProto);
+  const std::string proto = ms_select_any(*b1, security_);
+  Secured sec = secure(proto, b1, key_, true, expected);
+  auto b2 = std::make_shared<BufConn>(sec.conn);
+  if (sec.early_muxer.empty()) ms_select(*b2, kYamuxProto);
   raw->set_read_timeout(0);
   auto sess = std::make_shared<YamuxSession>(b2, true);
-  add_session(sec->remote_peer(), sess, relayed);
+  add_session(sec.peer, sess, relayed);
   return sess;
 }
 
 SessionPtr Host::upgrade_inbound(ConnPtr raw, bool relayed) {
   raw->set_read_timeout(kUpgradeTimeoutMs);
   auto b1 = std::make_shared<BufConn>(raw);
-  ms_handle(*b1, {kNoiseProto});
-  auto sec = NoiseConn::handshake(b1, key_, false);
-  auto b2 = std::make_shared<BufConn>(sec);
-  ms_handle(*b2, {kYamuxProto});
+  const std::string proto =
+      ms_handle(*b1, std::set<std::string>(security_.begin(), security_.end()));
+  Secured sec = secure(proto, b1, key_, false, PeerId());
+  auto b2 = std::make_shared<BufConn>(sec.conn);
+  if (sec.early_muxer.empty()) ms_handle(*b2, {kYamuxProto});
   raw->set_read_timeout(0);
   auto sess = std::make_shared<YamuxSession>(b2, false);
-  add_session(sec->remote_peer(), sess, relayed);
+  add_session(sec.peer, sess, relayed);
   return sess;
 }
 

@@ -86,6 +86,11 @@ class Host {
   // Relay dialer hook (installed by RelayClient).
   std::function<SessionPtr(const Multiaddr& relay, const PeerId& target, int timeout_ms)> relay_dialer;
 
+  // Secure channels: outbound proposals in this order, inbound accepts any of them.
+  // Names: "noise" (/noise), "tls" (/tls/1.0.0).  Default {"noise", "tls"}.
+  void set_security(const std::vector<std::string>& order);
+  std::vector<std::string> security() const { return security_; }
+
   void close();
   bool closed() const { return closed_; }
 
@@ -99,6 +104,7 @@ class Host {
   PrivateKey key_;
   PeerId id_;
   std::string agent_;
+  std::vector<std::string> security_{"/noise", "/tls/1.0.0"};  // protocol ids, preference order
   std::mutex mu_;
   std::map<std::string, StreamHandler> handlers_;
   std::map<PeerId, std::vector<Multiaddr>> peerstore_;

@@ -331,3 +331,45 @@ def test_nat_pmp_port_mapping(procs):
         stop.set()
         t.join(timeout=2)
         srv.close()
+
+
+@pytest.mark.parametrize("sec_a,sec_b,ok", [("tls", "tls", True), ("tls,noise", "noise", True),
+                                            ("noise,tls", "tls", True), ("tls", "noise", False)])
+def test_security_transports(procs, sec_a, sec_b, ok):
+    """SECURITY picks the secure channels (go-libp2p hosts offer /tls/1.0.0 and /noise):
+    outbound proposals fall through multistream "na" to the next one; with no common
+    channel the send fails with the reference's 500 "open stream failed"."""
+    d = start_directory(procs)
+    a = start_node(procs, "A", d, {"SECURITY": sec_a})
+    b = start_node(procs, "B", d, {"SECURITY": sec_b})
+    st, body, _ = http("POST", a + "/send", {"to_username": "B", "content": "over " + sec_a})
+    if not ok:
+        assert st == 500 and json.loads(body)["error"].startswith("open stream failed:")
+        return
+    assert st == 200, body
+    for _ in range(100):
+        got = json.loads(http("GET", b + "/inbox")[1])
+        if got:
+            break
+        time.sleep(0.05)
+    assert got[0]["content"] == "over " + sec_a and got[0]["from_user"] == "A"
+    assert http("POST", b + "/send", {"to_username": "A", "content": "back"})[0] == 200
+
+
+@pytest.mark.parametrize("sec", ["noise", "tls"])
+def test_secure_channel_authenticates_peer(procs, sec):
+    """A directory entry that pairs B's addresses with another identity: the secure
+    handshake proves B's key, the PeerID check fails, nothing is delivered."""
+    from p2p_llm_chat_go_amd.native import load
+
+    d = start_directory(procs)
+    a = start_node(procs, "A", d, {"SECURITY": sec})
+    b = start_node(procs, "B", d, {"SECURITY": sec})
+    me_b = json.loads(http("GET", b + "/me")[1])
+    _, _, other = load().keygen("ed25519")
+    addrs = [x.split("/p2p/")[0] + "/p2p/" + other for x in me_b["addrs"]]
+    http("POST", d + "/register", {"username": "evil", "peer_id": other, "addrs": addrs})
+    st, body, _ = http("POST", a + "/send", {"to_username": "evil", "content": "x"})
+    assert st == 500 and json.loads(body)["error"].startswith("open stream failed:")
+    time.sleep(0.2)
+    assert json.loads(http("GET", b + "/inbox")[1]) == []

@@ -124,9 +124,12 @@ def test_rfc3339(N):
 
 @pytest.mark.parametrize("kt", ["ed25519", "rsa"])
 @pytest.mark.parametrize("size", [0, 1, 65519, 65520, 300_000, 2_000_000])
-def test_noise_yamux_echo(N, kt, size):
+@pytest.mark.parametrize("sec", ["noise", "tls"])
+def test_secure_yamux_echo(N, kt, size, sec):
+    """Noise XX or libp2p TLS 1.3 (self-signed cert + SignedKey extension, ALPN early
+    muxer negotiation) + yamux, over a socketpair, both directions."""
     payload = bytes((i * 7 + 3) % 256 for i in range(size))
-    assert N.secure_echo(kt, payload) == payload
+    assert N.secure_echo(kt, payload, sec) == payload
 
 
 def test_uuid4(N):

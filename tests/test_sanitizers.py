@@ -100,7 +100,7 @@ def test_daemons_clean_under_sanitizer(sanbin, tmp_path):
         wait_http(d + "/health", timeout=60)
         assert http("GET", d + "/lookup")[0] == 400
         a = _node(sp, "A", d, key="rsa")
-        b = _node(sp, "B", d)
+        b = _node(sp, "B", d, {"SECURITY": "tls"})  # A proposes noise, falls to TLS
         assert http("POST", a + "/send", {"to_username": "B", "content": "hi"})[0] == 200
         assert http("POST", b + "/send", {"to_username": "A", "content": "yo"})[0] == 200
         # concurrent sends exercise the yamux session / inbox locking across threads
