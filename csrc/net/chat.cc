@@ -1,5 +1,7 @@
 #include "chat.h"
 
+#include <algorithm>
+
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -231,6 +233,7 @@ NodeConfig NodeConfig::from_env() {
   c.dht_mode = env_or("DHT_MODE", c.dht_mode);
   c.nat_pmp = env_or("NAT_PMP", c.nat_pmp);
   c.security = env_or("SECURITY", c.security);
+  c.upnp = env_or("UPNP", c.upnp);
   std::string la = env_or("LISTEN_ADDRS", "");
   if (la == "none") {
     c.listen.clear();  // relay-only node
@@ -335,7 +338,8 @@ void Node::start() {
     kad_ = std::make_unique<Kad>(host_, cfg_.dht_mode == "client" ? KadMode::Client : KadMode::Server);
   }
   for (auto& l : cfg_.listen) host_->listen(Multiaddr::parse(l));
-  if (cfg_.nat_pmp != "off" && !cfg_.nat_pmp.empty()) setup_nat();
+  if ((cfg_.nat_pmp != "off" && !cfg_.nat_pmp.empty()) || (cfg_.upnp != "off" && !cfg_.upnp.empty()))
+    setup_nat();
   relay_client_ = std::make_unique<RelayClient>(host_);
   host_->set_stream_handler(kChatProto, [this](StreamCtx& c) { on_chat(c); });
   for (auto& r : split_csv(cfg_.relays)) {
@@ -390,40 +394,68 @@ void Node::start() {
 
 void Node::wait() { http_.serve_forever(); }
 
+// NATPortMap (reference main.go:143): NAT-PMP first (NAT_PMP), else UPnP-IGD (UPNP);
+// every TCP listen port is mapped, the external address advertised + registered.
 void Node::setup_nat() {
-  nat_ = std::make_unique<NatPmp>(cfg_.nat_pmp == "on" ? "" : cfg_.nat_pmp, 1000);
-  if (!nat_->ok()) {
-    logf("NAT-PMP: no default gateway");
-    return;
-  }
-  const std::string ext = nat_->external_address();
-  if (ext.empty()) {
-    logf("NAT-PMP: gateway %s did not answer", nat_->gateway().c_str());
-    return;
-  }
-  std::vector<NatMapping> maps;
-  for (auto& a : host_->addrs()) {
-    std::string h;
-    int port = 0;
-    if (!a.tcp_host_port(&h, &port) || a.has(MA_P2P_CIRCUIT)) continue;
-    bool dup = false;
-    for (auto& m : maps) dup |= m.internal_port == port;
-    if (dup) continue;
-    NatMapping m;
-    if (nat_->map_tcp(port, port, 3600, &m)) {
-      maps.push_back(m);
-      host_->add_advertised_addr(
-          Multiaddr::parse("/ip4/" + ext + "/tcp/" + std::to_string(m.external_port)));
-      logf("NAT-PMP: mapped tcp %d -> %s:%d", port, ext.c_str(), m.external_port);
+  auto tcp_ports = [this] {
+    std::vector<int> ports;
+    for (auto& a : host_->addrs()) {
+      std::string h;
+      int port = 0;
+      if (!a.tcp_host_port(&h, &port) || a.has(MA_P2P_CIRCUIT)) continue;
+      if (std::find(ports.begin(), ports.end(), port) == ports.end()) ports.push_back(port);
+    }
+    return ports;
+  };
+  auto advertise = [this](const char* how, const std::string& ext, int port, const NatMapping& m) {
+    host_->add_advertised_addr(
+        Multiaddr::parse("/ip4/" + ext + "/tcp/" + std::to_string(m.external_port)));
+    logf("%s: mapped tcp %d -> %s:%d", how, port, ext.c_str(), m.external_port);
+  };
+  if (cfg_.nat_pmp != "off" && !cfg_.nat_pmp.empty()) {
+    nat_ = std::make_unique<NatPmp>(cfg_.nat_pmp == "on" ? "" : cfg_.nat_pmp, 1000);
+    const std::string ext = nat_->ok() ? nat_->external_address() : "";
+    if (ext.empty()) {
+      logf("NAT-PMP: gateway %s did not answer", nat_->ok() ? nat_->gateway().c_str() : "(none)");
+      nat_.reset();
+    } else {
+      std::vector<NatMapping> maps;
+      for (int port : tcp_ports()) {
+        NatMapping m;
+        if (nat_->map_tcp(port, port, 3600, &m)) {
+          maps.push_back(m);
+          advertise("NAT-PMP", ext, port, m);
+        }
+      }
+      nat_->keep_alive(maps);
+      return;
     }
   }
-  nat_->keep_alive(maps);
+  if (cfg_.upnp != "off" && !cfg_.upnp.empty()) {
+    upnp_ = std::make_unique<UpnpIgd>(cfg_.upnp == "on" ? "" : cfg_.upnp, 2000);
+    const std::string ext = upnp_->discover() ? upnp_->external_address() : "";
+    if (ext.empty()) {
+      logf("UPnP: no internet gateway device answered");
+      upnp_.reset();
+      return;
+    }
+    std::vector<NatMapping> maps;
+    for (int port : tcp_ports()) {
+      NatMapping m;
+      if (upnp_->map_tcp(port, port, 3600, &m)) {
+        maps.push_back(m);
+        advertise("UPnP", ext, port, m);
+      }
+    }
+    upnp_->keep_alive(maps);
+  }
 }
 
 void Node::stop() {
   std::lock_guard<std::mutex> lk(stop_mu_);
   if (stopping_.exchange(true)) return;
   if (nat_) nat_->stop();  // before http_.stop(): that releases wait() and main may exit
+  if (upnp_) upnp_->stop();
   http_.stop();
   if (refresher_.joinable()) refresher_.join();
   if (host_) host_->close();

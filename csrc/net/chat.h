@@ -17,6 +17,7 @@
 #include "json.h"
 #include "kad.h"
 #include "natpmp.h"
+#include "upnp.h"
 #include "relay.h"
 
 namespace p2p {
@@ -102,6 +103,9 @@ struct NodeConfig {
   // NAT port mapping (reference: libp2p.NATPortMap(), main.go:143): "off" (default here:
   // loopback tests/CI), "on" (default gateway) or an explicit "ip[:port]" NAT-PMP gateway
   std::string nat_pmp = "off";
+  // UPnP-IGD port mapping (the other half of NATPortMap): "off", "on" (SSDP multicast),
+  // "ip:port" (unicast M-SEARCH to that responder) or the device description URL
+  std::string upnp = "off";
   // Secure channels, outbound preference order ("noise", "tls" = /tls/1.0.0); inbound
   // accepts every listed one.  go-libp2p's default host offers both (TLS first).
   std::string security = "noise,tls";
@@ -146,6 +150,7 @@ class Node {
   std::unique_ptr<RelayClient> relay_client_;
   std::unique_ptr<Kad> kad_;
   std::unique_ptr<NatPmp> nat_;
+  std::unique_ptr<UpnpIgd> upnp_;
   std::unique_ptr<DirectoryClient> dir_;
   Inbox inbox_;
   HttpServer http_;

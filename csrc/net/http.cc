@@ -345,7 +345,8 @@ bool HttpServer::handle_one(BufConn& bc, TcpConn& raw) {
 
 // ================================================================ client
 HttpResult http_request(const std::string& method, const std::string& url, const std::string& body,
-                        const std::string& content_type, int timeout_ms) {
+                        const std::string& content_type, int timeout_ms,
+                        const std::vector<std::pair<std::string, std::string>>& headers) {
   if (url.rfind("http://", 0) != 0) throw NetError("unsupported URL scheme: " + url);
   std::string rest = url.substr(7);
   size_t slash = rest.find('/');
@@ -368,6 +369,7 @@ HttpResult http_request(const std::string& method, const std::string& url, const
     req += "Content-Length: " + std::to_string(body.size()) + "\r\n";
     if (!content_type.empty()) req += "Content-Type: " + content_type + "\r\n";
   }
+  for (auto& h : headers) req += h.first + ": " + h.second + "\r\n";
   req += "\r\n" + body;
   c->write_all(req);
   BufConn bc(c);

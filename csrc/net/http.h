@@ -90,7 +90,8 @@ struct HttpResult {
 // Throws NetError on connection failure / timeout (like Go's client.Do error).
 HttpResult http_request(const std::string& method, const std::string& url,
                         const std::string& body = "", const std::string& content_type = "",
-                        int timeout_ms = 5000);
+                        int timeout_ms = 5000,
+                        const std::vector<std::pair<std::string, std::string>>& headers = {});
 
 // Splits "host:port" (also "[v6]:port", ":port").
 void split_host_port(const std::string& addr, std::string* host, int* port);

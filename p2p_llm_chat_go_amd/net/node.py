@@ -66,7 +66,7 @@ FLAGS = [
     ("--engine-model", "ENGINE_MODEL"), ("--engine-device", "ENGINE_DEVICE"),
     ("--engine-checkpoint", "ENGINE_CHECKPOINT"), ("--engine-max-batch", "ENGINE_MAX_BATCH"),
     ("--engine-max-tokens", "ENGINE_MAX_TOKENS"), ("--tokenizer", "TOKENIZER_PATH"),
-    ("--engine-url", "ENGINE_URL"), ("--security", "SECURITY"), ("--nat-pmp", "NAT_PMP"),
+    ("--engine-url", "ENGINE_URL"), ("--security", "SECURITY"), ("--nat-pmp", "NAT_PMP"), ("--upnp", "UPNP"),
 ]
 
 

@@ -373,3 +373,89 @@ def test_secure_channel_authenticates_peer(procs, sec):
     assert st == 500 and json.loads(body)["error"].startswith("open stream failed:")
     time.sleep(0.2)
     assert json.loads(http("GET", b + "/inbox")[1]) == []
+
+
+def test_upnp_igd_port_mapping(procs):
+    """UPNP=<ssdp responder>: SSDP M-SEARCH -> device description -> WANIPConnection
+    control URL -> GetExternalIPAddress + AddPortMapping; the external address is
+    advertised and registered, SIGTERM sends DeletePortMapping (reference:
+    libp2p.NATPortMap(), its UPnP half).  The gateway is a fake IGD on loopback."""
+    import re
+    import socket
+    import threading
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+    calls = []
+    desc = ("<?xml version=\"1.0\"?><root xmlns=\"urn:schemas-upnp-org:device-1-0\"><device>"
+            "<deviceType>urn:schemas-upnp-org:device:InternetGatewayDevice:1</deviceType>"
+            "<deviceList><device><deviceList><device><serviceList><service>"
+            "<serviceType>urn:schemas-upnp-org:service:WANIPConnection:1</serviceType>"
+            "<serviceId>urn:upnp-org:serviceId:WANIPConn1</serviceId>"
+            "<controlURL>/ctl/IPConn</controlURL></service></serviceList></device></deviceList>"
+            "</device></deviceList></device></root>")
+
+    class H(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            b = desc.encode()
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(b)))
+            self.end_headers()
+            self.wfile.write(b)
+
+        def do_POST(self):
+            body = self.rfile.read(int(self.headers["Content-Length"])).decode()
+            action = self.headers["SOAPAction"].strip('"').split("#")[1]
+            calls.append((action, body))
+            out = ""
+            if action == "GetExternalIPAddress":
+                out = "<NewExternalIPAddress>198.51.100.9</NewExternalIPAddress>"
+            b = ("<s:Envelope><s:Body><u:%sResponse>%s</u:%sResponse></s:Body></s:Envelope>"
+                 % (action, out, action)).encode()
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(b)))
+            self.end_headers()
+            self.wfile.write(b)
+
+    web = ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=web.serve_forever, daemon=True).start()
+    ssdp = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    ssdp.bind(("127.0.0.1", 0))
+    ssdp.settimeout(0.2)
+    stop = threading.Event()
+
+    def answer():
+        while not stop.is_set():
+            try:
+                data, addr = ssdp.recvfrom(2048)
+            except socket.timeout:
+                continue
+            if data.startswith(b"M-SEARCH"):
+                ssdp.sendto(("HTTP/1.1 200 OK\r\nST: urn:schemas-upnp-org:device:"
+                             "InternetGatewayDevice:1\r\nLOCATION: http://127.0.0.1:%d/rootDesc.xml"
+                             "\r\n\r\n" % web.server_address[1]).encode(), addr)
+    t = threading.Thread(target=answer, daemon=True)
+    t.start()
+    try:
+        d = start_directory(procs)
+        a = start_node(procs, "A", d, {"UPNP": "127.0.0.1:%d" % ssdp.getsockname()[1]})
+        me = json.loads(http("GET", a + "/me")[1])
+        iport = int(me["addrs"][0].split("/tcp/")[1].split("/")[0])
+        ext = "/ip4/198.51.100.9/tcp/%d/p2p/%s" % (iport, me["peer_id"])
+        assert ext in me["addrs"], me["addrs"]
+        assert ext in json.loads(http("GET", d + "/lookup?username=A")[1])["addrs"]
+        add = [b for act, b in calls if act == "AddPortMapping"]
+        assert add and "<NewInternalPort>%d</NewInternalPort>" % iport in add[0]
+        assert re.search(r"<NewInternalClient>127\.0\.0\.1</NewInternalClient>", add[0])
+        node = procs.procs[-1]
+        node.terminate()
+        node.wait(timeout=10)
+        assert any(act == "DeletePortMapping" and "<NewExternalPort>%d<" % iport in b
+                   for act, b in calls), [c[0] for c in calls]
+    finally:
+        stop.set()
+        t.join(timeout=2)
+        ssdp.close()
+        web.shutdown()
