@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--jitter", type=int, default=16,
                     help="reply lengths vary in [new-tokens - jitter, new-tokens]")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--mixed", type=int, default=1,
+                    help="1: running sequences ride in prefill steps (mixed batches)")
     a = ap.parse_args()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device(a.device, local) if a.device == "cuda" else torch.device(a.device)
@@ -44,7 +46,7 @@ def main():
     tok = get_tokenizer(cfg)
     eng = Engine(cfg, device=dev, seed=7, max_batch=max(a.peers, 1), max_prefill_tokens=1024)
     eng.warmup(tuple(sorted({1, 2, 4, 8, a.peers} - {0})), ctx=256)
-    srv = EngineServer(eng, tok, max_batch=a.peers, decode_chunk=8)
+    srv = EngineServer(eng, tok, max_batch=a.peers, decode_chunk=8, mixed=bool(a.mixed))
     prompts = [tok.chat_ids(suggest_prompt(SAMPLE_MESSAGES[i % len(SAMPLE_MESSAGES)]))
                for i in range(a.peers)]
 
@@ -79,7 +81,7 @@ def main():
         "new_tokens": a.new_tokens, "elapsed_s": round(el, 3),
         "ttft_p50_ms": round(statistics.median(ttft), 3),
         "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
-        "mean_batch": round(toks / max(steps, 1), 2), "dtype": "bf16",
+        "mean_batch": round(toks / max(steps, 1), 2), "mixed": bool(a.mixed), "dtype": "bf16",
         "data": "synthetic chat prompts, random-init weights"}), flush=True)
 
 

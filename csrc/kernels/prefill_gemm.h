@@ -305,19 +305,22 @@ static SplitWs g_split_ws;
 // workspace is (re)allocated and re-armed by each tile's last arriver
 constexpr size_t kCounterBytes = 64 * 1024;  // 16384 tiles
 
+// A grown workspace never frees the previous buffer: a hipGraph captured earlier (the
+// decode graph of a mid-M batch bucket routed to this kernel) holds its address and its
+// ticket counters and replays against it for the life of the process.  Growth is
+// geometric, so the retired buffers total less than the live one.
 static bool split_ws(size_t bytes, hipStream_t st, char** out) {
   bytes += kCounterBytes;
   if (g_split_ws.bytes < bytes) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(st, &cs);
     if (cs != hipStreamCaptureStatusNone) return false;  // cannot allocate while capturing
-    (void)hipStreamSynchronize(st);
-    if (g_split_ws.buf) (void)hipFree(g_split_ws.buf);
-    g_split_ws.buf = nullptr;
-    g_split_ws.bytes = 0;
-    if (hipMalloc(&g_split_ws.buf, bytes) != hipSuccess) return false;
-    if (hipMemset(g_split_ws.buf, 0, bytes) != hipSuccess) return false;
-    g_split_ws.bytes = bytes;
+    const size_t want = std::max(bytes, 2 * g_split_ws.bytes);
+    void* buf = nullptr;
+    if (hipMalloc(&buf, want) != hipSuccess) return false;
+    if (hipMemsetAsync(buf, 0, want, st) != hipSuccess) return false;
+    g_split_ws.buf = buf;  // the old buffer stays allocated (see above)
+    g_split_ws.bytes = want;
   }
   *out = (char*)g_split_ws.buf;
   return true;

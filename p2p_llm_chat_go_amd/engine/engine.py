@@ -125,13 +125,16 @@ class Engine:
 
     # -------------------------------------------------------------- prefill
     def prefill(self, prompts: list, block_tables: list, return_logits: bool = False,
-                sampling: list | None = None):
+                sampling: list | None = None, starts: list | None = None):
         """Run all prompts (flat rows, chunked at max_prefill_tokens).
 
         Returns int32 first tokens [B] on the device (and, with return_logits,
         the fp32 last-position logits [B, V_local] of every sequence).
         sampling: one SamplingParams per prompt; non-greedy ones draw their first
         token with ops.sample (else every first token is the fused greedy argmax).
+        starts: per sequence, the first position to run (the KV of earlier positions is
+        already in its pages).  A running sequence rides along as one row (start =
+        its last position): the server mixes decode rows into a prefill this way.
         """
         sampled = sampling is not None and not all(p.greedy for p in sampling)
         dev = self.device
@@ -144,7 +147,8 @@ class Engine:
             bt[b, :len(pages)] = torch.tensor(pages, dtype=torch.int32)
         rows = []  # (seq, pos, token)
         for b, p in enumerate(prompts):
-            rows += [(b, i, t) for i, t in enumerate(p)]
+            s0 = starts[b] if starts else 0
+            rows += [(b, i, p[i]) for i in range(s0, len(p))]
         bt_d = bt.to(dev, non_blocking=True)
         first = torch.zeros(B, dtype=torch.int32, device=dev)
         all_logits = None

@@ -7,6 +7,7 @@ loop:
 
     plan = scheduler.schedule()
     prefill the newly admitted prompts (one flat batch)     -> first tokens (TTFT)
+      ... with one decode row per already-running sequence  (mixed batch)
     decode every running sequence for a chunk of k steps     (hipGraph replays)
     retire finished sequences (EOS / num_predict), free their KV pages
 
@@ -32,12 +33,16 @@ from .tokenizer import get_tokenizer
 class EngineServer:
     def __init__(self, engine: Engine, tokenizer=None, model_name: str = "llama3.1",
                  max_batch: int | None = None, decode_chunk: int = 8,
-                 default_max_tokens: int = 128, max_ctx: int | None = None):
+                 default_max_tokens: int = 128, max_ctx: int | None = None,
+                 mixed: bool = True):
         self.engine = engine
         self.tok = tokenizer or get_tokenizer(engine.cfg)
         self.model_name = model_name
         self.max_batch = max_batch or engine.max_batch
         self.decode_chunk = decode_chunk
+        # a prefill step also advances every running sequence by one token (its row rides
+        # in the prefill batch): admissions no longer stall the running batch for a step
+        self.mixed = mixed
         self.default_max_tokens = default_max_tokens
         self.max_ctx = max_ctx or min(engine.cfg.max_pos, CTX_BUCKETS[-1],
                                       engine.kv.num_pages * 64)
@@ -250,18 +255,32 @@ class EngineServer:
         if plan.prefill:
             prompts = [self._reqs[i]["prompt"] for i in plan.prefill]
             pages = [list(self.sched.get(i).pages) for i in plan.prefill]
+            ride = [i for i in plan.decode if self.sched.get(i).state == 1] if self.mixed else []
+            # riders fill the prefill's last 64-row GEMM tile, never start another one
+            n_rows = sum(len(p) for p in prompts)
+            ride = ride[:max(0, -(-n_rows // 64) * 64 - n_rows)]
+            starts = [0] * len(prompts)
+            for i in ride:  # running sequences: one decode row each (last token at r.pos)
+                r = self.sched.get(i)
+                prompts.append([0] * r.pos + [r.tokens[-1]])
+                pages.append(list(r.pages))
+                starts.append(r.pos)
+            ids = list(plan.prefill) + ride
             t0 = time.perf_counter_ns()
             for i in plan.prefill:
                 self._reqs[i]["t_admit"] = t0
-            with span("server.prefill", batch=len(prompts)):
-                first = eng.prefill(prompts, pages, sampling=[self._reqs[i]["params"]
-                                                              for i in plan.prefill]).cpu().tolist()
+            with span("server.prefill", batch=len(plan.prefill), decode_rows=len(ride)):
+                first = eng.prefill(prompts, pages, sampling=[self._reqs[i]["params"] for i in ids],
+                                    starts=starts if ride else None).cpu().tolist()
             t1 = time.perf_counter_ns()
-            self.stats["prefill_tokens"] += sum(len(p) for p in prompts)
+            self.stats["prefill_tokens"] += sum(len(self._reqs[i]["prompt"]) for i in plan.prefill)
             for i, tkn in zip(plan.prefill, first):
                 self._reqs[i]["t_first"] = t1
                 self.sched.on_first_token(i, int(tkn))
-            self._stream(plan.prefill)
+            if ride:
+                self.sched.on_decode_tokens(ride, [[int(t)] for t in first[len(plan.prefill):]])
+                self.stats["decode_steps"] += 1
+            self._stream(ids)
         running = [i for i in list(plan.decode) + list(plan.prefill)
                    if self.sched.get(i).state == 1]
         if running:

@@ -563,3 +563,38 @@ def test_sample_kernel_matches_reference(V):
             assert int(got[r]) in ids.tolist(), r
         agree += int(got[r]) == int(ref[r])
     assert agree >= B - 2, (agree, B)
+
+
+def test_split_k_workspace_survives_growth_under_captured_graph():
+    """A hipGraph that captured a split-K tiled GEMM keeps working after a later, larger
+    split-K launch grows the workspace (the old buffer must not be freed: the graph holds
+    its address).  Regression: a 32-peer decode graph routed to the tiled kernel faulted
+    after a long prefill chunk regrew the workspace."""
+    from p2p_llm_chat_go_amd.ops.gemm import TILED_FLAG
+
+    torch.manual_seed(5)
+    K = 4096
+    W1 = (torch.randn(1024, K) * 0.02).to(torch.bfloat16)
+    x1 = torch.randn(32, K).to(torch.bfloat16)
+    ref1 = x1.float() @ W1.float().t()
+    w1, xd1 = ops.tile_weight(W1).to(DEV), x1.to(DEV)
+    out1 = torch.zeros(32, 1024, dtype=torch.bfloat16, device=DEV)
+    ops.skinny_gemm(w1, xd1, ops.EPI_STORE, out=out1, waves=TILED_FLAG)  # sizes the workspace
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            ops.skinny_gemm(w1, xd1, ops.EPI_STORE, out=out1, waves=TILED_FLAG)
+    torch.cuda.synchronize()
+    W2 = (torch.randn(4096, K) * 0.02).to(torch.bfloat16)
+    x2 = torch.randn(128, K).to(torch.bfloat16)
+    out2 = ops.skinny_gemm(ops.tile_weight(W2).to(DEV), x2.to(DEV), ops.EPI_STORE)  # grows it
+    torch.cuda.synchronize()
+    assert _rel(out2.cpu(), x2.float() @ W2.float().t()) < 1e-2
+    for _ in range(3):
+        out1.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert _rel(out1.cpu(), ref1) < 1e-2
