@@ -125,7 +125,7 @@ def build_native(force=False, jobs=8):
         name = os.path.splitext(os.path.basename(app))[0]
         exe = os.path.join(BINDIR, name)
         if force or _stale(exe, [app, ar] + hdrs):
-            _run([CXX] + base + [app, ar, "-o", exe] + libs)
+            _run([CXX] + base + [app, ar, "-o", exe] + libs + ["-ldl"])
         outs.append(exe)
     # pybind11 module
     import pybind11
@@ -138,6 +138,17 @@ def build_native(force=False, jobs=8):
             _run([CXX] + base + ["-shared", "-I", pybind11.get_include(), "-I", pyinc] + bind
                  + [ar, "-o", mod] + libs)
         outs.append(mod)
+    # engine C ABI (embeds the interpreter that drives the Python/HIP engine)
+    eng_src = sorted(glob.glob(os.path.join(CSRC, "engine", "*.cc")))
+    if eng_src:
+        lib = os.path.join(LIBDIR, "libp2p_engine.so")
+        pyinc = sysconfig.get_paths()["include"]
+        pylib = ["-L" + (sysconfig.get_config_var("LIBDIR") or "/usr/lib"),
+                 "-lpython%s" % sysconfig.get_config_var("VERSION")]
+        ehdrs = glob.glob(os.path.join(CSRC, "engine", "*.h"))
+        if force or _stale(lib, eng_src + ehdrs):
+            _run([CXX] + base + ["-shared", "-I", pyinc] + eng_src + ["-o", lib] + pylib + ["-ldl"])
+        outs.append(lib)
     return outs
 
 
@@ -184,7 +195,7 @@ def build_sanitized(kind: str, force=False, jobs=8):
         name = os.path.splitext(os.path.basename(app))[0]
         exe = os.path.join(bdir, name)
         if force or _stale(exe, [app] + objs + hdrs):
-            _run([cxx] + base + [app] + objs + ["-o", exe, "-lssl", "-lcrypto", "-pthread"])
+            _run([cxx] + base + [app] + objs + ["-o", exe, "-lssl", "-lcrypto", "-pthread", "-ldl"])
         outs.append(exe)
     return outs
 

@@ -459,3 +459,35 @@ def test_upnp_igd_port_mapping(procs):
         t.join(timeout=2)
         ssdp.close()
         web.shutdown()
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_node_daemon_hosts_engine_in_process(procs, dev):
+    """ENGINE=inproc: the C++ node daemon loads the engine C ABI (libp2p_engine.so,
+    csrc/engine/engine_capi.h) and serves /api/generate (plain and streaming NDJSON)
+    and /suggest from the engine in its own process -- the node links the engine the
+    way the BASELINE north star's Go node links it through cgo (CPU tiny-llama here)."""
+    lib = os.path.join(os.path.dirname(BIN), "p2p_llm_chat_go_amd", "_lib", "libp2p_engine.so")
+    if not os.path.exists(lib):
+        pytest.skip("engine C ABI not built")
+    d = start_directory(procs)
+    port = free_port()
+    env = {"MYNAMEIS": "A", "HTTP_ADDR": "127.0.0.1:%d" % port, "DIRECTORY_URL": d,
+           "KEY_TYPE": "ed25519", "LISTEN_ADDRS": "/ip4/127.0.0.1/tcp/0", "ENGINE": "inproc",
+           "ENGINE_MODEL": "tiny-llama", "ENGINE_DEVICE": dev}
+    procs.spawn("p2p-node", env)
+    a = "http://127.0.0.1:%d" % port
+    wait_http(a + "/me", timeout=120)
+    st, body, _ = http("POST", a + "/api/generate", {"model": "llama3.1", "prompt": "hello",
+                                                      "stream": False,
+                                                      "options": {"num_predict": 5}})
+    out = json.loads(body)
+    assert st == 200 and out["done"] and out["eval_count"] == 5 and out["prompt_eval_count"] > 0
+    st, body, _ = http("POST", a + "/api/generate", {"model": "llama3.1", "prompt": "hello",
+                                                      "options": {"num_predict": 3}})
+    lines = [json.loads(x) for x in body.strip().splitlines()]
+    assert st == 200 and lines[-1]["done"] and lines[-1]["eval_count"] == 3
+    assert "".join(x.get("response", "") for x in lines) == out["response"][:len(
+        "".join(x.get("response", "") for x in lines))]
+    st, body, _ = http("POST", a + "/suggest", {"message": "Hey! How's it going?"})
+    assert st == 200 and "suggestion" in json.loads(body)
