@@ -73,16 +73,23 @@ __global__ __launch_bounds__(512) void moe_router_route_kernel(
     int K, int e_lo, int e_local, int* __restrict__ topk_ids, float* __restrict__ topk_w,
     int* __restrict__ cnt, int* __restrict__ rows, int rows_stride) {
   __shared__ int s_cnt[E];
+  __shared__ float s_part[64][E + 1];  // per (row, H slice): E logit partials + sum of squares
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (threadIdx.x < E) s_cnt[threadIdx.x] = 0;
-  __syncthreads();
-  for (int r = w; r < R; r += nw) {
+  // phase 1: logits.  With few rows the H reduction is split over the waves (a batch-1
+  // decode step would otherwise leave 7 of 8 waves idle behind one serial load chain).
+  const int ns = R >= nw ? 1 : nw / R;  // H slices per row
+  const int C = H / 8;                  // 16-byte chunks per row
+  for (int item = w; item < R * ns; item += nw) {
+    const int r = item / ns, sl = item % ns;
     const bf16x8* hp = reinterpret_cast<const bf16x8*>(h + (size_t)r * ldh);
     float acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = 0.f;
     float ss = 0.f;
-    for (int c = lane; c < H / 8; c += 64) {
+    const int c1 = (sl + 1) * C / ns;
+#pragma unroll 2
+    for (int c = sl * C / ns + lane; c < c1; c += 64) {
       const bf16x8 x = hp[c];
       float xf[8];
 #pragma unroll
@@ -100,6 +107,24 @@ __global__ __launch_bounds__(512) void moe_router_route_kernel(
     ss = wave_sum(ss);
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = wave_sum(acc[e]);
+    if (lane == 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) s_part[item][e] = acc[e];
+      s_part[item][E] = ss;
+    }
+  }
+  __syncthreads();
+  // phase 2: softmax / top-k / slot lists, one wave per row
+  for (int r = w; r < R; r += nw) {
+    float acc[E];
+    float ss = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+    for (int sl = 0; sl < ns; ++sl) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] += s_part[r * ns + sl][e];
+      ss += s_part[r * ns + sl][E];
+    }
     const float rstd = rsqrtf(ss / (float)H + eps);
     float m = -INFINITY;
 #pragma unroll
