@@ -45,7 +45,7 @@ __global__ __launch_bounds__(WAVES * 64) void paged_attn_kernel(
   // read the zero-initialised block-table tail = null page 0, always mapped), so the
   // kernel's dependent-latency chain is row_bt -> page -> K/V, not ctx -> ... -> K/V.
   const int ctx = ctx_lens[r];
-  const int rb = row_bt[r];
+  const int rb = row_bt ? row_bt[r] : r;  // null: row r uses block-table row r (decode)
 
   constexpr int VS = HD + 8;
   __shared__ bf16x2 qs[G][HD / 2];
@@ -215,6 +215,8 @@ int launch_attn(const void* q, int ldq, const void* kc, const void* vc, const in
 
 }  // namespace
 
+// row_bt null = identity (decode batches: row r is sequence r), one dependent load less
+// on the kernel's critical path (row_bt -> page -> K/V becomes page -> K/V).
 // max_ctx bounds the number of 256-key chunks (grid.x); rows whose context is
 // shorter exit early.  part_o / part_ml: workspace of R*Hq*n_chunks*(128 | 2) floats,
 // unused when max_ctx <= 256.

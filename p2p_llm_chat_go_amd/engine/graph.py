@@ -72,7 +72,7 @@ class DecodeState:
 
     def body_logits(self):
         """Forward only (sampling mode): logits of every row in ws.logits."""
-        self.model.forward(self.ws, self.ids, self.pos, self.slots, self.bt, self.row_bt,
+        self.model.forward(self.ws, self.ids, self.pos, self.slots, self.bt, None,
                            self.ctx, self.B, self.max_ctx)
 
     def advance(self):
@@ -92,7 +92,7 @@ class DecodeState:
 
     def body(self):
         m = self.model
-        keys = m.forward(self.ws, self.ids, self.pos, self.slots, self.bt, self.row_bt, self.ctx,
+        keys = m.forward(self.ws, self.ids, self.pos, self.slots, self.bt, None, self.ctx,
                          self.B, self.max_ctx, greedy=True)
         if m.tp > 1:
             m.comm.allreduce_max_u64_(keys[:self.B])

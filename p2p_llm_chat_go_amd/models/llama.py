@@ -56,6 +56,7 @@ class Workspace:
         self.moe = None  # lazily sized by models.moe
         # fused attention + o_proj hand-off counters (re-armed by the kernel) + fault flag
         self.sync = torch.zeros(2, device=dev, dtype=torch.int32)
+        self.row_ids = torch.arange(max_rows, device=dev, dtype=torch.int32)  # identity row_bt
         self.err = torch.zeros(1, device=dev, dtype=torch.int32)
 
 
@@ -141,6 +142,7 @@ class LlamaModel:
         argmax keys (ws.keys, see ops.lm_head_argmax).
         tiles: int32 [n, 4] prefill query tiles (ops.prefill_tiles) -> causal
         attention runs on the MFMA flash-prefill kernel instead of per row.
+        row_bt: block-table row of each query row; None = row r uses row r (decode).
         """
         cfg = self.cfg
         h = ws.h[:R]
@@ -154,14 +156,16 @@ class LlamaModel:
             ops.qkv_rope_gemm(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc,
                               vc, eps=cfg.eps)
             if fused:
-                ops.attn_oproj(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R], self.nq,
+                rb = row_bt[:R] if row_bt is not None else ws.row_ids[:R]
+                ops.attn_oproj(q, kc, vc, block_tables, rb, ctx_lens[:R], self.nq,
                                self.nkv, max_ctx, lw.o, h, attn, ws.sync, ws.err)
             else:
                 if tiles is not None:
                     ops.flash_prefill(q, kc, vc, block_tables, tiles, self.nq, self.nkv, out=attn,
                                       tiles_host=tiles_host)
                 else:
-                    ops.paged_attention(q, kc, vc, block_tables, row_bt[:R], ctx_lens[:R],
+                    ops.paged_attention(q, kc, vc, block_tables,
+                                        row_bt[:R] if row_bt is not None else None, ctx_lens[:R],
                                         self.nq, self.nkv, max_ctx, out=attn,
                                         workspace=ws.attn_ws)
                 self._row_parallel(lw.o, attn, h, ws, R)

@@ -42,7 +42,7 @@ def paged_attention_ref(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_h
     res = torch.empty(R, n_heads, HEAD_DIM, dtype=torch.float32, device=q.device)
     for r in range(R):
         ctx = int(ctx_lens[r])
-        bt_row = block_tables[int(row_bt[r])]
+        bt_row = block_tables[int(row_bt[r]) if row_bt is not None else r]
         for h in range(n_kv):
             K = _gather_kv(k_cache, bt_row, ctx, h)
             V = _gather_kv(v_cache, bt_row, ctx, h)
@@ -58,7 +58,8 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                     block_tables: torch.Tensor, row_bt: torch.Tensor, ctx_lens: torch.Tensor,
                     n_heads: int, n_kv: int, max_ctx: int, out: torch.Tensor | None = None,
                     workspace: tuple | None = None, scale: float | None = None) -> torch.Tensor:
-    """q: [R, n_heads*128] bf16 -> out [R, n_heads*128] bf16."""
+    """q: [R, n_heads*128] bf16 -> out [R, n_heads*128] bf16.  row_bt None: row r reads
+    block-table row r (decode batches)."""
     R = q.shape[0]
     if scale is None:
         scale = 1.0 / math.sqrt(HEAD_DIM)
@@ -73,7 +74,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     L = _lib.lib()
     _lib.check(L.p2p_paged_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(),
                                      v_cache.data_ptr(), block_tables.data_ptr(),
-                                     block_tables.stride(0), row_bt.data_ptr(), ctx_lens.data_ptr(),
+                                     block_tables.stride(0), _lib.ptr(row_bt), ctx_lens.data_ptr(),
                                      R, n_heads, n_kv, HEAD_DIM, float(scale), int(max_ctx),
                                      out.data_ptr(), out.stride(0), _lib.ptr(po), _lib.ptr(pml),
                                      _lib.stream_ptr(q.device)), "paged_attention")
