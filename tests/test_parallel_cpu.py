@@ -50,12 +50,32 @@ def _worker(rank, world, port, q, moe, a2a=False):
                      tp_rank=w.tp_rank, tp_size=w.tp_size,
                      ep_mode="a2a" if a2a else "allreduce")
         got = [r.tokens for r in eng.generate(prompts, 6, stop_on_eos=False)]
+        if not moe and got == ref:
+            # Ollama sampler under TP: every rank gathers the vocab shards and draws the
+            # same token (keyed by seed, position, token) as the unsharded engine
+            ref, got = _sampled(full, prompts), _sampled(eng, prompts)
         q.put((rank, got == ref, got, ref))
     except Exception as e:  # report instead of hanging the parent
         import traceback
         q.put((rank, False, traceback.format_exc(), None))
     finally:
         dist.destroy_process_group()
+
+
+def _sampled(eng, prompts, n=5):
+    from p2p_llm_chat_go_amd.engine.sampling import SamplingParams
+
+    params = [SamplingParams(temperature=1.2, top_k=20, top_p=0.95, seed=11 + b)
+              for b in range(len(prompts))]
+    pages = [eng.kv.allocator.alloc(2) for _ in prompts]
+    first = eng.prefill(prompts, pages, sampling=params).tolist()
+    g = eng.decode_graph(len(prompts), 128, greedy=False)
+    g.state.load(first, [len(p) for p in prompts], pages)
+    g.step_sampled(params, n)
+    out = [[first[b]] + g.state.hist[b, :n].tolist() for b in range(len(prompts))]
+    for p in pages:
+        eng.kv.allocator.free(p)
+    return out
 
 
 def _run(world, moe=False, a2a=False):
