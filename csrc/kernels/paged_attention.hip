@@ -49,10 +49,17 @@ __global__ __launch_bounds__(WAVES * 64) void paged_attn_kernel(
 
   constexpr int VS = HD + 8;
   __shared__ bf16x2 qs[G][HD / 2];
-  __shared__ __attribute__((aligned(16))) bf16 vs[WAVES][KPW][VS];
+  // V staging (P.V) and the wave partials of O (merge) share one region: the V rows are
+  // dead once every wave has finished its P.V (barrier below), and the union keeps the
+  // block under 80 KiB, i.e. two blocks per CU on long contexts (one block's loads in
+  // flight while the other one computes).
+  constexpr int kVsBytes = WAVES * KPW * VS * 2;
+  constexpr int kSoBytes = WAVES * G * HD * 4;
+  __shared__ __attribute__((aligned(16))) char vs_so[kVsBytes > kSoBytes ? kVsBytes : kSoBytes];
+  auto& vs = *reinterpret_cast<bf16(*)[WAVES][KPW][VS]>(vs_so);
+  auto& so = *reinterpret_cast<float(*)[WAVES][G][HD]>(vs_so);
   __shared__ float ps[WAVES][G][KPW];
   __shared__ float sm[WAVES][G], sl[WAVES][G];
-  __shared__ float so[WAVES][G][HD];
 
   const int key0 = c * CHUNK + w * KPW;  // first key of this wave
 
@@ -139,6 +146,7 @@ __global__ __launch_bounds__(WAVES * 64) void paged_attn_kernel(
       }
     }
   }
+  __syncthreads();  // every wave's P.V has read its V rows: the region becomes `so`
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     so[w][g][2 * lane] = o[g][0];
@@ -178,25 +186,62 @@ __global__ __launch_bounds__(WAVES * 64) void paged_attn_kernel(
   }
 }
 
-__global__ __launch_bounds__(HD) void attn_combine_kernel(const float* __restrict__ part_o,
-                                                          const float* __restrict__ part_ml,
-                                                          const int* __restrict__ ctx_lens,
-                                                          int Hq, int n_chunks,
-                                                          bf16* __restrict__ out, int ldo) {
-  const int r = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
-  const int nc = min((ctx_lens[r] + CHUNK - 1) / CHUNK, n_chunks);
+// Split-K combine: one block per (row, q head).  The chunk statistics go to LDS first
+// (one load per chunk, all in flight together), then CG groups of HD threads each sum
+// the partial outputs of every CG-th chunk with 8 loads in flight per thread, and the
+// groups meet in LDS.  (A serial per-dimension loop over the chunks leaves one load
+// in flight per thread: ~85 us per layer at a 32K context.)
+constexpr int CG = 8;                  // chunk groups per block
+constexpr int MAX_CHUNKS = 131072 / CHUNK;  // 128K-token contexts
+__global__ __launch_bounds__(HD * CG) void attn_combine_kernel(const float* __restrict__ part_o,
+                                                               const float* __restrict__ part_ml,
+                                                               const int* __restrict__ ctx_lens,
+                                                               int Hq, int n_chunks,
+                                                               bf16* __restrict__ out, int ldo) {
+  __shared__ float s_e[MAX_CHUNKS];  // exp(m_c - M)
+  __shared__ float s_l[MAX_CHUNKS];
+  __shared__ float s_red[CG][HD];
+  __shared__ float s_wmax[HD * CG / 64];
+  const int r = blockIdx.x, hq = blockIdx.y, tid = threadIdx.x;
+  const int d = tid % HD, grp = tid / HD;
+  const int nc = min(min((ctx_lens[r] + CHUNK - 1) / CHUNK, n_chunks), MAX_CHUNKS);
   const size_t base = ((size_t)r * Hq + hq) * n_chunks;
-  float M = -INFINITY;
-  for (int c = 0; c < nc; ++c) M = fmaxf(M, part_ml[(base + c) * 2]);
-  float num = 0.f, den = 0.f;
-  for (int c = 0; c < nc; ++c) {
+  float mloc = -INFINITY;
+  for (int c = tid; c < nc; c += HD * CG) {
     const float m = part_ml[(base + c) * 2];
-    if (m == -INFINITY) continue;
-    const float e = __expf(m - M);
-    num = fmaf(e, part_o[(base + c) * HD + d], num);
-    den = fmaf(e, part_ml[(base + c) * 2 + 1], den);
+    s_e[c] = m;
+    s_l[c] = part_ml[(base + c) * 2 + 1];
+    mloc = fmaxf(mloc, m);
   }
-  out[(size_t)r * ldo + (size_t)hq * HD + d] = f2bf(den > 0.f ? num / den : 0.f);
+  mloc = wave_max(mloc);
+  if ((tid & 63) == 0) s_wmax[tid >> 6] = mloc;
+  __syncthreads();
+  float M = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < HD * CG / 64; ++i) M = fmaxf(M, s_wmax[i]);
+  __syncthreads();
+  for (int c = tid; c < nc; c += HD * CG) s_e[c] = s_e[c] == -INFINITY ? 0.f : __expf(s_e[c] - M);
+  __syncthreads();
+  float num = 0.f;
+  const float* po = part_o + base * HD + d;
+  int c = grp;
+  for (; c + 7 * CG < nc; c += 8 * CG) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = po[(size_t)(c + u * CG) * HD];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) num = fmaf(s_e[c + u * CG], v[u], num);
+  }
+  for (; c < nc; c += CG) num = fmaf(s_e[c], po[(size_t)c * HD], num);
+  s_red[grp][d] = num;
+  __syncthreads();
+  if (grp == 0) {
+    float tot = 0.f, den = 0.f;
+#pragma unroll
+    for (int g = 0; g < CG; ++g) tot += s_red[g][d];
+    for (int i = 0; i < nc; ++i) den = fmaf(s_e[i], s_l[i], den);
+    out[(size_t)r * ldo + (size_t)hq * HD + d] = f2bf(den > 0.f ? tot / den : 0.f);
+  }
 }
 
 template <int G>
@@ -208,7 +253,7 @@ int launch_attn(const void* q, int ldq, const void* kc, const void* vc, const in
                      ctx, Hkv, scale, n_chunks, (bf16*)out, ldo, part_o, part_ml);
   int e = (int)hipGetLastError();
   if (e || n_chunks == 1) return e;
-  hipLaunchKernelGGL(attn_combine_kernel, dim3(R, Hkv * G), dim3(HD), 0, st, part_o, part_ml, ctx,
+  hipLaunchKernelGGL(attn_combine_kernel, dim3(R, Hkv * G), dim3(HD * CG), 0, st, part_o, part_ml, ctx,
                      Hkv * G, n_chunks, (bf16*)out, ldo);
   return (int)hipGetLastError();
 }
@@ -228,6 +273,7 @@ P2P_API int p2p_paged_attention(const void* q, int ldq, const void* k_cache, con
   if (head_dim != HD || Hkv <= 0 || Hq % Hkv != 0 || R <= 0) return (int)hipErrorInvalidValue;
   const int n_chunks = (max_ctx + CHUNK - 1) / CHUNK;
   if (n_chunks > 1 && (!part_o || !part_ml)) return (int)hipErrorInvalidValue;
+  if (n_chunks > MAX_CHUNKS) return (int)hipErrorInvalidValue;
   switch (Hq / Hkv) {
     case 1: return launch_attn<1>(q, ldq, k_cache, v_cache, block_tables, bt_stride, row_bt, ctx_lens, R, Hkv, scale, n_chunks, out, ldo, part_o, part_ml, stream);
     case 2: return launch_attn<2>(q, ldq, k_cache, v_cache, block_tables, bt_stride, row_bt, ctx_lens, R, Hkv, scale, n_chunks, out, ldo, part_o, part_ml, stream);
