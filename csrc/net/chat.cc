@@ -707,11 +707,12 @@ void Node::install_routes() {
         return;
       }
     }
-    char prompt[8192];
-    snprintf(prompt, sizeof(prompt), kSuggestTemplate, text.c_str());
+    std::string prompt = kSuggestTemplate;  // "...message:\n\n%s\n\nReply:" (no length cap)
+    const size_t ph = prompt.find("%s");
+    if (ph != std::string::npos) prompt.replace(ph, 2, text);
     Json g = Json::object();
     g.set("model", j.get_string("model", cfg_.llm_model));
-    g.set("prompt", std::string(prompt));
+    g.set("prompt", prompt);
     g.set("stream", false);
     if (j.has("options")) g.set("options", j.get("options"));
     Json out;

@@ -13,6 +13,7 @@ STRICT_SENDER, UI_FILE) and the engine knobs:
   ENGINE_CHECKPOINT  HF checkpoint dir (safetensors + config.json); default random-init
   ENGINE_MAX_BATCH   concurrent sequences (default 16)
   ENGINE_MAX_TOKENS  default num_predict (default 128)
+  ENGINE_WARMUP   1 (default on GPUs): autotune GEMMs + capture decode graphs at start
   TOKENIZER_PATH  tokenizer.json (default: synthetic offline tokenizer)
 
 The libp2p host, HTTP API and Directory client are the C++ ``Node``; this
@@ -50,6 +51,10 @@ def build_engine_server(model: str | None = None, device: str | None = None):
         weights = None
     kv_pages = None if str(dev).startswith("cuda") else 256
     eng = Engine(cfg, weights=weights, device=dev, kv_pages=kv_pages, max_batch=max_batch)
+    if str(dev).startswith("cuda") and os.environ.get("ENGINE_WARMUP", "1") != "0":
+        # autotuned GEMM launch codes + decode graphs of the common batch buckets, before
+        # the first request (ENGINE_WARMUP=0 skips: faster start, untuned first replies)
+        eng.warmup(tuple(b for b in (1, 2, 4, 8, 16) if b <= max_batch), ctx=256)
     tok = get_tokenizer(cfg, os.environ.get("TOKENIZER_PATH") or (ckpt or None))
     return EngineServer(eng, tok, model_name=os.environ.get("LLM_MODEL", "llama3.1"),
                         default_max_tokens=int(os.environ.get("ENGINE_MAX_TOKENS", "128")))
