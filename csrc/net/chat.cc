@@ -234,6 +234,9 @@ NodeConfig NodeConfig::from_env() {
   c.nat_pmp = env_or("NAT_PMP", c.nat_pmp);
   c.security = env_or("SECURITY", c.security);
   c.upnp = env_or("UPNP", c.upnp);
+  c.conn_low = atoi(env_or("CONN_LOW", std::to_string(c.conn_low)).c_str());
+  c.conn_high = atoi(env_or("CONN_HIGH", std::to_string(c.conn_high)).c_str());
+  c.conn_grace_ms = (int)(atof(env_or("CONN_GRACE", "60").c_str()) * 1000);
   std::string la = env_or("LISTEN_ADDRS", "");
   if (la == "none") {
     c.listen.clear();  // relay-only node
@@ -333,6 +336,7 @@ void Node::start() {
   PrivateKey key = load_or_make_identity(cfg_);
   host_ = std::make_shared<Host>(key);
   host_->set_security(split_csv(cfg_.security));
+  host_->set_conn_limits(cfg_.conn_low, cfg_.conn_high, cfg_.conn_grace_ms);
   if (cfg_.dht_mode != "off") {
     // created before any listener/dial so identify results feed the routing table
     kad_ = std::make_unique<Kad>(host_, cfg_.dht_mode == "client" ? KadMode::Client : KadMode::Server);
@@ -556,6 +560,7 @@ Json Node::metrics_json() {
   j.set("suggest_requests_total", (long)n_suggest_);
   j.set("inbox_size", (long)inbox_.size());
   j.set("connected_peers", (long)(host_ ? host_->peers().size() : 0));
+  j.set("connections_trimmed_total", (long)(host_ ? host_->trimmed() : 0));
   return j;
 }
 

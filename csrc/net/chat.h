@@ -109,6 +109,8 @@ struct NodeConfig {
   // Secure channels, outbound preference order ("noise", "tls" = /tls/1.0.0); inbound
   // accepts every listed one.  go-libp2p's default host offers both (TLS first).
   std::string security = "noise,tls";
+  // connection manager watermarks (go-libp2p default connmgr: 160 / 192, 1 min grace)
+  int conn_low = 160, conn_high = 192, conn_grace_ms = 60000;
   static NodeConfig from_env();
 };
 

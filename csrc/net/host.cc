@@ -218,6 +218,50 @@ SessionPtr Host::upgrade_inbound(ConnPtr raw, bool relayed) {
   return sess;
 }
 
+void Host::set_conn_limits(int low, int high, int grace_ms) {
+  std::lock_guard<std::mutex> lk(mu_);
+  conn_high_ = std::max(1, high);
+  conn_low_ = std::max(0, std::min(low, conn_high_));
+  conn_grace_ms_ = std::max(0, grace_ms);
+}
+
+void Host::touch(const PeerId& p) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = conn_use_.find(p);
+  if (it != conn_use_.end()) it->second.used = std::chrono::steady_clock::now();
+}
+
+void Host::trim_connections(const PeerId& keep) {
+  std::vector<SessionPtr> victims;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    std::vector<std::pair<std::chrono::steady_clock::time_point, PeerId>> cands;
+    int live = 0;
+    const auto now = std::chrono::steady_clock::now();
+    for (auto& kv : sessions_) {
+      if (kv.second->closed()) continue;
+      ++live;
+      auto u = conn_use_.find(kv.first);
+      if (kv.first == keep || u == conn_use_.end() || kv.second->num_streams() > 0) continue;
+      if (now - u->second.opened < std::chrono::milliseconds(conn_grace_ms_)) continue;
+      cands.push_back({u->second.used, kv.first});
+    }
+    if (live <= conn_high_) return;
+    std::sort(cands.begin(), cands.end());
+    for (auto& c : cands) {
+      if (live <= conn_low_) break;
+      victims.push_back(sessions_[c.second]);
+      sessions_.erase(c.second);
+      conn_use_.erase(c.second);
+      --live;
+    }
+  }
+  for (auto& v : victims) {
+    v->close();
+    trimmed_++;
+  }
+}
+
 void Host::add_session(const PeerId& p, SessionPtr s, bool relayed) {
   SessionPtr old;
   {
@@ -226,6 +270,8 @@ void Host::add_session(const PeerId& p, SessionPtr s, bool relayed) {
     // Prefer a direct connection over a relayed one; otherwise keep the newest.
     if (it != sessions_.end() && !it->second->closed()) old = it->second;
     sessions_[p] = s;
+    const auto now = std::chrono::steady_clock::now();
+    conn_use_[p] = ConnUse{now, now};
   }
   std::weak_ptr<YamuxSession> ws = s;
   busy_++;  // released by the session's on_close
@@ -239,9 +285,13 @@ void Host::add_session(const PeerId& p, SessionPtr s, bool relayed) {
              std::lock_guard<std::mutex> lk(mu_);
              auto it = sessions_.find(p);
              auto sp = ws.lock();
-             if (it != sessions_.end() && (!sp || it->second == sp)) sessions_.erase(it);
+             if (it != sessions_.end() && (!sp || it->second == sp)) {
+               sessions_.erase(it);
+               conn_use_.erase(p);
+             }
            });
   (void)old;  // the old session stays usable for its open streams and dies on its own
+  trim_connections(p);
   busy_++;
   std::thread([this, p, s] {
     run_identify(p, s);
@@ -266,6 +316,7 @@ void Host::accept_loop(std::shared_ptr<TcpListener> l) {
 }
 
 void Host::handle_stream(StreamPtr s, PeerId peer, bool relayed) {
+  touch(peer);
   auto io = std::make_shared<BufConn>(s);
   std::set<std::string> protos;
   {
@@ -365,7 +416,11 @@ SessionPtr Host::connect(const PeerId& p, const std::vector<Multiaddr>& addrs, i
   {
     std::lock_guard<std::mutex> lk(mu_);
     auto it = sessions_.find(p);
-    if (it != sessions_.end() && !it->second->closed()) return it->second;
+    if (it != sessions_.end() && !it->second->closed()) {
+      auto u = conn_use_.find(p);
+      if (u != conn_use_.end()) u->second.used = std::chrono::steady_clock::now();
+      return it->second;
+    }
   }
   add_addrs(p, addrs);
   std::vector<Multiaddr> cands = peer_addrs(p);

@@ -91,6 +91,13 @@ class Host {
   void set_security(const std::vector<std::string>& order);
   std::vector<std::string> security() const { return security_; }
 
+  // Connection manager (go-libp2p's default host runs connmgr with low 160 / high 192
+  // / 1 min grace): once more than `high` sessions are live, the least recently used
+  // ones that are past the grace period and carry no open stream are closed until
+  // `low` remain.  A trimmed peer is simply re-dialed on its next message.
+  void set_conn_limits(int low, int high, int grace_ms);
+  long trimmed() const { return trimmed_; }
+
   void close();
   bool closed() const { return closed_; }
 
@@ -99,6 +106,8 @@ class Host {
   void handle_stream(StreamPtr s, PeerId peer, bool relayed);
   void add_session(const PeerId& p, SessionPtr s, bool relayed);
   void run_identify(const PeerId& p, SessionPtr s);
+  void touch(const PeerId& p);
+  void trim_connections(const PeerId& keep);
   void identify_handler(StreamCtx& ctx);
 
   PrivateKey key_;
@@ -109,6 +118,12 @@ class Host {
   std::map<std::string, StreamHandler> handlers_;
   std::map<PeerId, std::vector<Multiaddr>> peerstore_;
   std::map<PeerId, SessionPtr> sessions_;
+  struct ConnUse {
+    std::chrono::steady_clock::time_point opened, used;
+  };
+  std::map<PeerId, ConnUse> conn_use_;
+  int conn_low_ = 160, conn_high_ = 192, conn_grace_ms_ = 60000;
+  std::atomic<long> trimmed_{0};
   std::map<PeerId, std::vector<std::string>> peer_protos_;
   std::map<PeerId, std::string> peer_agents_;
   std::vector<std::shared_ptr<TcpListener>> listeners_;

@@ -491,3 +491,35 @@ def test_node_daemon_hosts_engine_in_process(procs, dev):
         "".join(x.get("response", "") for x in lines))]
     st, body, _ = http("POST", a + "/suggest", {"message": "Hey! How's it going?"})
     assert st == 200 and "suggestion" in json.loads(body)
+
+
+def test_connection_manager_trims_to_low_watermark(procs):
+    """CONN_LOW / CONN_HIGH / CONN_GRACE (go-libp2p's connmgr, default 160/192/1 min):
+    beyond `high` live connections the least recently used idle ones are closed down
+    to `low`; a trimmed peer is re-dialed transparently on its next message."""
+    d = start_directory(procs)
+    a = start_node(procs, "A", d, {"CONN_LOW": "1", "CONN_HIGH": "2", "CONN_GRACE": "0"})
+    me_a = json.loads(http("GET", a + "/me")[1])
+    others = [start_node(procs, n, d, {"BOOTSTRAP_ADDRS": me_a["addrs"][0]}) for n in "BCDE"]
+    def trimmed():  # Prometheus text exposition
+        for line in http("GET", a + "/metrics")[1].splitlines():
+            if line.startswith("p2p_connections_trimmed_total "):
+                return int(line.split()[1])
+        return -1
+
+    for _ in range(100):
+        if trimmed() >= 2:
+            break
+        time.sleep(0.05)
+    assert trimmed() >= 2
+    assert len(json.loads(http("GET", a + "/peers")[1])) <= 2
+    # every peer still reaches A and A reaches every peer (re-dial after trimming)
+    for n, u in zip("BCDE", others):
+        assert http("POST", u + "/send", {"to_username": "A", "content": "hi " + n})[0] == 200
+        assert http("POST", a + "/send", {"to_username": n, "content": "yo " + n})[0] == 200
+    for _ in range(100):
+        if len(json.loads(http("GET", a + "/inbox")[1])) == 4:
+            break
+        time.sleep(0.05)
+    assert sorted(x["content"] for x in json.loads(http("GET", a + "/inbox")[1])) == \
+        ["hi B", "hi C", "hi D", "hi E"]
