@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree (ranks per engine replica, RCCL over xGMI)")
+    ap.add_argument("--weights", choices=("bf16", "fp8"), default="bf16",
+                    help="weight storage of the dense projections (fp8: weight-only e4m3, "
+                         "bf16 compute; opt-in -- the headline number is bf16)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -77,7 +80,7 @@ def main():
     need_pages = sum((len(p) + a.new_tokens + 63) // 64 for p in prompts) + 8
     eng = Engine(cfg, device=dev, seed=1234 + replica, kv_pages=max(need_pages, 64),
                  max_prefill_tokens=1024, max_batch=max(a.peers, 1), use_graph=not a.no_graph,
-                 comm=comm, tp_rank=tp_rank, tp_size=tp)
+                 comm=comm, tp_rank=tp_rank, tp_size=tp, weight_dtype=a.weights)
     eng.warmup((a.peers,), ctx=max(len(p) for p in prompts) + a.new_tokens)
 
     for _ in range(a.warmup):
@@ -133,7 +136,8 @@ def main():
                        "new_tokens": a.new_tokens,
                        "parallelism": ("dp%d" % (world // tp)) + ("-tp%d" % tp if tp > 1 else ""),
                        "tp": tp,
-                       "peers_per_gpu": a.peers, "hipgraph_decode": not a.no_graph},
+                       "peers_per_gpu": a.peers, "hipgraph_decode": not a.no_graph,
+                       "weights": a.weights},
             "ttft_p50_ms": round(statistics.median(all_ttft), 3),
             "ttft_p99_ms": round(sorted(all_ttft)[min(len(all_ttft) - 1,
                                                       int(0.99 * len(all_ttft)))], 3),

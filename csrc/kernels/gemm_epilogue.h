@@ -35,6 +35,7 @@ struct EpiArgs {
   const float* row_w;
   long long w_stride;
   int n_experts;
+  const float* wscale;  // FP8 weights: per-output-channel scale [N] (null = bf16 weights)
   int u;   // requested pipeline depth (0 = default)
   int ng;  // requested column groups per block (skinny GEMM, M > 16; 0/1 = one)
 };

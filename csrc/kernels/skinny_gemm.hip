@@ -34,9 +34,33 @@
 // Split-K across the waves of a block (WAVES), reduced through LDS.
 #include "gemm_epilogue.h"
 
+#include <type_traits>
+
 namespace {
 
-template <int MT, int WAVES, int EPI, bool NORM, int U, bool MOE = false, int NG = 1>
+// F8: weight-only FP8 (OCP e4m3) -- the weight stream is 8 bytes per lane per k-step (half
+// of bf16), widened to bf16 in registers right before the MFMA; the per-output-channel
+// scale (ea.wscale) is applied to the accumulator in the epilogue.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+template <bool F8>
+using wraw_t = typename std::conditional<F8, u32x2, bf16x8>::type;
+
+__device__ __forceinline__ bf16x8 widen(const bf16x8& w) { return w; }
+// 8 e4m3 codes -> 8 bf16: four gfx950 v_cvt_scalef32_pk_bf16_fp8 (unit scale)
+__device__ __forceinline__ bf16x8 widen(const u32x2& w) {
+  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, false);
+  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, true);
+  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, false);
+  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, true);
+  bf16x8 r;
+  r[0] = a.x; r[1] = a.y; r[2] = b.x; r[3] = b.y;
+  r[4] = c.x; r[5] = c.y; r[6] = d.x; r[7] = d.y;
+  return r;
+}
+
+template <int MT, int WAVES, int EPI, bool NORM, int U, bool MOE = false, int NG = 1, bool F8 = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     const bf16x8* __restrict__ Wt, const bf16* __restrict__ X, int ldx, int M, int K,
     int up_group_offset, void* __restrict__ out, int ldo, float eps, EpiArgs ea) {
@@ -60,11 +84,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     mrows = ea.moe_rows + (size_t)e * ea.rows_stride;
   }
 
-  const bf16x8* wp[NW];
+  using WR = wraw_t<F8>;
+  const WR* wq = reinterpret_cast<const WR*>(Wt);
+  const WR* wp[NW];
 #pragma unroll
   for (int c = 0; c < NG; ++c) {
-    wp[c * NB] = Wt + (size_t)(g0 + c) * S * 64 + lane;
-    if constexpr (NB == 2) wp[c * NB + 1] = Wt + (size_t)(g0 + c + up_group_offset) * S * 64 + lane;
+    wp[c * NB] = wq + (size_t)(g0 + c) * S * 64 + lane;
+    if constexpr (NB == 2) wp[c * NB + 1] = wq + (size_t)(g0 + c + up_group_offset) * S * 64 + lane;
   }
 
   const bf16* xp[MT];
@@ -111,18 +137,21 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
 
-  auto load = [&](int s, bf16x8(&bw)[U][NW], bf16x8(&ax)[U][MT]) {
+  auto load = [&](int s, WR(&bw)[U][NW], bf16x8(&ax)[U][MT]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int b = 0; b < NW; ++b) bw[u][b] = load_nt(wp[b] + (size_t)(s + u) * 64);
+      for (int b = 0; b < NW; ++b) bw[u][b] = __builtin_nontemporal_load(wp[b] + (size_t)(s + u) * 64);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
         ax[u][mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + (s + u) * 32)
                            : zero_bf16x8();
     }
   };
-  auto compute1 = [&](const bf16x8(&bw)[NW], const bf16x8(&ax)[MT]) {
+  auto compute1 = [&](const WR(&bwr)[NW], const bf16x8(&ax)[MT]) {
+    bf16x8 bw[NW];
+#pragma unroll
+    for (int b = 0; b < NW; ++b) bw[b] = widen(bwr[b]);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -137,7 +166,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
       }
     }
   };
-  auto compute = [&](bf16x8(&bw)[U][NW], bf16x8(&ax)[U][MT]) {
+  auto compute = [&](WR(&bw)[U][NW], bf16x8(&ax)[U][MT]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) compute1(bw[u], ax[u]);
   };
@@ -145,7 +174,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   const int n = s1 - s0;
   const int nb = n / U;
   if (nb > 0) {
-    bf16x8 bA[U][NW], aA[U][MT], bB[U][NW], aB[U][MT];
+    WR bA[U][NW], bB[U][NW];
+    bf16x8 aA[U][MT], aB[U][MT];
     load(s0, bA, aA);
     int b = 0;
     for (; b + 2 < nb; b += 2) {
@@ -163,9 +193,10 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     }
   }
   for (int s = s0 + nb * U; s < s1; ++s) {
-    bf16x8 b1[NW], a1[MT];
+    WR b1[NW];
+    bf16x8 a1[MT];
 #pragma unroll
-    for (int b = 0; b < NW; ++b) b1[b] = load_nt(wp[b] + (size_t)s * 64);
+    for (int b = 0; b < NW; ++b) b1[b] = __builtin_nontemporal_load(wp[b] + (size_t)s * 64);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
       a1[mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + s * 32) : zero_bf16x8();
@@ -249,6 +280,12 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           orow = m < M ? mrows[m] : 0;
           if (ea.row_w && m < M) scale *= ea.row_w[orow];
         }
+        float s0 = scale, s1 = scale;  // F8: per-output-channel weight scales
+        if constexpr (F8) {
+          s0 *= ea.wscale[(size_t)g * 16 + r];
+          if constexpr (NB == 2) s1 *= ea.wscale[(size_t)(g + up_group_offset) * 16 + r];
+          else s1 = s0;
+        }
         if constexpr (EPI == EPI_QKV_ROPE) {
           float2 cs;
           if constexpr (NG == 1) {
@@ -258,11 +295,11 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
             const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
             cs = m < M ? ea.cs[(size_t)rpos[mt][j] * 64 + dd] : float2{1.f, 0.f};
           }
-          epi_store<EPI>(orow, m < M, g, r, acc[c][mt][j] * scale, 0.f, out, ldo, ea, cs,
+          epi_store<EPI>(orow, m < M, g, r, acc[c][mt][j] * s0, 0.f, out, ldo, ea, cs,
                          rslot[mt][j]);
         } else {
-          epi_store<EPI>(orow, m < M, g, r, acc[c * NB][mt][j] * scale,
-                         acc[c * NB + NB - 1][mt][j] * scale, out, ldo, ea);
+          epi_store<EPI>(orow, m < M, g, r, acc[c * NB][mt][j] * s0,
+                         acc[c * NB + NB - 1][mt][j] * s1, out, ldo, ea);
         }
       }
     }
@@ -296,6 +333,13 @@ int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, 
 template <int MT, int WAVES, int EPI, bool NORM, int U>
 int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
                void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
+  if (ea.wscale) {  // FP8 weights (dense projections, one column group per block)
+    if (ea.moe_cnt) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, false, 1, true>), dim3(groups),
+                       dim3(WAVES * 64), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K,
+                       up_off, out, ldo, eps, ea);
+    return (int)hipGetLastError();
+  }
   if (ea.moe_cnt) {
     if constexpr (EPI == EPI_SILU || EPI == EPI_STORE) {
       hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, true>),
@@ -420,11 +464,15 @@ P2P_API void p2p_skinny_gemm_tune(int u_mt1, int resident) {
   if (resident >= 1 && resident <= 8) g_resident = resident;
 }
 
+// wscale (all three entry points): null = bf16 fragment-major weights; else FP8 e4m3
+// weights in the same fragment order (8 bytes per lane per k-step) and their
+// per-output-channel fp32 scales.
 P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
                             int norm, void* out, int ldo, float eps, int waves,
-                            hipStream_t stream) {
+                            const float* wscale, hipStream_t stream) {
   if (epi == EPI_QKV_ROPE) return (int)hipErrorInvalidValue;
   EpiArgs ea = {};
+  ea.wscale = wscale;
   return skinny_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, waves, ea, stream);
 }
 
@@ -433,9 +481,10 @@ P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K
 // the shards and reset them).
 P2P_API int p2p_skinny_gemm_argmax(const void* Wt, const void* X, int ldx, int M, int K, int N,
                                    unsigned long long* keys, int col_offset, float eps, int waves,
-                                   hipStream_t stream) {
+                                   const float* wscale, hipStream_t stream) {
   EpiArgs ea = {};
   ea.col_offset = col_offset;
+  ea.wscale = wscale;
   return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_ARGMAX, 1, keys, 0, eps, waves, ea, stream);
 }
 
@@ -443,8 +492,10 @@ P2P_API int p2p_skinny_gemm_argmax(const void* Wt, const void* X, int ldx, int M
 P2P_API int p2p_skinny_gemm_qkv_rope(const void* Wt, const void* X, int ldx, int M, int K,
                                      int Hq, int Hkv, const int* pos, const int* slots,
                                      const void* cos_sin, void* q_out, int ldq, void* k_cache,
-                                     void* v_cache, float eps, int waves, hipStream_t stream) {
+                                     void* v_cache, float eps, int waves, const float* wscale,
+                                     hipStream_t stream) {
   EpiArgs ea = {};
+  ea.wscale = wscale;
   ea.pos = pos;
   ea.slots = slots;
   ea.cs = (const float2*)cos_sin;

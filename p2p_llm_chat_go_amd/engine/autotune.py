@@ -95,7 +95,7 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
         for name, wts, epi, fn in jobs:
             N, K = G.tiled_shape(wts[0])
             times = {}
-            for code in _configs(K, M, G.tiled_ok(N, K, epi)):
+            for code in _configs(K, M, G.tiled_ok(N, K, epi) and not G._is_f8(wts[0])):
                 times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
             best = min(times, key=times.get)
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)

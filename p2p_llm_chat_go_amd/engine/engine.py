@@ -59,12 +59,18 @@ class Engine:
                  seed: int = 0, kv_pages: int | None = None, max_prefill_tokens: int = 1024,
                  max_batch: int = 64, use_graph: bool = True, comm=None, tp_rank: int = 0,
                  tp_size: int = 1, kv_fraction: float = 0.85, ep_rank: int = 0,
-                 ep_size: int = 1, ep_mode: str = "allreduce"):
+                 ep_size: int = 1, ep_mode: str = "allreduce", weight_dtype: str | None = None):
         self.cfg = cfg
         self.device = torch.device(device)
         if weights is None:
             weights = EngineWeights.random(cfg, self.device, seed=seed, tp_rank=tp_rank,
                                            tp_size=tp_size, ep_rank=ep_rank, ep_size=ep_size)
+        # weight_dtype "fp8": weight-only e4m3 dense projections (EngineWeights.quantize_fp8)
+        self.weight_dtype = weight_dtype or os.environ.get("ENGINE_WEIGHTS", "bf16")
+        if self.weight_dtype == "fp8":
+            weights.quantize_fp8()
+        elif self.weight_dtype != "bf16":
+            raise ValueError("weight_dtype must be bf16 or fp8, got %r" % self.weight_dtype)
         self.weights = weights
         if kv_pages is None:
             self.kv = KVCache.from_free_memory(cfg, self.device, fraction=kv_fraction,

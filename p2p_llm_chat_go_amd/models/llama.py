@@ -149,7 +149,7 @@ class LlamaModel:
         ops.gather_rows(self.w.embed, ids[:R], out=h)
         q, attn = ws.q[:R], ws.attn[:R]
         fused = (self.fuse_attn_oproj and tiles is None and self.tp == 1
-                 and self.device.type == "cuda"
+                 and self.device.type == "cuda" and isinstance(self.w.layers[0].o, torch.Tensor)
                  and ops.attn_oproj_ok(R, self.nq, self.nkv, max_ctx, cfg.hidden))
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)

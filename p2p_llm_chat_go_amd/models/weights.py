@@ -59,13 +59,30 @@ class EngineWeights:
         return self.embed.device
 
     def nbytes(self) -> int:
-        n = self.embed.numel() + self.lm_head.numel()
+        def nb(t):
+            if isinstance(t, ops.Fp8Weight):
+                return t.data.numel() + 4 * t.scale.numel()
+            return t.numel() * t.element_size()
+
+        n = nb(self.embed) + nb(self.lm_head)
         for lw in self.layers:
             for f in dataclasses.fields(lw):
                 t = getattr(lw, f.name)
                 if t is not None:
-                    n += t.numel()
-        return 2 * n
+                    n += nb(t)
+        return n
+
+    def quantize_fp8(self, names=("qkv", "o", "gate_up", "down")) -> "EngineWeights":
+        """Weight-only FP8 (e4m3, per-output-channel scale) for the dense projections, in
+        place: the decode weight stream -- the roofline of batch-1 decode -- halves.  The
+        embedding, LM head, router and MoE experts stay bf16.  Opt-in (ENGINE_WEIGHTS=fp8 /
+        bench.py --weights fp8); the headline numbers are bf16."""
+        for lw in self.layers:
+            for name in names:
+                t = getattr(lw, name)
+                if isinstance(t, torch.Tensor):
+                    setattr(lw, name, ops.quantize_fp8(t))
+        return self
 
     # ------------------------------------------------------------------ build
     @classmethod

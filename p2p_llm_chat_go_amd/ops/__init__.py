@@ -5,7 +5,8 @@ a missing library raises).  CPU tensors run the PyTorch reference of the same
 math -- that is the CPU tiny-llama plumbing config and the numerics oracle,
 never a fallback for GPU tensors.
 """
-from .gemm import (EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, argmax_finalize, fold_norm,
+from .gemm import (EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, Fp8Weight, argmax_finalize, fold_norm,
+                   quantize_fp8,
                    lm_head_argmax, new_argmax_keys, qkv_rope_gemm, rope_row_perm, skinny_gemm, tile_weight,
                    tiled_shape, untile_weight)
 from .attention import (PAGE, HEAD_DIM, attn_oproj, attn_oproj_ok, attn_workspace,

@@ -32,7 +32,7 @@ c_void_p = ctypes.c_void_p
 _SIGS = {
     # name: argtypes (all return int hipError_t)
     "p2p_skinny_gemm": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
-                        c_int, c_float, c_int, c_void_p],
+                        c_int, c_float, c_int, c_void_p, c_void_p],
     "p2p_paged_attention": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                             c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int,
                             c_void_p, c_void_p, c_void_p],
@@ -57,10 +57,10 @@ _SIGS = {
                     c_int, c_void_p, c_int, c_void_p],
     "p2p_argmax_finalize": [c_void_p, c_void_p, c_int, c_void_p],
     "p2p_skinny_gemm_argmax": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
-                               c_float, c_int, c_void_p],
+                               c_float, c_int, c_void_p, c_void_p],
     "p2p_skinny_gemm_qkv_rope": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float,
-                                 c_int, c_void_p],
+                                 c_int, c_void_p, c_void_p],
     "p2p_sample": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                    c_void_p, c_void_p],
     "p2p_tiled_gemm": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,

@@ -20,8 +20,65 @@ EPI_STORE, EPI_RESID, EPI_SILU, EPI_F32 = 0, 1, 2, 3
 EPI_QKV_ROPE, EPI_ARGMAX = 4, 5
 SKINNY_MAX_M = 64
 
-# Autotuned launch codes: (N, K, epi, norm, m_tile) -> waves | (U << 8)  (engine/autotune.py)
+# Autotuned launch codes: (N, K, epi, norm, m_tile[, "fp8"]) -> waves | (U << 8)
+# (engine/autotune.py)
 _TUNE: dict = {}
+
+FP8_MAX = 448.0  # OCP e4m3 (the gfx950 format; torch.float8_e4m3fn)
+
+
+class Fp8Weight:
+    """Weight-only FP8 projection: e4m3 codes in the fragment-major order of
+    ``tile_weight`` (uint8 ``[N/16, K/32, 64, 8]``: the decode stream is 8 bytes per lane
+    per k-step, half of bf16) and a per-output-channel fp32 scale ``[N]``.  The skinny
+    GEMM widens the codes to bf16 in registers and applies the scale in its epilogue."""
+
+    def __init__(self, data: torch.Tensor, scale: torch.Tensor):
+        self.data = data
+        self.scale = scale
+
+    @property
+    def shape(self):
+        return self.data.shape
+
+    @property
+    def device(self):
+        return self.data.device
+
+    def numel(self):
+        return self.data.numel()
+
+    def to(self, device):
+        return Fp8Weight(self.data.to(device), self.scale.to(device))
+
+    def element_size(self):
+        return 1
+
+    def dequantize_f32(self) -> torch.Tensor:
+        """Exact fp32 [N, K] (natural layout) values the kernel multiplies with."""
+        q = untile_weight(self.data.view(torch.float8_e4m3fn)).float()
+        return q * self.scale.float()[:, None].to(q.device)
+
+    def dequantize(self) -> torch.Tensor:
+        """bf16 fragment-major weight with (bf16-rounded) same values (CPU reference)."""
+        return tile_weight(self.dequantize_f32().to(torch.bfloat16))
+
+
+def quantize_fp8(wt: torch.Tensor) -> Fp8Weight:
+    """bf16 fragment-major weight -> Fp8Weight (per-output-channel absmax scaling)."""
+    w = untile_weight(wt).float()
+    amax = w.abs().amax(dim=1).clamp_min(1e-12)
+    scale = amax / FP8_MAX
+    q = (w / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return Fp8Weight(tile_weight(q.view(torch.uint8)), scale.float().contiguous())
+
+
+def _is_f8(wt) -> bool:
+    return isinstance(wt, Fp8Weight)
+
+
+def _wptr(wt):
+    return (wt.data.data_ptr(), wt.scale.data_ptr()) if _is_f8(wt) else (wt.data_ptr(), None)
 
 
 def m_tile(M: int) -> int:
@@ -30,7 +87,8 @@ def m_tile(M: int) -> int:
 
 def tune_key(wt, M, epi, norm):
     N, K = tiled_shape(wt)
-    return (N, K, int(epi), bool(norm), m_tile(min(M, SKINNY_MAX_M)))
+    key = (N, K, int(epi), bool(norm), m_tile(min(M, SKINNY_MAX_M)))
+    return key + ("fp8",) if _is_f8(wt) else key
 
 
 def set_tune(key, code: int):
@@ -62,6 +120,8 @@ TILED_FLAG = 1 << 24
 
 
 def _want_tiled(wt, M, N, K, epi, norm, waves) -> bool:
+    if _is_f8(wt):  # FP8 weights run on the skinny kernel only (M chunks of 64)
+        return False
     if use_tiled(M, N, K, epi):
         return True
     if M > SKINNY_MAX_M or not tiled_ok(N, K, epi):
@@ -107,7 +167,7 @@ def fold_norm(w: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
 
 def _ref(wt, x, epi, norm, out, eps):
     N, K = tiled_shape(wt)
-    W = untile_weight(wt).float()
+    W = wt.dequantize_f32() if _is_f8(wt) else untile_weight(wt).float()
     xf = x.float()
     acc = xf @ W.t()
     if norm:
@@ -154,9 +214,10 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
         mc = min(SKINNY_MAX_M, M - m0)
         xs = x[m0:m0 + mc]
         os_ = out[m0:m0 + mc]
-        _lib.check(L.p2p_skinny_gemm(wt.data_ptr(), xs.data_ptr(), x.stride(0), mc, K, N, epi,
+        wp, sp = _wptr(wt)
+        _lib.check(L.p2p_skinny_gemm(wp, xs.data_ptr(), x.stride(0), mc, K, N, epi,
                                      int(norm), os_.data_ptr(), out.stride(0), float(eps),
-                                     _code(wt, mc, epi, norm, waves), s), "skinny_gemm")
+                                     _code(wt, mc, epi, norm, waves), sp, s), "skinny_gemm")
     return out
 
 
@@ -200,11 +261,12 @@ def qkv_rope_gemm(wt, x, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_c
         return q_out
     for m0 in range(0, M, SKINNY_MAX_M):
         mc = min(SKINNY_MAX_M, M - m0)
+        wp, sp = _wptr(wt)
         _lib.check(L.p2p_skinny_gemm_qkv_rope(
-            wt.data_ptr(), x[m0:].data_ptr(), x.stride(0), mc, K, n_heads, n_kv,
+            wp, x[m0:].data_ptr(), x.stride(0), mc, K, n_heads, n_kv,
             pos[m0:].data_ptr(), slots[m0:].data_ptr(), cos_sin.data_ptr(), q_out[m0:].data_ptr(),
             q_out.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), float(eps),
-            _code(wt, mc, EPI_QKV_ROPE, True, waves), s), "skinny_gemm_qkv_rope")
+            _code(wt, mc, EPI_QKV_ROPE, True, waves), sp, s), "skinny_gemm_qkv_rope")
     return q_out
 
 
@@ -241,9 +303,10 @@ def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: i
                                            keys.data_ptr(), int(col_offset), float(eps),
                                            _lib.stream_ptr(x.device)), "tiled_gemm_argmax")
         return keys
-    _lib.check(L.p2p_skinny_gemm_argmax(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N,
+    wp, sp = _wptr(wt)
+    _lib.check(L.p2p_skinny_gemm_argmax(wp, x.data_ptr(), x.stride(0), M, K, N,
                                         keys.data_ptr(), int(col_offset), float(eps),
-                                        _code(wt, M, EPI_ARGMAX, True, waves),
+                                        _code(wt, M, EPI_ARGMAX, True, waves), sp,
                                         _lib.stream_ptr(x.device)), "skinny_gemm_argmax")
     return keys
 

@@ -154,3 +154,36 @@ def test_sampled_decode_graph_gpu():
     a = run(False, hot)
     assert a == run(False, hot) == run(False, hot, use_graph=False)
     assert a != ref
+
+
+def test_fp8_quantize_roundtrip_cpu():
+    from p2p_llm_chat_go_amd import ops
+
+    torch.manual_seed(0)
+    W = (torch.randn(256, 512) * 0.03).to(torch.bfloat16)
+    q = ops.quantize_fp8(ops.tile_weight(W))
+    assert q.data.dtype == torch.uint8 and q.data.shape == (16, 16, 64, 8)
+    assert q.scale.shape == (256,)
+    Wd = ops.untile_weight(q.dequantize()).float()
+    # e4m3: 3 mantissa bits -> relative error <= 2^-4 per element (normal range)
+    err = (Wd - W.float()).abs() / W.float().abs().amax(1, keepdim=True)
+    assert err.max() < 0.07
+    assert ((Wd - W.float()).norm() / W.float().norm()) < 0.04
+
+
+def test_fp8_engine_cpu_matches_dequantized_weights():
+    w8 = EngineWeights.random(TINY_LLAMA, "cpu", seed=5)
+    e8 = Engine(TINY_LLAMA, weights=w8, device="cpu", kv_pages=64, max_batch=4,
+                weight_dtype="fp8")
+    wd = EngineWeights.random(TINY_LLAMA, "cpu", seed=5)
+    for lw, l8 in zip(wd.layers, e8.weights.layers):
+        for n in ("qkv", "o", "gate_up", "down"):
+            setattr(lw, n, getattr(l8, n).dequantize())
+    ed = Engine(TINY_LLAMA, weights=wd, device="cpu", kv_pages=64, max_batch=4)
+    prompts = [[1, 5, 9, 200, 31], [7, 7, 3]]
+    a = e8.generate(prompts, max_new_tokens=6)
+    b = ed.generate(prompts, max_new_tokens=6)
+    assert [r.tokens for r in a] == [r.tokens for r in b]
+    assert e8.weights.nbytes() < 0.75 * EngineWeights.random(TINY_LLAMA, "cpu", seed=5).nbytes()
+    with pytest.raises(ValueError):
+        Engine(TINY_LLAMA, device="cpu", kv_pages=8, weight_dtype="int3")

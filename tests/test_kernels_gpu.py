@@ -598,3 +598,102 @@ def test_split_k_workspace_survives_growth_under_captured_graph():
         g.replay()
         torch.cuda.synchronize()
         assert _rel(out1.cpu(), ref1) < 1e-2
+
+
+# ------------------------------------------------------------ FP8 weight-only
+def _fp8_pair(N, K, seed, std=0.05):
+    torch.manual_seed(seed)
+    W = (torch.randn(N, K) * std).to(torch.bfloat16)
+    q = ops.quantize_fp8(ops.tile_weight(W))
+    return q, q.dequantize_f32()  # kernel operand, exact fp32 oracle
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 40, 64, 100])
+@pytest.mark.parametrize("epi", ["store", "f32", "resid", "silu"])
+def test_skinny_gemm_fp8_weights(M, epi):
+    K, N = 2048, 1024
+    q, Wd = _fp8_pair(N, K, M * 13 + len(epi))
+    x = torch.randn(M, K).to(torch.bfloat16)
+    rstd = torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    acc = x.float() @ Wd.t()
+    qd, xd = q.to(DEV), x.to(DEV)
+    if epi == "store":
+        out, ref = ops.skinny_gemm(qd, xd, ops.EPI_STORE), acc
+    elif epi == "f32":
+        out, ref = ops.skinny_gemm(qd, xd, ops.EPI_F32, norm=True), acc * rstd
+        assert out.dtype == torch.float32
+    elif epi == "resid":
+        h = torch.randn(M, N).to(torch.bfloat16)
+        out = h.to(DEV)
+        ops.skinny_gemm(qd, xd, ops.EPI_RESID, out=out)
+        ref = h.float() + acc
+    else:
+        a = acc * rstd
+        out = ops.skinny_gemm(qd, xd, ops.EPI_SILU, norm=True)
+        ref = torch.nn.functional.silu(a[:, :N // 2]) * a[:, N // 2:]
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref) < 1e-2
+    # CPU path (dequantized) of the same op agrees
+    if epi == "store":
+        assert _rel(ops.skinny_gemm(q, x, ops.EPI_STORE), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 7])
+def test_fp8_qkv_rope_and_argmax(M):
+    from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
+
+    Hq, Hkv, K = 4, 2, 512
+    N = (Hq + 2 * Hkv) * 128
+    torch.manual_seed(M)
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    q8 = ops.quantize_fp8(ops.tile_weight(W[ops.rope_row_perm(Hq + 2 * Hkv)]))
+    x = torch.randn(M, K).to(torch.bfloat16)
+    cs = rope_table(LLAMA31_8B, max_pos=2048)
+    pos = torch.randint(0, 2000, (M,), dtype=torch.int32)
+    slots = torch.randperm(4 * 64)[:M].to(torch.int32)
+    outs = []
+    for dev in ("cpu", DEV):  # CPU = dequantized reference of the same fused op
+        qo = torch.zeros(M, Hq * 128, dtype=torch.bfloat16, device=dev)
+        kc = torch.zeros(4, Hkv, 64, 128, dtype=torch.bfloat16, device=dev)
+        vc = torch.zeros_like(kc)
+        ops.qkv_rope_gemm(q8.to(dev), x.to(dev), pos.to(dev), slots.to(dev), cs.to(dev), Hq, Hkv,
+                          qo, kc, vc)
+        outs.append([t.cpu() for t in (qo, kc, vc)])
+    for a, b in zip(outs[1], outs[0]):
+        assert _rel(a, b) < 1e-2
+    V = 4096
+    l8, Wl = _fp8_pair(V, K, 99)
+    ref = (x.float() @ Wl.t()).argmax(-1)
+    keys = ops.new_argmax_keys(M, DEV)
+    ops.lm_head_argmax(l8.to(DEV), x.to(DEV), keys)
+    ids = torch.zeros(M, dtype=torch.int32, device=DEV)
+    ops.argmax_finalize(keys, ids)
+    assert ids.cpu().long().tolist() == ref.tolist()
+
+
+def test_engine_fp8_weights_decode_matches_dequantized_bf16():
+    from p2p_llm_chat_go_amd.engine import Engine
+    from p2p_llm_chat_go_amd.models.config import get_config
+    from p2p_llm_chat_go_amd.models.weights import EngineWeights
+
+    cfg = get_config("tiny-llama")
+    w8 = EngineWeights.random(cfg, DEV, seed=3)
+    e8 = Engine(cfg, weights=w8, device=DEV, kv_pages=64, max_batch=4, weight_dtype="fp8")
+    wd = EngineWeights.random(cfg, DEV, seed=3)
+    for lw, l8 in zip(wd.layers, e8.weights.layers):
+        for n in ("qkv", "o", "gate_up", "down"):
+            setattr(lw, n, getattr(l8, n).dequantize())
+    ed = Engine(cfg, weights=wd, device=DEV, kv_pages=64, max_batch=4)
+    prompts = [[1, 5, 9, 200, 31], [7, 7, 3]]
+    res = []
+    for e in (e8, ed):
+        bts = [e.kv.allocator.alloc(1) for _ in prompts]
+        _first, logits = e.prefill(prompts, bts, return_logits=True)
+        res.append(logits.float().cpu())
+        for b in bts:
+            e.kv.allocator.free(b)
+    # same weight values; only where the per-channel scale is applied differs (fp32 epilogue
+    # vs folded into bf16 weights)
+    assert _rel(res[0], res[1]) < 2e-2
+    assert len(e8.generate(prompts, max_new_tokens=8)[0].tokens) == 8
+    assert e8.weights.nbytes() < ed.weights.nbytes()
