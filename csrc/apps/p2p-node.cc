@@ -1,7 +1,7 @@
 // Chat node daemon (`go/cmd/node/main.go`), env-configured like the reference:
 // MYNAMEIS, HTTP_ADDR, DIRECTORY_URL, BOOTSTRAP_ADDRS; opt-in extras RELAY_ADDRS,
 // KEY_TYPE, IDENTITY_FILE, INBOX_FILE, ENGINE_URL, REGISTER_INTERVAL, STRICT_SENDER,
-// SECURITY, NAT_PMP, UPNP.
+// SECURITY, NAT_PMP, UPNP, DIAL_PREFER.
 // The LLM engine: ENGINE=inproc loads the engine C ABI (libp2p_engine.so,
 // csrc/engine/engine_capi.h) into this process -- the node links the engine
 // instead of calling Ollama over HTTP; otherwise /api/generate forwards to

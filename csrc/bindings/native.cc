@@ -9,6 +9,7 @@
 #include <thread>
 
 #include "net/chat.h"
+#include "net/quic.h"
 #include "net/tls.h"
 #include "net/relay.h"
 #include "runtime/scheduler.h"
@@ -38,6 +39,7 @@ NodeConfig cfg_from_dict(const py::dict& d) {
   S("relays", &c.relays);
   S("key_type", &c.key_type);
   S("security", &c.security);
+  S("dial_prefer", &c.dial_prefer);
   S("identity_file", &c.identity_file);
   S("inbox_file", &c.inbox_file);
   S("engine_url", &c.engine_url);
@@ -137,6 +139,81 @@ std::string secure_echo(const std::string& key_type, const std::string& payload,
   return res;
 }
 
+// QUIC self-test on loopback: two transports, client dials, opens `streams`
+// streams in parallel and each echoes `payload` through a multistream-negotiated
+// "/echo/1.0.0" handler.  Returns {echo ok, client retransmitted frames, rtt us}.
+std::tuple<bool, uint64_t, long> quic_echo(const std::string& kt, const std::string& payload,
+                                           double drop_rate, int streams) {
+  const KeyType t = kt == "rsa" ? KeyType::RSA : KeyType::Ed25519;
+  PrivateKey ka = PrivateKey::generate(t), kb = PrivateKey::generate(t);
+  const PeerId idb = PeerId::from_public_key(kb.public_key());
+  const PeerId ida = PeerId::from_public_key(ka.public_key());
+  auto srv = QuicTransport::create("127.0.0.1", 0, kb);
+  auto cli = QuicTransport::create("127.0.0.1", 0, ka);
+  srv->set_drop_rate(drop_rate);
+  cli->set_drop_rate(drop_rate);
+  std::string err;
+  std::mutex em;
+  srv->set_accept([&](QuicConnPtr c) {
+    if (c->remote_peer() != ida) {
+      std::lock_guard<std::mutex> lk(em);
+      err = "server saw the wrong client identity";
+    }
+    c->start([&](StreamPtr s) {
+      try {
+        auto io = std::make_shared<BufConn>(s);
+        ms_handle(*io, {"/echo/1.0.0"});
+        s->set_read_timeout(30000);
+        Bytes all = io->read_all(256 << 20);
+        io->write_all(all);
+        s->close();
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> lk(em);
+        err = std::string("server stream: ") + e.what();
+      }
+    });
+  });
+  bool ok = true;
+  long rtt = -1;
+  uint64_t retx = 0;
+  try {
+    auto c = cli->dial("127.0.0.1", srv->port(), idb, 10000);
+    c->start(nullptr);
+    std::vector<std::thread> th;
+    std::vector<int> good(streams, 0);
+    for (int i = 0; i < streams; ++i)
+      th.emplace_back([&, i] {
+        try {
+          StreamPtr s = c->open_stream();
+          auto io = std::make_shared<BufConn>(s);
+          s->set_read_timeout(30000);
+          ms_select(*io, "/echo/1.0.0");
+          io->write_all(payload);
+          s->close_write();
+          Bytes got = io->read_all(256 << 20);
+          s->close();
+          good[i] = std::string(got.begin(), got.end()) == payload;
+        } catch (const std::exception& e) {
+          std::lock_guard<std::mutex> lk(em);
+          err = std::string("client stream: ") + e.what();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (int g : good) ok = ok && g;
+    rtt = c->ping(2000);
+    retx = c->retransmitted();
+    c->close();
+  } catch (const std::exception& e) {
+    cli->close();
+    srv->close();
+    throw NetError(std::string("quic client: ") + e.what() + (err.empty() ? "" : " / " + err));
+  }
+  cli->close();
+  srv->close();
+  if (!err.empty()) throw NetError(err);
+  return {ok, retx, rtt};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -188,6 +265,20 @@ PYBIND11_MODULE(_native, m) {
     }
     return py::bytes(out);
   }, py::arg("key_type"), py::arg("payload"), py::arg("security") = "noise");
+  m.def("quic_echo", [](const std::string& kt, const py::bytes& payload, double drop, int streams) {
+    std::string in = payload;
+    py::gil_scoped_release rel;
+    return quic_echo(kt, in, drop, streams);
+  }, py::arg("key_type"), py::arg("payload"), py::arg("drop_rate") = 0.0, py::arg("streams") = 1);
+  m.def("quic_initial_keys", [](const py::bytes& dcid) {
+    QuicKeys c, s;
+    quic_initial_keys(U(dcid), &c, &s);
+    auto t = [](const QuicKeys& k) {
+      return py::make_tuple(py::bytes((const char*)k.key, 16), py::bytes((const char*)k.iv, 12),
+                            py::bytes((const char*)k.hp, 16));
+    };
+    return py::make_tuple(t(c), t(s));
+  });
   m.def("chat_message_from_json", [](const std::string& s) {
     return ChatMessage::from_json(Json::parse(s)).to_json().dump();
   });

@@ -237,6 +237,7 @@ NodeConfig NodeConfig::from_env() {
   c.conn_low = atoi(env_or("CONN_LOW", std::to_string(c.conn_low)).c_str());
   c.conn_high = atoi(env_or("CONN_HIGH", std::to_string(c.conn_high)).c_str());
   c.conn_grace_ms = (int)(atof(env_or("CONN_GRACE", "60").c_str()) * 1000);
+  c.dial_prefer = env_or("DIAL_PREFER", c.dial_prefer);
   std::string la = env_or("LISTEN_ADDRS", "");
   if (la == "none") {
     c.listen.clear();  // relay-only node
@@ -337,6 +338,7 @@ void Node::start() {
   host_ = std::make_shared<Host>(key);
   host_->set_security(split_csv(cfg_.security));
   host_->set_conn_limits(cfg_.conn_low, cfg_.conn_high, cfg_.conn_grace_ms);
+  host_->set_prefer_quic(cfg_.dial_prefer == "quic");
   if (cfg_.dht_mode != "off") {
     // created before any listener/dial so identify results feed the routing table
     kad_ = std::make_unique<Kad>(host_, cfg_.dht_mode == "client" ? KadMode::Client : KadMode::Server);
@@ -748,6 +750,7 @@ void Node::install_routes() {
       Json e = Json::object();
       e.set("peer_id", p.to_base58());
       e.set("agent", host_->peer_agent(p));
+      e.set("transport", host_->peer_transport(p));
       Json pr = Json::array();
       for (auto& x : host_->peer_protocols(p)) pr.push(x);
       e.set("protocols", pr);

@@ -111,6 +111,9 @@ struct NodeConfig {
   std::string security = "noise,tls";
   // connection manager watermarks (go-libp2p default connmgr: 160 / 192, 1 min grace)
   int conn_low = 160, conn_high = 192, conn_grace_ms = 60000;
+  // Dial ranking when a peer has QUIC and TCP addresses: "quic" (go-libp2p's
+  // ranker: QUIC first) or "order" (as advertised)
+  std::string dial_prefer = "quic";
   static NodeConfig from_env();
 };
 

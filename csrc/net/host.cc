@@ -50,6 +50,12 @@ void Host::close() {
   }
   for (auto& l : ls) l->close();
   for (auto& kv : ss) kv.second->close();
+  std::shared_ptr<QuicTransport> q;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    q = quic_;
+  }
+  if (q) q->close();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   // let detached reader / handler / identify threads that reference this host finish
@@ -60,8 +66,27 @@ void Host::close() {
 void Host::listen(const Multiaddr& ma) {
   std::string host;
   int port = 0;
+  if (ma.quic_host_port(&host, &port)) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (quic_) {
+      logf("one QUIC listener per host; skipping %s", ma.str().c_str());
+      return;
+    }
+    quic_ = QuicTransport::create(host, port, key_);
+    quic_->set_accept([this](QuicConnPtr c) {
+      if (closed_) {
+        c->close();
+        return;
+      }
+      Busy b(this);
+      add_session(c->remote_peer(), c, false);
+    });
+    listen_addrs_.push_back(
+        Multiaddr::parse("/ip4/" + host + "/udp/" + std::to_string(quic_->port()) + "/quic-v1"));
+    return;
+  }
   if (ma.has(MA_QUIC_V1) || ma.has(MA_QUIC) || ma.has(MA_UDP)) {
-    logf("transport not available (QUIC is not built; TCP only): %s", ma.str().c_str());
+    logf("transport not available (only /ip4/.../udp/.../quic-v1 is): %s", ma.str().c_str());
     return;
   }
   if (!ma.tcp_host_port(&host, &port)) throw NetError("listen: unsupported address " + ma.str());
@@ -85,6 +110,9 @@ std::vector<Multiaddr> Host::addrs() {
     if (a.tcp_host_port(&h, &port) && (h == "0.0.0.0")) {
       for (auto& ip : local_ipv4_addrs(true))
         out.push_back(Multiaddr::parse("/ip4/" + ip + "/tcp/" + std::to_string(port)));
+    } else if (a.quic_host_port(&h, &port) && (h == "0.0.0.0")) {
+      for (auto& ip : local_ipv4_addrs(true))
+        out.push_back(Multiaddr::parse("/ip4/" + ip + "/udp/" + std::to_string(port) + "/quic-v1"));
     } else {
       out.push_back(a);
     }
@@ -153,6 +181,14 @@ std::vector<std::string> Host::peer_protocols(const PeerId& p) {
   std::lock_guard<std::mutex> lk(mu_);
   auto it = peer_protos_.find(p);
   return it == peer_protos_.end() ? std::vector<std::string>{} : it->second;
+}
+
+std::string Host::peer_transport(const PeerId& p) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = sessions_.find(p);
+  if (it == sessions_.end() || it->second->closed()) return "";
+  auto t = peer_transport_.find(p);
+  return t == peer_transport_.end() ? "" : t->second;
 }
 
 std::string Host::peer_agent(const PeerId& p) {
@@ -270,10 +306,11 @@ void Host::add_session(const PeerId& p, SessionPtr s, bool relayed) {
     // Prefer a direct connection over a relayed one; otherwise keep the newest.
     if (it != sessions_.end() && !it->second->closed()) old = it->second;
     sessions_[p] = s;
+    peer_transport_[p] = relayed ? "p2p-circuit" : (s->transport() == "quic-v1" ? "quic-v1" : "tcp");
     const auto now = std::chrono::steady_clock::now();
     conn_use_[p] = ConnUse{now, now};
   }
-  std::weak_ptr<YamuxSession> ws = s;
+  std::weak_ptr<MuxSession> ws = s;
   busy_++;  // released by the session's on_close
   s->start([this, p, relayed](StreamPtr st) {
              Busy b(this);
@@ -424,10 +461,13 @@ SessionPtr Host::connect(const PeerId& p, const std::vector<Multiaddr>& addrs, i
   }
   add_addrs(p, addrs);
   std::vector<Multiaddr> cands = peer_addrs(p);
-  // direct addresses first, then relayed ones
-  std::stable_sort(cands.begin(), cands.end(), [](const Multiaddr& a, const Multiaddr& b) {
-    return !a.has(MA_P2P_CIRCUIT) && b.has(MA_P2P_CIRCUIT);
-  });
+  // direct addresses first (QUIC ahead of TCP when preferred), then relayed ones
+  auto rank = [this](const Multiaddr& a) {
+    if (a.has(MA_P2P_CIRCUIT)) return 2;
+    return (prefer_quic_ && a.has(MA_QUIC_V1)) ? 0 : 1;
+  };
+  std::stable_sort(cands.begin(), cands.end(),
+                   [&](const Multiaddr& a, const Multiaddr& b) { return rank(a) < rank(b); });
   if (cands.empty()) throw NetError("no addresses");
   std::string errs;
   auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
@@ -444,6 +484,11 @@ SessionPtr Host::connect(const PeerId& p, const std::vector<Multiaddr>& addrs, i
       }
       std::string h;
       int port;
+      if (a.quic_host_port(&h, &port)) {
+        auto c = quic_for_dial()->dial(h, port, p, std::min(left, 5000));
+        add_session(p, c, false);
+        return c;
+      }
       if (!a.tcp_host_port(&h, &port)) {
         errs += " [" + a.str() + ": unsupported transport]";
         continue;
@@ -460,6 +505,14 @@ SessionPtr Host::connect(const PeerId& p, const std::vector<Multiaddr>& addrs, i
     }
   }
   throw NetError("failed to dial " + p.to_base58() + ":" + errs);
+}
+
+std::shared_ptr<QuicTransport> Host::quic_for_dial() {
+  std::lock_guard<std::mutex> lk(mu_);
+  // dial from the listening socket (one 4-tuple per peer, NAT-friendly like
+  // go-libp2p's reuse); a host without a QUIC listener gets a dial-only socket
+  if (!quic_) quic_ = QuicTransport::create("0.0.0.0", 0, key_);
+  return quic_;
 }
 
 StreamCtx Host::new_stream(const PeerId& p, const std::string& proto, int timeout_ms) {

@@ -14,6 +14,7 @@
 
 #include "conn.h"
 #include "multiaddr.h"
+#include "quic.h"
 #include "yamux.h"
 
 namespace p2p {
@@ -45,8 +46,8 @@ class Host {
   const PrivateKey& key() const { return key_; }
   std::string agent() const { return agent_; }
 
-  // Listen on /ip4/<host>/tcp/<port> (port 0 = ephemeral).  Other transports
-  // (quic-v1) are accepted in the address list but skipped with a log line.
+  // Listen on /ip4/<host>/tcp/<port> or /ip4/<host>/udp/<port>/quic-v1 (port 0 =
+  // ephemeral).  Other transports are skipped with a log line.
   void listen(const Multiaddr& ma);
   // h.Addrs(): listen addrs with 0.0.0.0 expanded to interface addresses, plus
   // relay circuit addresses of active reservations.
@@ -77,6 +78,8 @@ class Host {
   // Identify results for a peer (protocols / listen addrs / agent).
   std::vector<std::string> peer_protocols(const PeerId& p);
   std::string peer_agent(const PeerId& p);
+  // Transport of the live session: "tcp", "quic-v1" or "p2p-circuit" ("" = none).
+  std::string peer_transport(const PeerId& p);
 
   // Called after identify completes for a peer (protocols, listen addrs); the
   // DHT uses it to fill its routing table like go-libp2p-kad-dht does.
@@ -96,6 +99,10 @@ class Host {
   // ones that are past the grace period and carry no open stream are closed until
   // `low` remain.  A trimmed peer is simply re-dialed on its next message.
   void set_conn_limits(int low, int high, int grace_ms);
+
+  // Dial ranking: go-libp2p dials QUIC addresses ahead of TCP ones (its dial
+  // ranker delays TCP while a QUIC dial is pending); off = keep address order.
+  void set_prefer_quic(bool on) { prefer_quic_ = on; }
   long trimmed() const { return trimmed_; }
 
   void close();
@@ -103,6 +110,7 @@ class Host {
 
  private:
   void accept_loop(std::shared_ptr<TcpListener> l);
+  std::shared_ptr<QuicTransport> quic_for_dial();
   void handle_stream(StreamPtr s, PeerId peer, bool relayed);
   void add_session(const PeerId& p, SessionPtr s, bool relayed);
   void run_identify(const PeerId& p, SessionPtr s);
@@ -126,7 +134,10 @@ class Host {
   std::atomic<long> trimmed_{0};
   std::map<PeerId, std::vector<std::string>> peer_protos_;
   std::map<PeerId, std::string> peer_agents_;
+  std::map<PeerId, std::string> peer_transport_;
   std::vector<std::shared_ptr<TcpListener>> listeners_;
+  std::shared_ptr<QuicTransport> quic_;  // the QUIC listener, or a dial-only socket
+  bool prefer_quic_ = true;
   std::vector<Multiaddr> listen_addrs_;
   std::vector<Multiaddr> extra_addrs_;
   std::vector<std::thread> threads_;

@@ -198,4 +198,13 @@ bool Multiaddr::tcp_host_port(std::string* host, int* port) const {
   return false;
 }
 
+bool Multiaddr::quic_host_port(std::string* host, int* port) const {
+  if (parts_.size() < 3 || parts_[0].code != MA_IP4 || parts_[1].code != MA_UDP ||
+      parts_[2].code != MA_QUIC_V1)
+    return false;
+  *host = value_to_string(by_code(MA_IP4), parts_[0].value);
+  *port = (parts_[1].value[0] << 8) | parts_[1].value[1];
+  return true;
+}
+
 }  // namespace p2p

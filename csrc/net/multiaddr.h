@@ -39,6 +39,8 @@ class Multiaddr {
   bool split_circuit(Multiaddr* relay, Multiaddr* target) const;
   // For /ip4|ip6|dns*/.../tcp/<port>: host + port.
   bool tcp_host_port(std::string* host, int* port) const;
+  // For /ip4/<a>/udp/<port>/quic-v1: host + port.
+  bool quic_host_port(std::string* host, int* port) const;
   bool operator==(const Multiaddr& o) const { return bytes() == o.bytes(); }
 
  private:

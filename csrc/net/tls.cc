@@ -179,6 +179,18 @@ Bytes tls_signed_key_der(const Bytes& pubkey_pb, const Bytes& sig) {
   return out;
 }
 
+void tls_make_cert(const PrivateKey& id, void** key_out, void** cert_out) {
+  EVP_PKEY* k = nullptr;
+  X509* c = nullptr;
+  make_cert(id, &k, &c);
+  *key_out = k;
+  *cert_out = c;
+}
+
+void tls_verify_peer_cert(void* x509, PublicKey* key, PeerId* id) {
+  verify_peer_cert((X509*)x509, key, id);
+}
+
 bool tls_parse_signed_key(const Bytes& der, Bytes* pubkey_pb, Bytes* sig) {
   size_t p = 0;
   Bytes seq;

@@ -70,5 +70,10 @@ class TlsConn : public Conn {
 // Certificate extension helpers (exposed for tests / codecs).
 Bytes tls_signed_key_der(const Bytes& pubkey_pb, const Bytes& sig);
 bool tls_parse_signed_key(const Bytes& der, Bytes* pubkey_pb, Bytes* sig);
+// The libp2p certificate of `id` (fresh P-256 key; EVP_PKEY** / X509** as void**),
+// and authentication of a peer certificate (X509*) -> its libp2p key and PeerID.
+// Shared with the QUIC transport, whose TLS handshake carries the same certificate.
+void tls_make_cert(const PrivateKey& id, void** key_out, void** cert_out);
+void tls_verify_peer_cert(void* x509, PublicKey* key, PeerId* id);
 
 }  // namespace p2p

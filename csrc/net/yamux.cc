@@ -153,7 +153,7 @@ void YamuxSession::send_frame(uint8_t type, uint16_t flags, uint32_t id, uint32_
 
 StreamPtr YamuxSession::open_stream() {
   if (closed_) throw NetError("session closed");
-  StreamPtr s;
+  YStreamPtr s;
   {
     std::lock_guard<std::mutex> lk(mu_);
     uint32_t id = next_id_;
@@ -184,7 +184,7 @@ void YamuxSession::close() {
   } catch (...) {
   }
   conn_->close();
-  std::map<uint32_t, StreamPtr> ss;
+  std::map<uint32_t, YStreamPtr> ss;
   {
     std::lock_guard<std::mutex> lk(mu_);
     ss.swap(streams_);
@@ -213,7 +213,7 @@ long YamuxSession::ping(int timeout_ms) {
       .count();
 }
 
-void YamuxSession::handle_flags(const StreamPtr& s, uint16_t flags) {
+void YamuxSession::handle_flags(const YStreamPtr& s, uint16_t flags) {
   bool remove = false;
   {
     std::lock_guard<std::mutex> lk(s->mu_);
@@ -262,7 +262,7 @@ void YamuxSession::reader_loop() {
         if (len > kInitialWindow * 64) throw NetError("yamux: frame too large");
         payload = conn_->read_exact(len);
       }
-      StreamPtr s;
+      YStreamPtr s;
       bool is_new = false;
       {
         std::lock_guard<std::mutex> lk(mu_);

@@ -15,12 +15,13 @@
 #include <thread>
 
 #include "conn.h"
+#include "mux.h"
 
 namespace p2p {
 
 class YamuxSession;
 
-class YamuxStream : public Conn {
+class YamuxStream : public MuxStream {
  public:
   YamuxStream(std::shared_ptr<YamuxSession> s, uint32_t id);
   ~YamuxStream() override;
@@ -29,12 +30,11 @@ class YamuxStream : public Conn {
   void write_all(const uint8_t* buf, size_t n) override;
   void close_write() override;  // FIN
   void close() override;        // FIN + stop reading
-  void reset();                 // RST
+  void reset() override;        // RST
   void set_read_timeout(int ms) override { timeout_ms_ = ms; }
   std::string remote_addr() const override;
   uint32_t id() const { return id_; }
   std::shared_ptr<YamuxSession> session() const { return s_; }
-  std::string protocol;  // negotiated protocol (set by the host)
 
  private:
   friend class YamuxSession;
@@ -50,9 +50,9 @@ class YamuxStream : public Conn {
   bool remote_fin_ = false, local_fin_ = false, reset_ = false, local_closed_ = false;
   int timeout_ms_ = 0;
 };
-using StreamPtr = std::shared_ptr<YamuxStream>;
+using YStreamPtr = std::shared_ptr<YamuxStream>;
 
-class YamuxSession : public std::enable_shared_from_this<YamuxSession> {
+class YamuxSession : public MuxSession, public std::enable_shared_from_this<YamuxSession> {
  public:
   static constexpr uint32_t kInitialWindow = 256 * 1024;
   static constexpr uint32_t kMaxFrame = 64 * 1024;
@@ -61,13 +61,15 @@ class YamuxSession : public std::enable_shared_from_this<YamuxSession> {
   ~YamuxSession();
   // Starts the reader thread.  on_stream runs (in its own thread) for every inbound stream;
   // on_close runs once when the session dies.
-  void start(std::function<void(StreamPtr)> on_stream, std::function<void()> on_close = nullptr);
-  StreamPtr open_stream();
-  void close();
-  bool closed() const { return closed_; }
+  void start(std::function<void(StreamPtr)> on_stream,
+             std::function<void()> on_close = nullptr) override;
+  StreamPtr open_stream() override;
+  void close() override;
+  bool closed() const override { return closed_; }
+  std::string transport() const override { return "yamux"; }
   // Round-trip ping; returns RTT in microseconds or -1 on timeout.
-  long ping(int timeout_ms);
-  size_t num_streams();
+  long ping(int timeout_ms) override;
+  size_t num_streams() override;
   const ConnPtr& conn() const { return conn_; }
 
  private:
@@ -76,13 +78,13 @@ class YamuxSession : public std::enable_shared_from_this<YamuxSession> {
   void send_frame(uint8_t type, uint16_t flags, uint32_t id, uint32_t length,
                   const uint8_t* data = nullptr);
   void remove_stream(uint32_t id);
-  void handle_flags(const StreamPtr& s, uint16_t flags);
+  void handle_flags(const YStreamPtr& s, uint16_t flags);
 
   ConnPtr conn_;
   bool client_;
   std::mutex wmu_;
   std::mutex mu_;
-  std::map<uint32_t, StreamPtr> streams_;
+  std::map<uint32_t, YStreamPtr> streams_;
   uint32_t next_id_;
   std::atomic<bool> closed_{false};
   std::function<void(StreamPtr)> on_stream_;
@@ -94,6 +96,5 @@ class YamuxSession : public std::enable_shared_from_this<YamuxSession> {
   uint32_t ping_id_ = 0;
   std::map<uint32_t, bool> ping_done_;
 };
-using SessionPtr = std::shared_ptr<YamuxSession>;
 
 }  // namespace p2p

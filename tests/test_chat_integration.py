@@ -523,3 +523,55 @@ def test_connection_manager_trims_to_low_watermark(procs):
         time.sleep(0.05)
     assert sorted(x["content"] for x in json.loads(http("GET", a + "/inbox")[1])) == \
         ["hi B", "hi C", "hi D", "hi E"]
+
+
+# ------------------------------------------------------------------ QUIC transport
+def _wait_inbox(url, n):
+    for _ in range(200):
+        inbox = json.loads(http("GET", url + "/inbox")[1])
+        if len(inbox) >= n:
+            return inbox
+        time.sleep(0.05)
+    return inbox
+
+
+@pytest.mark.parametrize("key", ["ed25519", "rsa"])
+def test_quic_only_nodes_exchange_messages(procs, key):
+    """Both nodes listen on /udp/.../quic-v1 only (the reference's second listener,
+    `go/cmd/node/main.go:140`): the chat stream runs over a native QUIC stream with
+    TLS 1.3 (libp2p certificate) inside the QUIC handshake."""
+    d = start_directory(procs)
+    q = {"LISTEN_ADDRS": "/ip4/127.0.0.1/udp/0/quic-v1"}
+    a = start_node(procs, "A", d, q, key=key)
+    b = start_node(procs, "B", d, q, key=key)
+    me = json.loads(http("GET", a + "/me")[1])
+    assert me["addrs"] and all("/udp/" in x and "/quic-v1/p2p/" in x for x in me["addrs"])
+    for i in range(3):
+        assert http("POST", a + "/send", {"to_username": "B", "content": "q%d" % i})[0] == 200
+    assert [m["content"] for m in _wait_inbox(b, 3)] == ["q0", "q1", "q2"]
+    assert http("POST", b + "/send", {"to_username": "A", "content": "back"})[0] == 200
+    assert _wait_inbox(a, 1)[0]["content"] == "back"
+    peers = json.loads(http("GET", a + "/peers")[1])
+    assert peers and peers[0]["transport"] == "quic-v1"
+    for _ in range(100):  # identify ran over a QUIC stream too
+        peers = json.loads(http("GET", a + "/peers")[1])
+        if peers[0]["protocols"]:
+            break
+        time.sleep(0.05)
+    assert "/p2p-llm-chat/1.0.0" in peers[0]["protocols"]
+
+
+@pytest.mark.parametrize("prefer,transport", [("quic", "quic-v1"), ("order", "tcp")])
+def test_dial_ranking_tcp_and_quic(procs, prefer, transport):
+    """With TCP and QUIC listeners (the reference's default pair), the dialer ranks
+    QUIC first like go-libp2p; DIAL_PREFER=order keeps the advertised order (TCP)."""
+    d = start_directory(procs)
+    both = {"LISTEN_ADDRS": "/ip4/127.0.0.1/tcp/0,/ip4/127.0.0.1/udp/0/quic-v1",
+            "DIAL_PREFER": prefer}
+    a = start_node(procs, "A", d, both)
+    b = start_node(procs, "B", d, both)
+    addrs = json.loads(http("GET", b + "/me")[1])["addrs"]
+    assert any("/tcp/" in x for x in addrs) and any("/quic-v1/" in x for x in addrs)
+    assert http("POST", a + "/send", {"to_username": "B", "content": "hi"})[0] == 200
+    assert _wait_inbox(b, 1)[0]["content"] == "hi"
+    assert json.loads(http("GET", a + "/peers")[1])[0]["transport"] == transport

@@ -1,6 +1,7 @@
 """Unit tests of the native libp2p subset: varint, base58, multiaddr, keys/PeerIDs,
 signatures, Go-compatible JSON, RFC3339, and Noise XX + yamux over a socketpair."""
 import json
+import os
 
 import pytest
 from hypothesis import given, settings, strategies as st
@@ -135,3 +136,29 @@ def test_secure_yamux_echo(N, kt, size, sec):
 def test_uuid4(N):
     u = N.uuid4()
     assert len(u) == 36 and u[14] == "4" and u[19] in "89ab"
+
+
+# ------------------------------------------------------------------ QUIC (RFC 9000/9001)
+def test_quic_initial_keys_rfc9001_appendix_a(N):
+    """RFC 9001 Appendix A.1: Initial keys for DCID 0x8394c8f03e515708."""
+    c, s = N.quic_initial_keys(bytes.fromhex("8394c8f03e515708"))
+    assert [x.hex() for x in c] == ["1f369613dd76d5467730efcbe3b1a22d", "fa044b2f42a3fd3b46fb255c",
+                                    "9f50449e04a0e810283a1e9933adedd2"]
+    assert [x.hex() for x in s] == ["cf3a5331653c364c88f0f379b6067e37", "0ac1493ca1905853b0bba03e",
+                                    "c206b8d9b9f0f37644430b490eeaa314"]
+
+
+@pytest.mark.parametrize("key,size,drop,streams", [
+    ("ed25519", 10, 0.0, 1),
+    ("rsa", 1 << 20, 0.0, 1),          # flow-control credit updates, multi-packet crypto flight
+    ("ed25519", 4 << 20, 0.0, 4),      # concurrent streams, in-flight window
+    ("ed25519", 128 << 10, 0.1, 8),    # 10% datagram loss each way: PTO retransmission,
+    ("rsa", 512 << 10, 0.05, 2),       # reordered stream opening, handshake recovery
+])
+def test_quic_echo(N, key, size, drop, streams):
+    payload = os.urandom(size)
+    ok, retx, rtt = N.quic_echo(key, payload, drop, streams)
+    assert ok
+    assert rtt > 0  # PING acknowledged
+    if drop > 0:
+        assert retx > 0

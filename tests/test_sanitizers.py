@@ -127,6 +127,18 @@ def test_daemons_clean_under_sanitizer(sanbin, tmp_path):
         c = _node(sp, "C", d, {"LISTEN_ADDRS": "none", "RELAY_ADDRS": lines[0]})
         assert http("POST", a + "/send", {"to_username": "C", "content": "via relay"})[0] == 200
         assert _wait_inbox(c, 1)[0]["content"] == "via relay"
+        # QUIC pair: transport thread, stream readers and senders share each connection
+        q = {"LISTEN_ADDRS": "/ip4/127.0.0.1/udp/0/quic-v1"}
+        e = _node(sp, "E", d, q)
+        f = _node(sp, "F", d, q, key="rsa")
+        with cf.ThreadPoolExecutor(8) as ex:
+            sts = list(ex.map(lambda i: http("POST", e + "/send",
+                                             {"to_username": "F", "content": "q%d" % i})[0],
+                              range(16)))
+        assert sts == [200] * 16
+        assert http("POST", f + "/send", {"to_username": "E", "content": "back"})[0] == 200
+        assert len(_wait_inbox(f, 16)) == 16
+        assert _wait_inbox(e, 1)[0]["content"] == "back"
     finally:
         sp.close()
     bad = sp.reports()
