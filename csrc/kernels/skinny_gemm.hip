@@ -38,22 +38,26 @@
 
 namespace {
 
-// F8: weight-only FP8 (OCP e4m3) -- the weight stream is 8 bytes per lane per k-step (half
-// of bf16), widened to bf16 in registers right before the MFMA; the per-output-channel
-// scale (ea.wscale) is applied to the accumulator in the epilogue.
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// F8: weight-only FP8 (OCP e4m3) -- half the bytes of bf16, widened to bf16 in registers
+// right before the MFMA; the per-output-channel scale (ea.wscale) is applied to the
+// accumulator in the epilogue.  The codes of k-steps 2p and 2p+1 are interleaved per lane
+// (ops.gemm.pair_f8), so one 16-byte load per lane (1 KiB per wave, as in bf16) feeds two
+// MFMAs: the pipeline runs over "super-steps" of KP = 2 k-steps.  (8-byte loads, one
+// k-step each, left the fp8 stream at ~2.5-4.8 TB/s: half the bytes in flight per load.)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 template <bool F8>
-using wraw_t = typename std::conditional<F8, u32x2, bf16x8>::type;
+using wraw_t = typename std::conditional<F8, u32x4, bf16x8>::type;
 
-__device__ __forceinline__ bf16x8 widen(const bf16x8& w) { return w; }
-// 8 e4m3 codes -> 8 bf16: four gfx950 v_cvt_scalef32_pk_bf16_fp8 (unit scale)
-__device__ __forceinline__ bf16x8 widen(const u32x2& w) {
-  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, false);
-  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, true);
-  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, false);
-  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, true);
+__device__ __forceinline__ bf16x8 widen(const bf16x8& w, int) { return w; }
+// 8 e4m3 codes (half h of the pair) -> 8 bf16: four gfx950 v_cvt_scalef32_pk_bf16_fp8
+__device__ __forceinline__ bf16x8 widen(const u32x4& p, int h) {
+  const unsigned lo = h ? p.z : p.x, hi = h ? p.w : p.y;
+  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, false);
+  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, true);
+  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, false);
+  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, true);
   bf16x8 r;
   r[0] = a.x; r[1] = a.y; r[2] = b.x; r[3] = b.y;
   r[4] = c.x; r[5] = c.y; r[6] = d.x; r[7] = d.y;
@@ -68,7 +72,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   // A loads (MT per k-step) and the NORM sum of squares dominate unless reused.
   constexpr int NB = (EPI == EPI_SILU) ? 2 : 1;
   constexpr int NW = NG * NB;  // weight fragments per k-step
-  const int S = K >> 5;
+  constexpr int KP = F8 ? 2 : 1;  // k-steps per 16-byte weight load
+  const int S = (K >> 5) / KP;    // super-steps
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int g0 = blockIdx.x * NG;
@@ -137,36 +142,46 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
 
-  auto load = [&](int s, WR(&bw)[U][NW], bf16x8(&ax)[U][MT]) {
+  // A fragments of super-step s: ax[h * MT + mt] = rows of m-tile mt at k-step s*KP + h
+  auto loadx = [&](int s, bf16x8(&ax)[KP * MT]) {
+#pragma unroll
+    for (int h = 0; h < KP; ++h)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        ax[h * MT + mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + (s * KP + h) * 32)
+                                 : zero_bf16x8();
+  };
+  auto load = [&](int s, WR(&bw)[U][NW], bf16x8(&ax)[U][KP * MT]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int b = 0; b < NW; ++b) bw[u][b] = __builtin_nontemporal_load(wp[b] + (size_t)(s + u) * 64);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        ax[u][mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + (s + u) * 32)
-                           : zero_bf16x8();
+      loadx(s + u, ax[u]);
     }
   };
-  auto compute1 = [&](const WR(&bwr)[NW], const bf16x8(&ax)[MT]) {
-    bf16x8 bw[NW];
+  auto compute1 = [&](const WR(&bwr)[NW], const bf16x8(&ax)[KP * MT]) {
 #pragma unroll
-    for (int b = 0; b < NW; ++b) bw[b] = widen(bwr[b]);
+    for (int h = 0; h < KP; ++h) {
+      bf16x8 bw[NW];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+      for (int b = 0; b < NW; ++b) bw[b] = widen(bwr[b], h);
 #pragma unroll
-      for (int b = 0; b < NW; ++b)
-        acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[mt], bw[b], acc[b][mt], 0, 0, 0);
-      if constexpr (NORM) {
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16x8& a = ax[h * MT + mt];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xf = (float)ax[mt][j];
-          ss[mt] = fmaf(xf, xf, ss[mt]);
+        for (int b = 0; b < NW; ++b)
+          acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[b], acc[b][mt], 0, 0, 0);
+        if constexpr (NORM) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xf = (float)a[j];
+            ss[mt] = fmaf(xf, xf, ss[mt]);
+          }
         }
       }
     }
   };
-  auto compute = [&](WR(&bw)[U][NW], bf16x8(&ax)[U][MT]) {
+  auto compute = [&](WR(&bw)[U][NW], bf16x8(&ax)[U][KP * MT]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) compute1(bw[u], ax[u]);
   };
@@ -175,7 +190,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   const int nb = n / U;
   if (nb > 0) {
     WR bA[U][NW], bB[U][NW];
-    bf16x8 aA[U][MT], aB[U][MT];
+    bf16x8 aA[U][KP * MT], aB[U][KP * MT];
     load(s0, bA, aA);
     int b = 0;
     for (; b + 2 < nb; b += 2) {
@@ -194,12 +209,10 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   }
   for (int s = s0 + nb * U; s < s1; ++s) {
     WR b1[NW];
-    bf16x8 a1[MT];
+    bf16x8 a1[KP * MT];
 #pragma unroll
     for (int b = 0; b < NW; ++b) b1[b] = __builtin_nontemporal_load(wp[b] + (size_t)s * 64);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-      a1[mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + s * 32) : zero_bf16x8();
+    loadx(s, a1);
     compute1(b1, a1);
   }
 
@@ -318,7 +331,10 @@ int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, 
               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   // pipeline depth: MT=1 -> 4 or 8 k-steps per batch; MT>1 holds MT A fragments per
   // k-step, so batches of 2 (4 at MT=2) keep it under ~128 VGPRs (no scratch)
-  const int u = ea.u ? ea.u : (MT == 1 ? g_u_mt1 : 2);
+  int u = ea.u ? ea.u : (MT == 1 ? g_u_mt1 : 2);
+  // FP8 holds KP = 2 A fragments per weight load: the deep batch spills to scratch at
+  // 8 waves (<= 128 VGPRs) and at MT = 4, so those take the shallow one.
+  if (ea.wscale && (WAVES == 8 || MT == 4)) u = MT == 1 ? 4 : 2;
   if constexpr (MT == 1) {
     if (u == 8)
       return launch_mwu<MT, WAVES, EPI, NORM, 8>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
@@ -334,7 +350,7 @@ template <int MT, int WAVES, int EPI, bool NORM, int U>
 int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
                void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   if (ea.wscale) {  // FP8 weights (dense projections, one column group per block)
-    if (ea.moe_cnt) return (int)hipErrorInvalidValue;
+    if (ea.moe_cnt || (K % 64) != 0) return (int)hipErrorInvalidValue;  // k-step pairs
     hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, false, 1, true>), dim3(groups),
                        dim3(WAVES * 64), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K,
                        up_off, out, ldo, eps, ea);
@@ -465,7 +481,7 @@ P2P_API void p2p_skinny_gemm_tune(int u_mt1, int resident) {
 }
 
 // wscale (all three entry points): null = bf16 fragment-major weights; else FP8 e4m3
-// weights in the same fragment order (8 bytes per lane per k-step) and their
+// weights in the same fragment order, k-steps paired (ops.gemm.pair_f8), and their
 // per-output-channel fp32 scales.
 P2P_API int p2p_skinny_gemm(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
                             int norm, void* out, int ldo, float eps, int waves,

@@ -29,9 +29,11 @@ FP8_MAX = 448.0  # OCP e4m3 (the gfx950 format; torch.float8_e4m3fn)
 
 class Fp8Weight:
     """Weight-only FP8 projection: e4m3 codes in the fragment-major order of
-    ``tile_weight`` (uint8 ``[N/16, K/32, 64, 8]``: the decode stream is 8 bytes per lane
-    per k-step, half of bf16) and a per-output-channel fp32 scale ``[N]``.  The skinny
-    GEMM widens the codes to bf16 in registers and applies the scale in its epilogue."""
+    ``tile_weight`` with k-steps interleaved in pairs (uint8 ``[N/16, K/32, 64, 8]``, see
+    ``pair_f8``: each lane's 16-byte load holds its codes of two consecutive k-steps, so
+    a wave still moves 1 KiB per load instruction, as in bf16) and a per-output-channel
+    fp32 scale ``[N]``.  The skinny GEMM widens the codes to bf16 in registers and applies
+    the scale in its epilogue."""
 
     def __init__(self, data: torch.Tensor, scale: torch.Tensor):
         self.data = data
@@ -56,7 +58,7 @@ class Fp8Weight:
 
     def dequantize_f32(self) -> torch.Tensor:
         """Exact fp32 [N, K] (natural layout) values the kernel multiplies with."""
-        q = untile_weight(self.data.view(torch.float8_e4m3fn)).float()
+        q = untile_weight(unpair_f8(self.data).view(torch.float8_e4m3fn)).float()
         return q * self.scale.float()[:, None].to(q.device)
 
     def dequantize(self) -> torch.Tensor:
@@ -67,10 +69,23 @@ class Fp8Weight:
 def quantize_fp8(wt: torch.Tensor) -> Fp8Weight:
     """bf16 fragment-major weight -> Fp8Weight (per-output-channel absmax scaling)."""
     w = untile_weight(wt).float()
+    assert w.shape[1] % 64 == 0, "fp8 weights need K % 64 == 0 (k-step pairs)"
     amax = w.abs().amax(dim=1).clamp_min(1e-12)
     scale = amax / FP8_MAX
     q = (w / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
-    return Fp8Weight(tile_weight(q.view(torch.uint8)), scale.float().contiguous())
+    return Fp8Weight(pair_f8(tile_weight(q.view(torch.uint8))), scale.float().contiguous())
+
+
+def pair_f8(t: torch.Tensor) -> torch.Tensor:
+    """Fragment-major 1-byte codes [G, S, 64, 8] -> k-step pairs: [G, S/2, lane, (2, 8)],
+    i.e. lane l's 16 bytes at pair p are its fragments of k-steps 2p and 2p+1."""
+    G, S = t.shape[0], t.shape[1]
+    return t.reshape(G, S // 2, 2, 64, 8).transpose(2, 3).contiguous().reshape(G, S, 64, 8)
+
+
+def unpair_f8(t: torch.Tensor) -> torch.Tensor:
+    G, S = t.shape[0], t.shape[1]
+    return t.reshape(G, S // 2, 64, 2, 8).transpose(2, 3).contiguous().reshape(G, S, 64, 8)
 
 
 def _is_f8(wt) -> bool:

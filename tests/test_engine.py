@@ -171,6 +171,22 @@ def test_fp8_quantize_roundtrip_cpu():
     assert ((Wd - W.float()).norm() / W.float().norm()) < 0.04
 
 
+def test_fp8_pair_layout_cpu():
+    """Lane l's 16 bytes at pair p = its fragment of k-step 2p, then of k-step 2p+1."""
+    from p2p_llm_chat_go_amd import ops
+
+    t = torch.randint(0, 256, (3, 6, 64, 8), dtype=torch.uint8)
+    p = ops.gemm.pair_f8(t)
+    assert p.shape == t.shape
+    flat = p.reshape(3, 3, 64, 16)
+    for g, pp, lane in [(0, 0, 0), (1, 2, 17), (2, 1, 63)]:
+        assert torch.equal(flat[g, pp, lane, :8], t[g, 2 * pp, lane])
+        assert torch.equal(flat[g, pp, lane, 8:], t[g, 2 * pp + 1, lane])
+    assert torch.equal(ops.gemm.unpair_f8(p), t)
+    with pytest.raises(AssertionError):
+        ops.quantize_fp8(ops.tile_weight(torch.randn(16, 96).to(torch.bfloat16)))
+
+
 def test_fp8_engine_cpu_matches_dequantized_weights():
     w8 = EngineWeights.random(TINY_LLAMA, "cpu", seed=5)
     e8 = Engine(TINY_LLAMA, weights=w8, device="cpu", kv_pages=64, max_batch=4,
