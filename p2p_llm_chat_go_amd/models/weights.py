@@ -72,16 +72,20 @@ class EngineWeights:
                     n += nb(t)
         return n
 
-    def quantize_fp8(self, names=("qkv", "o", "gate_up", "down")) -> "EngineWeights":
-        """Weight-only FP8 (e4m3, per-output-channel scale) for the dense projections, in
-        place: the decode weight stream -- the roofline of batch-1 decode -- halves.  The
-        embedding, LM head, router and MoE experts stay bf16.  Opt-in (ENGINE_WEIGHTS=fp8 /
-        bench.py --weights fp8); the headline numbers are bf16."""
+    def quantize_fp8(self, names=("qkv", "o", "gate_up", "down"), lm_head=True) -> "EngineWeights":
+        """Weight-only FP8 (e4m3, per-output-channel scale) for the dense projections and
+        the LM head, in place: the decode weight stream -- the roofline of batch-1 decode --
+        halves (the 8B LM head alone is 1 GiB of bf16 per token).  The embedding, router
+        and MoE experts stay bf16.  Opt-in (ENGINE_WEIGHTS=fp8 / bench.py --weights fp8);
+        the headline numbers are bf16."""
         for lw in self.layers:
             for name in names:
                 t = getattr(lw, name)
                 if isinstance(t, torch.Tensor):
                     setattr(lw, name, ops.quantize_fp8(t))
+        if lm_head and isinstance(self.lm_head, torch.Tensor) and \
+                ops.tiled_shape(self.lm_head)[1] % 64 == 0:
+            self.lm_head = ops.quantize_fp8(self.lm_head)
         return self
 
     # ------------------------------------------------------------------ build

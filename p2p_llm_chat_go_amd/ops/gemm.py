@@ -319,10 +319,12 @@ def lm_head_argmax(wt, x, keys, col_offset: int = 0, eps: float = 1e-5, waves: i
                                            _lib.stream_ptr(x.device)), "tiled_gemm_argmax")
         return keys
     wp, sp = _wptr(wt)
-    _lib.check(L.p2p_skinny_gemm_argmax(wp, x.data_ptr(), x.stride(0), M, K, N,
-                                        keys.data_ptr(), int(col_offset), float(eps),
-                                        _code(wt, M, EPI_ARGMAX, True, waves), sp,
-                                        _lib.stream_ptr(x.device)), "skinny_gemm_argmax")
+    for m0 in range(0, M, SKINNY_MAX_M):  # > 64 rows only reach here with FP8 weights
+        mc = min(SKINNY_MAX_M, M - m0)
+        _lib.check(L.p2p_skinny_gemm_argmax(wp, x[m0:].data_ptr(), x.stride(0), mc, K, N,
+                                            keys[m0:].data_ptr(), int(col_offset), float(eps),
+                                            _code(wt, mc, EPI_ARGMAX, True, waves), sp,
+                                            _lib.stream_ptr(x.device)), "skinny_gemm_argmax")
     return keys
 
 

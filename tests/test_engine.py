@@ -8,6 +8,7 @@ near-tie (random-init models have many near-ties).
 import pytest
 import torch
 
+from p2p_llm_chat_go_amd import ops
 from p2p_llm_chat_go_amd.engine import Engine
 from p2p_llm_chat_go_amd.models import TINY_LLAMA
 from p2p_llm_chat_go_amd.models.reference import (random_state_dict, reference_forward,
@@ -195,6 +196,8 @@ def test_fp8_engine_cpu_matches_dequantized_weights():
     for lw, l8 in zip(wd.layers, e8.weights.layers):
         for n in ("qkv", "o", "gate_up", "down"):
             setattr(lw, n, getattr(l8, n).dequantize())
+    if isinstance(e8.weights.lm_head, ops.Fp8Weight):  # fp8 mode quantizes the LM head too
+        wd.lm_head = e8.weights.lm_head.dequantize()
     ed = Engine(TINY_LLAMA, weights=wd, device="cpu", kv_pages=64, max_batch=4)
     prompts = [[1, 5, 9, 200, 31], [7, 7, 3]]
     a = e8.generate(prompts, max_new_tokens=6)

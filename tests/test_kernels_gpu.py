@@ -638,7 +638,7 @@ def test_skinny_gemm_fp8_weights(M, epi):
         assert _rel(ops.skinny_gemm(q, x, ops.EPI_STORE), ref) < 1e-2
 
 
-@pytest.mark.parametrize("M", [1, 7])
+@pytest.mark.parametrize("M", [1, 7, 100])  # 100: two skinny row chunks
 def test_fp8_qkv_rope_and_argmax(M):
     from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
 
@@ -683,6 +683,8 @@ def test_engine_fp8_weights_decode_matches_dequantized_bf16():
     for lw, l8 in zip(wd.layers, e8.weights.layers):
         for n in ("qkv", "o", "gate_up", "down"):
             setattr(lw, n, getattr(l8, n).dequantize())
+    if isinstance(e8.weights.lm_head, ops.Fp8Weight):  # fp8 mode quantizes the LM head too
+        wd.lm_head = e8.weights.lm_head.dequantize()
     ed = Engine(cfg, weights=wd, device=DEV, kv_pages=64, max_batch=4)
     prompts = [[1, 5, 9, 200, 31], [7, 7, 3]]
     res = []
