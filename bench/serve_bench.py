@@ -7,8 +7,9 @@ batched decode), in-process through EngineServer + the native scheduler.
 so the engine sees requests join and leave the running batch at arbitrary
 steps.  Prints one JSON line: aggregate generated tokens/s, TTFT p50/p99
 (submit -> first token, queueing included), mean batch occupancy.
-Per GPU; run one process per GPU (torchrun) for the 8-GPU number -- each rank
-serves its own peers (replica-per-GPU, dp).
+``--gpus N [--tp T | --ep E]``: the node's multi-GPU path instead (engine.cluster:
+N / (T*E) replicas of one process per GPU, least-loaded routing of the peers'
+Ollama JSON requests), i.e. exactly what a node with ENGINE_GPUS/ENGINE_TP serves.
 """
 import argparse
 import json
@@ -39,7 +40,12 @@ def main():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--mixed", type=int, default=1,
                     help="1: running sequences ride in prefill steps (mixed batches)")
+    ap.add_argument("--gpus", type=int, default=1, help="serve through engine.cluster on N GPUs")
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--ep", type=int, default=1)
     a = ap.parse_args()
+    if a.gpus > 1 or a.tp > 1 or a.ep > 1:
+        return cluster_main(a)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device(a.device, local) if a.device == "cuda" else torch.device(a.device)
     cfg = get_config(a.model)
@@ -82,6 +88,56 @@ def main():
         "ttft_p50_ms": round(statistics.median(ttft), 3),
         "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
         "mean_batch": round(toks / max(steps, 1), 2), "mixed": bool(a.mixed), "dtype": "bf16",
+        "data": "synthetic chat prompts, random-init weights"}), flush=True)
+
+
+def cluster_main(a):
+    """Peers -> Ollama JSON -> ClusterServer router -> replica leaders (no GPU in this
+    process)."""
+    from p2p_llm_chat_go_amd.engine.cluster import ClusterServer
+
+    cs = ClusterServer(a.model, gpus=a.gpus, tp=a.tp, ep=a.ep,
+                       device="cpu" if a.device == "cpu" else "cuda",
+                       max_batch=max(8, a.peers), max_tokens=a.new_tokens)
+
+    def req(p, r):
+        n = a.new_tokens - ((p * 31 + r) * 7919) % (a.jitter + 1)
+        msg = SAMPLE_MESSAGES[p % len(SAMPLE_MESSAGES)]
+        return json.dumps({"model": "llama3.1", "prompt": suggest_prompt(msg), "stream": False,
+                           "options": {"temperature": 0, "num_predict": max(1, n),
+                                       "ignore_eos": True}})
+
+    try:
+        ths = [threading.Thread(target=lambda p=p: cs.handle_json(req(p, -1)))
+               for p in range(a.peers)]  # warm pass
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        results, lock = [], threading.Lock()
+
+        def peer(p):
+            for r in range(a.requests):
+                out = json.loads(cs.handle_json(req(p, r)))
+                with lock:
+                    results.append(out)
+
+        t0 = time.perf_counter()
+        ths = [threading.Thread(target=peer, args=(p,)) for p in range(a.peers)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        el = time.perf_counter() - t0
+        m = cs.metrics()
+    finally:
+        cs.close()
+    toks = sum(r["eval_count"] for r in results)
+    ttft = sorted((r["total_duration"] - r["eval_duration"]) / 1e6 for r in results)
+    print(json.dumps({
+        "metric": "suggest-reply tokens/sec (continuous batching, multi-GPU node)",
+        "value": round(toks / el, 2), "unit": "tokens/s", "model": a.model, "gpus": a.gpus,
+        "tp": a.tp, "ep": a.ep, "replicas": m.get("replicas"), "peers": a.peers,
+        "requests": len(results), "new_tokens": a.new_tokens, "elapsed_s": round(el, 3),
+        "ttft_p50_ms": round(statistics.median(ttft), 3),
+        "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
+        "routed": [r.get("routed") for r in m.get("per_replica", [])], "dtype": "bf16",
         "data": "synthetic chat prompts, random-init weights"}), flush=True)
 
 

@@ -1,36 +1,54 @@
-// One-shot all-reduce over IPC-mapped peer buffers (xGMI) for decode-size
+// One-shot collectives over IPC-mapped peer buffers (xGMI) for decode-size
 // tensor-parallel messages (SURVEY.md §2C "Collective backend", §5 last row,
 // kernel K12).  The reference has no collectives at all; this replaces RCCL's
 // ring for the 2 x L per-token all-reduces of TP decode (16 KiB at B=1 for
-// 70B), where a ring's 2(W-1) latency-bound hops dominate.
+// 70B), where a ring's 2(W-1) latency-bound hops dominate, and for the two
+// small per-step exchanges of vocab-parallel sampling (greedy argmax keys:
+// MAX of u64; sampled decode: all-gather of per-shard top-k candidates).
 //
 // Every rank owns one uncached (MTYPE UC) buffer, hipIpc-exported to the other
 // ranks of the group:
 //   flags : [2 parities][MAX_RANKS src][MAX_BLOCKS] u32   (one 4-byte word each)
 //   data  : [2 parities][MAX_RANKS src][max_bytes]
-// Call k of block b on rank r (seq = per-block counter, parity = seq & 1):
-//   1. push its chunk of `partial` into slot [parity][r] of EVERY rank's buffer
+// Call k (k = the group's call index, identical on every rank and every block:
+// seq = k + 1, parity = seq & 1), block b, rank r:
+//   1. push its slice of the input into slot [parity][r] of EVERY rank's buffer
 //      (xGMI writes; all 7 links of a rank are used at once),
 //   2. fence (system scope), then store seq into flag [parity][r][b] of every rank,
 //   3. spin on its OWN flags [parity][*][b] until all ranks posted seq,
-//   4. h[chunk] += sum over ranks in rank order (bit-identical on every rank).
-// No grid barrier: block b only waits for block b of the peers (same chunk).
-// Parity double-buffering makes slot reuse safe: a rank can only start call
-// k+2 after every peer posted call k+1, i.e. finished reading call k.
-// Every spin is bounded: on timeout the kernel records an error and finishes
-// (wrong numbers, never a hung GPU); the host checks the error word.
+//   4. combine: h += sum in rank order (bit-identical on every rank) | max | gather.
+// No grid barrier: block b only waits for block b of the peers.
+//
+// Slot reuse: a rank starts call k+2 only after its whole call-(k+1) kernel
+// finished, i.e. after it saw a call-(k+1) flag of every peer; a peer posts
+// call k+1 only after its call-k kernel completed (same stream).  So every peer
+// is done reading parity k&1 before anyone rewrites it -- for ANY mapping of
+// data to blocks, because seq is the call index on every block: block 0 keeps
+// the counters of the blocks a small call does not launch in step
+// (counters[nblk..MAX_BLOCKS) = seq), so a later call with more blocks still
+// agrees on seq and parity.
+//
+// Every spin is bounded: on timeout the kernel sets the error word and finishes
+// (wrong numbers, never a hung GPU).  Once the error word is set, later calls
+// skip their waits (a dead peer costs one timeout, not one per call); the host
+// raises on it (LlamaModel.check_faults).
 #include <cstring>
 
 #include "common.h"
 
 namespace {
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // one 16-byte lane payload
+
 constexpr int MAX_RANKS = 8;
 constexpr int MAX_BLOCKS = 64;
 constexpr int NT = 256;
 constexpr size_t FLAG_BYTES = 2ull * MAX_RANKS * MAX_BLOCKS * 4;
-// spin bound in wall-clock ticks (100 MHz constant clock): 5 s; a healthy call waits microseconds
-constexpr long long SPIN_TICKS = 500000000ll;
+// default spin bound in wall-clock ticks (100 MHz constant clock): 5 s; a healthy call
+// waits microseconds (p2p_car_set_timeout_ms overrides, e.g. for fault-injection tests)
+__device__ long long g_spin_ticks = 500000000ll;
+
+enum { OP_ADD_BF16 = 0, OP_MAX_U64 = 1, OP_GATHER = 2 };
 
 struct Peers {
   char* base[MAX_RANKS];  // every rank's buffer, mapped into this process
@@ -40,25 +58,31 @@ __device__ __forceinline__ unsigned* flag_ptr(char* base, int parity, int src, i
   return reinterpret_cast<unsigned*>(base) + ((size_t)parity * MAX_RANKS + src) * MAX_BLOCKS + blk;
 }
 
-__device__ __forceinline__ bf16x8* data_ptr(char* base, size_t max_bytes, int parity, int src) {
-  return reinterpret_cast<bf16x8*>(base + FLAG_BYTES + ((size_t)parity * MAX_RANKS + src) * max_bytes);
+__device__ __forceinline__ v4u* data_ptr(char* base, size_t max_bytes, int parity, int src) {
+  return reinterpret_cast<v4u*>(base + FLAG_BYTES + ((size_t)parity * MAX_RANKS + src) * max_bytes);
 }
 
-__global__ __launch_bounds__(NT) void car_allreduce_add_kernel(
-    Peers peers, int rank, int world, size_t max_bytes, const bf16x8* __restrict__ partial,
-    bf16x8* __restrict__ h, int n_vec, unsigned* __restrict__ counters, int* __restrict__ err) {
+template <int OP>
+__global__ __launch_bounds__(NT) void car_kernel(Peers peers, int rank, int world, size_t max_bytes,
+                                                 const v4u* __restrict__ in, void* __restrict__ out,
+                                                 int n_vec, unsigned* __restrict__ counters,
+                                                 int* __restrict__ err) {
   const int blk = blockIdx.x, nblk = gridDim.x;
   const int per = (n_vec + nblk - 1) / nblk;
   const int v0 = blk * per, v1 = min(n_vec, v0 + per);
   __shared__ unsigned s_seq;
-  if (threadIdx.x == 0) s_seq = counters[blk] + 1;
+  __shared__ int s_failed;
+  if (threadIdx.x == 0) {
+    s_seq = counters[blk] + 1;
+    s_failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   const unsigned seq = s_seq;
   const int parity = seq & 1;
 
-  // 1. push this rank's chunk to every rank (including itself)
+  // 1. push this rank's slice to every rank (including itself)
   for (int i = v0 + threadIdx.x; i < v1; i += NT) {
-    const bf16x8 v = partial[i];
+    const v4u v = in[i];
     for (int p = 0; p < world; ++p) data_ptr(peers.base[p], max_bytes, parity, rank)[i] = v;
   }
   __threadfence_system();
@@ -67,12 +91,13 @@ __global__ __launch_bounds__(NT) void car_allreduce_add_kernel(
   if (threadIdx.x < world)
     __hip_atomic_store(flag_ptr(peers.base[threadIdx.x], parity, rank, blk), seq,
                        __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  // 3. wait for every source rank's block `blk`
-  if (threadIdx.x < world) {
+  // 3. wait for every source rank's block `blk` (skipped once a peer is known dead)
+  if (threadIdx.x < world && !s_failed) {
     unsigned* f = flag_ptr(peers.base[rank], parity, threadIdx.x, blk);
     const long long t0 = wall_clock64();
+    const long long bound = g_spin_ticks;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
-      if (wall_clock64() - t0 > SPIN_TICKS) {
+      if (wall_clock64() - t0 > bound) {
         atomicOr(err, 1);
         break;
       }
@@ -80,23 +105,80 @@ __global__ __launch_bounds__(NT) void car_allreduce_add_kernel(
     }
   }
   __syncthreads();
-  // 4. reduce in fixed rank order
-  for (int i = v0 + threadIdx.x; i < v1; i += NT) {
-    float acc[8];
-    const bf16x8 hv = h[i];
+  // 4. combine
+  if constexpr (OP == OP_ADD_BF16) {
+    bf16x8* h = reinterpret_cast<bf16x8*>(out);
+    for (int i = v0 + threadIdx.x; i < v1; i += NT) {
+      float acc[8];
+      const bf16x8 hv = h[i];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = (float)hv[j];
-    for (int p = 0; p < world; ++p) {
-      const bf16x8 v = __builtin_nontemporal_load(data_ptr(peers.base[rank], max_bytes, parity, p) + i);
+      for (int j = 0; j < 8; ++j) acc[j] = (float)hv[j];
+      for (int p = 0; p < world; ++p) {  // fixed rank order: identical sums on every rank
+        const v4u raw = __builtin_nontemporal_load(data_ptr(peers.base[rank], max_bytes, parity, p) + i);
+        bf16x8 v;
+        memcpy(&v, &raw, 16);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+        for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+      h[i] = o;
     }
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
-    h[i] = o;
+  } else if constexpr (OP == OP_MAX_U64) {
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(out);
+    for (int i = v0 + threadIdx.x; i < v1; i += NT) {
+      unsigned long long a = 0, b = 0;
+      for (int p = 0; p < world; ++p) {
+        const v4u raw = __builtin_nontemporal_load(data_ptr(peers.base[rank], max_bytes, parity, p) + i);
+        const unsigned long long x = ((unsigned long long)raw.y << 32) | raw.x;
+        const unsigned long long y = ((unsigned long long)raw.w << 32) | raw.z;
+        a = x > a ? x : a;
+        b = y > b ? y : b;
+      }
+      o[2 * i] = a;
+      o[2 * i + 1] = b;
+    }
+  } else {  // OP_GATHER: out[p * n_vec + i] = rank p's input[i]
+    v4u* o = reinterpret_cast<v4u*>(out);
+    for (int p = 0; p < world; ++p)
+      for (int i = v0 + threadIdx.x; i < v1; i += NT)
+        o[(size_t)p * n_vec + i] =
+            __builtin_nontemporal_load(data_ptr(peers.base[rank], max_bytes, parity, p) + i);
   }
-  if (threadIdx.x == 0) counters[blk] = seq;
+  if (threadIdx.x == 0) {
+    counters[blk] = seq;
+    if (blk == 0)
+      for (int j = nblk; j < MAX_BLOCKS; ++j) counters[j] = seq;  // keep idle blocks in step
+  }
+}
+
+int launch(int op, void* const* bases, int rank, int world, size_t max_bytes, const void* in,
+           void* out, int n_vec, unsigned* counters, int* err, int blocks, void* stream) {
+  if (world < 1 || world > MAX_RANKS || rank < 0 || rank >= world || n_vec <= 0) return 1;
+  if ((size_t)n_vec * 16 > max_bytes) return 1;
+  Peers peers = {};
+  for (int p = 0; p < world; ++p) peers.base[p] = (char*)bases[p];
+  if (blocks <= 0) blocks = (n_vec + NT * 2 - 1) / (NT * 2);
+  blocks = max(1, min(blocks, MAX_BLOCKS));
+  hipStream_t st = (hipStream_t)stream;
+  switch (op) {
+    case OP_ADD_BF16:
+      hipLaunchKernelGGL(car_kernel<OP_ADD_BF16>, dim3(blocks), dim3(NT), 0, st, peers, rank,
+                         world, max_bytes, (const v4u*)in, out, n_vec, counters, err);
+      break;
+    case OP_MAX_U64:
+      hipLaunchKernelGGL(car_kernel<OP_MAX_U64>, dim3(blocks), dim3(NT), 0, st, peers, rank,
+                         world, max_bytes, (const v4u*)in, out, n_vec, counters, err);
+      break;
+    case OP_GATHER:
+      hipLaunchKernelGGL(car_kernel<OP_GATHER>, dim3(blocks), dim3(NT), 0, st, peers, rank,
+                         world, max_bytes, (const v4u*)in, out, n_vec, counters, err);
+      break;
+    default:
+      return 1;
+  }
+  P2P_CHECK_LAUNCH();
 }
 
 }  // namespace
@@ -130,22 +212,40 @@ P2P_API int p2p_car_close_handle(void* p) { return (int)hipIpcCloseMemHandle(p);
 
 P2P_API int p2p_car_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
 
+// Spin bound of every later call on the current device (ms > 0).
+P2P_API int p2p_car_set_timeout_ms(int ms) {
+  if (ms <= 0) return 1;
+  const long long ticks = (long long)ms * 100000ll;  // 100 MHz constant clock
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_spin_ticks), &ticks, sizeof(ticks));
+}
+
 // h[n] += sum over the group's ranks of partial[n] (bf16, n % 8 == 0,
 // n * 2 <= max_bytes).  bases: world device pointers (this rank's own buffer at
 // index rank).  counters: device u32 [64] (zeroed, private to this rank and
-// buffer); err: device int, set nonzero if a peer never arrived.
+// buffer, shared by every op of the group); err: device int, set nonzero if a
+// peer never arrived.
 P2P_API int p2p_car_allreduce_add(void* const* bases, int rank, int world, size_t max_bytes,
                                   const void* partial, void* h, int n, unsigned* counters,
                                   int* err, int blocks, void* stream) {
-  if (world < 1 || world > MAX_RANKS || rank < 0 || rank >= world) return 1;
-  if (n % 8 || (size_t)n * 2 > max_bytes) return 1;
-  Peers peers = {};
-  for (int p = 0; p < world; ++p) peers.base[p] = (char*)bases[p];
-  const int n_vec = n / 8;
-  if (blocks <= 0) blocks = (n_vec + NT * 2 - 1) / (NT * 2);
-  blocks = max(1, min(blocks, MAX_BLOCKS));
-  hipLaunchKernelGGL(car_allreduce_add_kernel, dim3(blocks), dim3(NT), 0, (hipStream_t)stream,
-                     peers, rank, world, max_bytes, (const bf16x8*)partial, (bf16x8*)h, n_vec,
-                     counters, err);
-  P2P_CHECK_LAUNCH();
+  if (n % 8) return 1;
+  return launch(OP_ADD_BF16, bases, rank, world, max_bytes, partial, h, n / 8, counters, err,
+                blocks, stream);
+}
+
+// keys[n] = max over ranks of keys[n] (u64, n even, in place allowed).
+P2P_API int p2p_car_allreduce_max_u64(void* const* bases, int rank, int world, size_t max_bytes,
+                                      const void* keys_in, void* keys_out, int n,
+                                      unsigned* counters, int* err, int blocks, void* stream) {
+  if (n % 2) return 1;
+  return launch(OP_MAX_U64, bases, rank, world, max_bytes, keys_in, keys_out, n / 2, counters,
+                err, blocks, stream);
+}
+
+// out[world][nbytes] = every rank's in[nbytes] (nbytes % 16 == 0), rank-major.
+P2P_API int p2p_car_all_gather(void* const* bases, int rank, int world, size_t max_bytes,
+                               const void* in, void* out, long long nbytes, unsigned* counters,
+                               int* err, int blocks, void* stream) {
+  if (nbytes % 16) return 1;
+  return launch(OP_GATHER, bases, rank, world, max_bytes, in, out, (int)(nbytes / 16), counters,
+                err, blocks, stream);
 }

@@ -1,0 +1,488 @@
+"""Multi-GPU serving behind one node: data-parallel replicas of tensor/expert-
+parallel engine groups (SURVEY §2C "TP", "EP", "DP / replica serving").
+
+The reference serves one suggestion per click from a single Ollama process
+(`web/streamlit_app.py:89-101`, reached from the node API of
+`go/cmd/node/main.go:213-283`).  On an 8 x MI355X box this node instead runs
+
+    node process (HTTP, libp2p, router; never touches a GPU)
+      |-- replica 0: leader rank (scheduler + EngineServer) --pipes--> follower ranks
+      |-- replica 1: ...
+      ...
+
+with ``ENGINE_GPUS`` GPUs split into ``ENGINE_GPUS / (ENGINE_TP * ENGINE_EP)``
+replicas.  Every rank is its own process pinned to one GPU (one process per
+GPU; RCCL over xGMI plus the one-shot IPC collectives inside each group).
+
+* **TP/EP lockstep.**  Only the group leader runs the continuous-batching
+  scheduler.  Each engine-level call it makes (a prefill batch, a chunk of k
+  decode steps) is first sent to its followers over a host pipe as a small
+  plan (prompt ids, block tables, positions, sampling params, k), then executed
+  locally; the followers execute the same call, so every rank replays the same
+  hipGraphs and their collectives line up.  Results (tokens) are identical on
+  every rank -- greedy keys are MAX-reduced, sampled draws are keyed by
+  (seed, position, token) -- so the leader uses its own.
+* **DP router.**  The node process sends each request to the live replica with
+  the fewest outstanding requests (least-loaded) and relays streamed chunks.
+* **Failures are loud.**  A rank that dies breaks its group's collectives: the
+  leader's next call raises (``CollectiveTimeout`` / transport error), the
+  leader reports ``dead`` and exits non-zero, its in-flight requests fail with
+  an error reply, and the router stops sending it work.  A follower whose pipe
+  closes (leader gone) exits non-zero.
+
+The worker processes are started with the ``spawn`` method before anything
+in the node process initialises the GPU (only ``torch.cuda.device_count()`` is
+consulted), so no process that touched the GPU ever forks or execs.
+"""
+from __future__ import annotations
+
+import itertools
+import json
+import os
+import socket
+import threading
+import time
+import traceback
+from concurrent.futures import Future
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+# ------------------------------------------------------------------ rank side
+class LockstepEngine:
+    """The leader's view of its engine group: every call that runs collectives is
+    broadcast to the followers first (plan over the host pipes), then run locally.
+    Everything else (cfg, kv, limits) is the local engine's."""
+
+    def __init__(self, engine, follower_conns):
+        self._eng = engine
+        self._conns = list(follower_conns)
+        self._lock = threading.Lock()
+
+    def __getattr__(self, name):
+        return getattr(self._eng, name)
+
+    def _bcast(self, msg):
+        for c in self._conns:
+            c.send(msg)
+
+    @staticmethod
+    def _resolve(params):
+        # a request without a seed draws one lazily; draw it HERE so every rank samples
+        # with the same key (ranks that drew different tokens would corrupt each other's KV)
+        for p in params or ():
+            if p is not None and not p.greedy:
+                p.resolved_seed()
+
+    def prefill(self, prompts, block_tables, return_logits=False, sampling=None, starts=None):
+        self._resolve(sampling)
+        with self._lock:
+            self._bcast(("prefill", prompts, block_tables, return_logits, sampling, starts))
+            return self._eng.prefill(prompts, block_tables, return_logits=return_logits,
+                                     sampling=sampling, starts=starts)
+
+    def decode_steps(self, last_ids, pos, block_tables, ctx, k, params=None):
+        self._resolve(params)
+        with self._lock:
+            self._bcast(("decode", last_ids, pos, block_tables, ctx, k, params))
+            return self._eng.decode_steps(last_ids, pos, block_tables, ctx, k, params)
+
+    def generate(self, prompts, max_new_tokens=64, stop_on_eos=True, check_every=8):
+        with self._lock:
+            self._bcast(("generate", prompts, max_new_tokens, stop_on_eos, check_every))
+            return self._eng.generate(prompts, max_new_tokens, stop_on_eos, check_every)
+
+    def stop(self):
+        for c in self._conns:
+            try:
+                c.send(("stop",))
+            except (OSError, EOFError):
+                pass
+
+
+def _follower_loop(eng, conn):
+    while True:
+        try:
+            msg = conn.recv()
+        except (EOFError, OSError):
+            os._exit(2)  # leader gone: this group is over
+        op = msg[0]
+        if op == "stop":
+            return
+        if op == "prefill":
+            _, prompts, bts, ret, sampling, starts = msg
+            eng.prefill(prompts, bts, return_logits=ret, sampling=sampling, starts=starts)
+        elif op == "decode":
+            _, ids, pos, bts, ctx, k, params = msg
+            eng.decode_steps(ids, pos, bts, ctx, k, params)
+        elif op == "generate":
+            _, prompts, n, eos, every = msg
+            eng.generate(prompts, n, eos, every)
+        if eng.device.type == "cuda":
+            import torch
+
+            torch.cuda.synchronize(eng.device)
+
+
+def build_rank_engine(spec: dict, rank: int, device: str):
+    """Engine of one rank of a replica group (also used by tests)."""
+    from ..engine import Engine
+    from ..models.config import get_config
+    from ..models.weights import EngineWeights
+    from ..parallel.comm import TPComm
+
+    cfg = get_config(spec["model"])
+    tp, ep = spec.get("tp", 1), spec.get("ep", 1)
+    par = dict(tp_rank=rank, tp_size=tp) if tp > 1 else {}
+    if ep > 1:
+        par = dict(ep_rank=rank, ep_size=ep, ep_mode="allreduce")
+    weights = None
+    if spec.get("sd_seed") is not None:  # sharding-invariant random init (tests, parity)
+        from ..models.reference import random_state_dict
+
+        sd = random_state_dict(cfg, seed=int(spec["sd_seed"]))
+        weights = EngineWeights.from_state_dict(sd, cfg, device, **{
+            k: v for k, v in par.items() if k != "ep_mode"})
+    comm = TPComm() if tp * ep > 1 else None
+    cuda = device.startswith("cuda")
+    return Engine(cfg, weights=weights, device=device, seed=spec.get("seed", 0),
+                  kv_pages=spec.get("kv_pages") or (None if cuda else 256),
+                  max_batch=spec.get("max_batch", 16), comm=comm,
+                  weight_dtype=spec.get("weights"), **par)
+
+
+def _rank_main(spec, replica, rank, device, port, parent_conn, follower_conns, leader_conn):
+    """Entry of one rank process (spawned)."""
+    try:
+        group = spec.get("tp", 1) * spec.get("ep", 1)
+        import torch
+
+        if device.startswith("cuda"):
+            torch.cuda.set_device(torch.device(device))
+        else:
+            torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(1, spec["world"])))
+        if group > 1:
+            import datetime
+
+            import torch.distributed as dist
+
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            backend = "nccl" if device.startswith("cuda") else "gloo"
+            kw = {"device_id": torch.device(device)} if backend == "nccl" else {}
+            dist.init_process_group(backend, rank=rank, world_size=group,
+                                    timeout=datetime.timedelta(seconds=spec.get("pg_timeout", 600)),
+                                    **kw)
+        eng = build_rank_engine(spec, rank, device)
+        if device.startswith("cuda") and spec.get("warmup", True):
+            mb = spec.get("max_batch", 16)
+            eng.warmup(tuple(b for b in (1, 2, 4, 8, 16) if b <= mb), ctx=256)
+        if rank != 0:
+            leader_conn.send(("ready", rank))
+            _follower_loop(eng, leader_conn)
+            os._exit(0)
+        for c in follower_conns:  # every follower built its engine
+            msg = c.recv()
+            if msg[0] != "ready":
+                raise RuntimeError("follower failed: %r" % (msg,))
+        _leader_main(spec, replica, eng, parent_conn, follower_conns)
+    except BaseException:
+        tb = traceback.format_exc()
+        try:
+            (parent_conn or leader_conn).send(("dead", tb))
+        except Exception:
+            pass
+        print(tb, flush=True)
+        os._exit(1)
+
+
+def _leader_main(spec, replica, eng, parent_conn, follower_conns):
+    from .server import EngineServer
+    from .tokenizer import get_tokenizer
+
+    group = spec.get("tp", 1) * spec.get("ep", 1)
+    front = LockstepEngine(eng, follower_conns) if group > 1 else eng
+    server = EngineServer(front, get_tokenizer(eng.cfg, spec.get("tokenizer")),
+                          model_name=spec.get("model_name", "llama3.1"),
+                          default_max_tokens=spec.get("max_tokens", 128))
+    send_lock = threading.Lock()
+    cancelled = set()
+
+    def send(msg):
+        with send_lock:
+            parent_conn.send(msg)
+
+    def run(kind, rid, text):
+        try:
+            if kind == "gen":
+                out = server.handle_json(text)
+            elif kind == "metrics":
+                out = json.dumps(dict(server.metrics(), replica=replica, errors=server.errors))
+            else:
+                def emit(chunk):
+                    if rid in cancelled:
+                        return False
+                    send(("chunk", rid, chunk))
+                    return True
+
+                out = server.handle_json_stream(text, emit)
+            send(("done", rid, out))
+        except BaseException as e:  # noqa: BLE001 -- every failure becomes an error reply
+            send(("err", rid, "%s: %s" % (type(e).__name__, e)))
+        finally:
+            cancelled.discard(rid)
+
+    send(("ready", replica))
+
+    def watchdog():  # a fatal engine error ends the replica loudly
+        while server.dead is None:
+            time.sleep(0.1)
+        send(("dead", "replica %d: %s" % (replica, server.dead)))
+        time.sleep(0.5)
+        os._exit(3)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    while True:
+        try:
+            msg = parent_conn.recv()
+        except (EOFError, OSError):
+            break
+        op = msg[0]
+        if op == "stop":
+            break
+        if op == "cancel":
+            cancelled.add(msg[1])
+            continue
+        threading.Thread(target=run, args=(op, msg[1], msg[2]), daemon=True).start()
+    server.close()
+    if group > 1:
+        front.stop()
+    os._exit(0)
+
+
+# ------------------------------------------------------------------ node side
+class _Replica:
+    def __init__(self, idx, conn, procs):
+        self.idx = idx
+        self.conn = conn
+        self.procs = procs
+        self.outstanding = 0
+        self.served = 0
+        self.alive = True
+        self.error = None
+        self.lock = threading.Lock()
+
+
+class ClusterServer:
+    """DP router over replica groups; the node's generate hooks (same interface as
+    EngineServer: handle_json / handle_json_stream / metrics / close)."""
+
+    def __init__(self, model: str, gpus: int = 1, tp: int = 1, ep: int = 1, device: str = "cuda",
+                 max_batch: int = 16, max_tokens: int = 128, model_name: str = "llama3.1",
+                 weights: str | None = None, tokenizer: str | None = None, sd_seed=None,
+                 kv_pages=None, warmup: bool = True, start_timeout: float = 1800.0,
+                 first_gpu: int = 0):
+        import multiprocessing as mp
+
+        group = tp * ep
+        if gpus % group:
+            raise ValueError("ENGINE_GPUS=%d is not a multiple of TP*EP=%d" % (gpus, group))
+        self.n_replicas = gpus // group
+        self.group = group
+        spec = dict(model=model, tp=tp, ep=ep, max_batch=max_batch, max_tokens=max_tokens,
+                    model_name=model_name, weights=weights, tokenizer=tokenizer, sd_seed=sd_seed,
+                    kv_pages=kv_pages, warmup=warmup, world=gpus)
+        ctx = mp.get_context("spawn")
+        self._replicas = []
+        self._rid = itertools.count(1)
+        self._waiters = {}  # rid -> (future, emit)
+        self._wlock = threading.Lock()
+        self._closed = False
+        for r in range(self.n_replicas):
+            parent_end, leader_end = ctx.Pipe()
+            pipes = [ctx.Pipe() for _ in range(group - 1)]
+            port = _free_port()
+            procs = []
+            for k in range(group):
+                dev = "cuda:%d" % (first_gpu + r * group + k) if device == "cuda" else "cpu"
+                if k == 0:
+                    args = (spec, r, 0, dev, port, leader_end, [p[0] for p in pipes], None)
+                else:
+                    args = (spec, r, k, dev, port, None, [], pipes[k - 1][1])
+                p = ctx.Process(target=_rank_main, args=args, daemon=True,
+                                name="engine-r%d-k%d" % (r, k))
+                p.start()
+                procs.append(p)
+            self._replicas.append(_Replica(r, parent_end, procs))
+        deadline = time.time() + start_timeout
+        for rep in self._replicas:
+            while not rep.conn.poll(1.0):
+                if time.time() > deadline or not all(p.is_alive() for p in rep.procs):
+                    self.close()
+                    raise RuntimeError("engine replica %d failed to start" % rep.idx)
+            msg = rep.conn.recv()
+            if msg[0] != "ready":
+                self.close()
+                raise RuntimeError("engine replica %d failed to start:\n%s" % (rep.idx, msg[1]))
+        for rep in self._replicas:
+            threading.Thread(target=self._reader, args=(rep,), daemon=True,
+                             name="replica-%d-reader" % rep.idx).start()
+
+    # ------------------------------------------------------------ plumbing
+    def _reader(self, rep: _Replica):
+        while True:
+            try:
+                msg = rep.conn.recv()
+            except (EOFError, OSError):
+                msg = ("dead", "replica %d exited" % rep.idx)
+            op = msg[0]
+            if op == "dead":
+                self._mark_dead(rep, msg[1])
+                return
+            rid = msg[1]
+            with self._wlock:
+                w = self._waiters.get(rid)
+            if w is None:
+                continue
+            fut, emit = w
+            if op == "chunk":
+                ok = False
+                try:
+                    ok = bool(emit(msg[2])) if emit else True
+                except Exception:
+                    ok = False
+                if not ok:
+                    self._send(rep, ("cancel", rid))
+                continue
+            with self._wlock:
+                self._waiters.pop(rid, None)
+            with rep.lock:
+                rep.outstanding -= 1
+                rep.served += 1
+            if op == "done":
+                fut.set_result(msg[2])
+            else:
+                fut.set_exception(RuntimeError(msg[2]))
+
+    def _mark_dead(self, rep: _Replica, why: str):
+        with rep.lock:
+            rep.alive = False
+            rep.error = why
+        with self._wlock:  # fail what this replica still owed
+            for rid, (fut, _emit) in list(self._waiters.items()):
+                if getattr(fut, "_replica", None) == rep.idx:
+                    self._waiters.pop(rid, None)
+                    if not fut.done():
+                        fut.set_exception(RuntimeError("engine replica %d died: %s"
+                                                       % (rep.idx, why.strip().splitlines()[-1]
+                                                          if why.strip() else why)))
+
+    def _send(self, rep, msg):
+        try:
+            with rep.lock:
+                rep.conn.send(msg)
+        except (OSError, EOFError, ValueError) as e:
+            self._mark_dead(rep, "send failed: %s" % e)
+            raise
+
+    def _pick(self) -> _Replica:
+        live = [r for r in self._replicas if r.alive]
+        if not live:
+            errs = "; ".join("%d: %s" % (r.idx, (r.error or "").strip().splitlines()[-1:])
+                             for r in self._replicas)
+            raise RuntimeError("no live engine replica (%s)" % errs)
+        return min(live, key=lambda r: (r.outstanding, r.idx))
+
+    def _call(self, kind, text, emit=None, timeout=600.0):
+        rep = self._pick()
+        rid = next(self._rid)
+        fut = Future()
+        fut._replica = rep.idx
+        with self._wlock:
+            self._waiters[rid] = (fut, emit)
+        with rep.lock:
+            rep.outstanding += 1
+        self._send(rep, (kind, rid, text))
+        return fut.result(timeout)
+
+    # ------------------------------------------------------------- hooks
+    def handle_json(self, req_text: str) -> str:
+        req = json.loads(req_text)
+        if req.get("endpoint") == "metrics":
+            return json.dumps(self.metrics())
+        return self._call("gen", req_text)
+
+    def handle_json_stream(self, req_text: str, emit) -> str:
+        return self._call("stream", req_text, emit=emit)
+
+    def metrics(self) -> dict:
+        per = []
+        tot = {}
+        for rep in self._replicas:
+            if not rep.alive:
+                per.append({"replica": rep.idx, "alive": False})
+                continue
+            try:
+                rid = next(self._rid)
+                fut = Future()
+                fut._replica = rep.idx
+                with self._wlock:
+                    self._waiters[rid] = (fut, None)
+                with rep.lock:
+                    rep.outstanding += 1
+                self._send(rep, ("metrics", rid, ""))
+                m = json.loads(fut.result(30))
+            except Exception as e:  # noqa: BLE001
+                per.append({"replica": rep.idx, "alive": rep.alive, "error": str(e)})
+                continue
+            m["alive"] = True
+            m["routed"] = rep.served
+            per.append(m)
+            for k, v in m.items():
+                if isinstance(v, (int, float)) and not isinstance(v, bool) and k != "replica":
+                    tot[k] = tot.get(k, 0) + v
+        tot["replicas"] = self.n_replicas
+        tot["live_replicas"] = sum(1 for r in self._replicas if r.alive)
+        tot["group_size"] = self.group
+        tot["per_replica"] = per
+        return tot
+
+    def close(self):
+        if self._closed:
+            return
+        self._closed = True
+        for rep in self._replicas:
+            try:
+                rep.conn.send(("stop",))
+            except Exception:
+                pass
+        for rep in self._replicas:
+            for p in rep.procs:
+                p.join(timeout=30)
+                if p.is_alive():
+                    p.terminate()
+
+
+def from_env(device: str | None = None):
+    """ClusterServer from the node's ENGINE_* environment (net.node)."""
+    gpus = int(os.environ.get("ENGINE_GPUS", "1"))
+    tp = int(os.environ.get("ENGINE_TP", "1"))
+    ep = int(os.environ.get("ENGINE_EP", "1"))
+    dev = device or os.environ.get("ENGINE_DEVICE") or "cuda"
+    dev = "cpu" if dev.startswith("cpu") else "cuda"
+    model = os.environ.get("ENGINE_MODEL") or ("llama3.1-8b" if dev == "cuda" else "tiny-llama")
+    seed = os.environ.get("ENGINE_SD_SEED")
+    return ClusterServer(model, gpus=gpus, tp=tp, ep=ep, device=dev,
+                         max_batch=int(os.environ.get("ENGINE_MAX_BATCH", "16")),
+                         max_tokens=int(os.environ.get("ENGINE_MAX_TOKENS", "128")),
+                         model_name=os.environ.get("LLM_MODEL", "llama3.1"),
+                         weights=os.environ.get("ENGINE_WEIGHTS") or None,
+                         tokenizer=os.environ.get("TOKENIZER_PATH") or None,
+                         sd_seed=int(seed) if seed else None,
+                         warmup=os.environ.get("ENGINE_WARMUP", "1") != "0",
+                         first_gpu=int(os.environ.get("ENGINE_FIRST_GPU", "0")))

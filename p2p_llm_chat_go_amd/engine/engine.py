@@ -62,13 +62,19 @@ class Engine:
                  ep_size: int = 1, ep_mode: str = "allreduce", weight_dtype: str | None = None):
         self.cfg = cfg
         self.device = torch.device(device)
-        if weights is None:
+        own = weights is None
+        if own:
             weights = EngineWeights.random(cfg, self.device, seed=seed, tp_rank=tp_rank,
                                            tp_size=tp_size, ep_rank=ep_rank, ep_size=ep_size)
         # weight_dtype "fp8": weight-only e4m3 dense projections (EngineWeights.quantize_fp8)
         self.weight_dtype = weight_dtype or os.environ.get("ENGINE_WEIGHTS", "bf16")
         if self.weight_dtype == "fp8":
-            weights.quantize_fp8()
+            # a caller's store stays bf16 (it may back a reference engine); ours is swapped
+            weights = (weights if own else weights.shallow_copy()).quantize_fp8()
+            if self.device.type == "cuda":
+                # the bf16 originals and the quantizer's fp32 temporaries stay reserved in
+                # torch's caching allocator; release them before sizing the KV pool
+                torch.cuda.empty_cache()
         elif self.weight_dtype != "bf16":
             raise ValueError("weight_dtype must be bf16 or fp8, got %r" % self.weight_dtype)
         self.weights = weights
@@ -128,6 +134,12 @@ class Engine:
             self.autotune(tuple(bucket(b, BATCH_BUCKETS) for b in batch_sizes) + (64,))
         for b in batch_sizes:
             self.decode_graph(b, ctx)
+
+    def check_comm(self):
+        """Raise if a TP/EP collective timed out (a peer rank is dead or hung)."""
+        comm = self.model.comm
+        if comm is not None and hasattr(comm, "check"):
+            comm.check()
 
     # -------------------------------------------------------------- prefill
     def prefill(self, prompts: list, block_tables: list, return_logits: bool = False,
@@ -204,6 +216,26 @@ class Engine:
                 all_logits.index_copy_(0, sel, res)
         return (first, all_logits) if return_logits else first
 
+    # --------------------------------------------------------------- decode
+    def decode_steps(self, last_ids: list, pos: list, block_tables: list, ctx: int, k: int,
+                     params: list | None = None) -> list:
+        """k decode steps for running sequences (continuous batching): row b continues
+        from token ``last_ids[b]`` at position ``pos[b]`` in its pages; ``params`` =
+        per-row SamplingParams (None / all greedy: the fused-argmax graph).  Returns the
+        k new tokens of every row (host lists).  Every TP/EP rank makes the same call
+        (engine.cluster broadcasts it), so the graphs' collectives line up."""
+        greedy = params is None or all(p.greedy for p in params)
+        g = self.decode_graph(len(last_ids), ctx, greedy=greedy)
+        st = g.state
+        st.load(last_ids, pos, block_tables)
+        if greedy:
+            g.replay(k)
+        else:
+            g.step_sampled(params, k)
+        hist = st.hist[:len(last_ids), :k].cpu().tolist()
+        self.model.check_faults(st.ws)
+        return hist
+
     # ------------------------------------------------------------- generate
     def generate(self, prompts: list, max_new_tokens: int = 64, stop_on_eos: bool = True,
                  check_every: int = 8) -> list:
@@ -217,6 +249,7 @@ class Engine:
             with span("prefill", batch=B, tokens=sum(len(p) for p in prompts)):
                 first = self.prefill(prompts, pages)
                 first_h = first.cpu()  # sync: first token is on the host -> TTFT
+            self.check_comm()
             t1 = time.perf_counter_ns()
             out = [[int(first_h[b])] for b in range(B)]
             done = [stop_on_eos and out[b][0] in self.cfg.eos_ids for b in range(B)]

@@ -135,8 +135,14 @@ class DecodeGraph:
             with torch.cuda.graph(g):
                 self._body()
         except Exception as e:  # e.g. a collective backend that cannot be captured
+            import os
             import warnings
 
+            if st.model.tp > 1 and os.environ.get("P2P_ALLOW_EAGER", "0") != "1":
+                # a TP group must not silently lose its graphs (eager TP decode is several
+                # times slower); P2P_ALLOW_EAGER=1 accepts it
+                raise RuntimeError("TP decode graph capture failed: %s (set P2P_ALLOW_EAGER=1 to "
+                                   "run the step eagerly)" % e) from e
             warnings.warn("decode graph capture failed (%s); running the step eagerly" % e)
             torch.cuda.synchronize(st.model.device)
             st.reset_dummy()

@@ -44,8 +44,10 @@ class SamplingParams:
         n = int(o.get("num_predict", default_max))
         if n < 0:
             n = default_max
+        # ignore_eos (llama.cpp server option; benchmarks): decode exactly num_predict tokens
         return cls(temperature=float(o.get("temperature", 0.0)), top_k=int(o.get("top_k", 40)),
-                   top_p=float(o.get("top_p", 0.9)), seed=o.get("seed"), max_tokens=max(1, n))
+                   top_p=float(o.get("top_p", 0.9)), seed=o.get("seed"), max_tokens=max(1, n),
+                   stop_on_eos=not bool(o.get("ignore_eos", False)))
 
 
 class SamplerSlots:

@@ -56,16 +56,41 @@ class EngineServer:
         self._pending = []   # (prompt_ids, params, future, t_submit) waiting to enter the scheduler
         self._cancels = set()  # futures whose requests should stop
         self._stop = False
+        self._dead = None
+        self.errors = 0
         self.stats = {"requests": 0, "tokens": 0, "prefill_tokens": 0, "decode_steps": 0,
                       "busy_s": 0.0}
         self._thread = threading.Thread(target=self._loop, name="engine-loop", daemon=True)
         self._thread.start()
 
     # --------------------------------------------------------------- API
+    @staticmethod
+    def fatal(e: BaseException) -> bool:
+        """Errors after which this engine cannot serve again: a TP/EP peer rank is dead
+        (one-shot collective timeout, or the process group's transport broke)."""
+        from ..parallel.custom_ar import CollectiveTimeout
+
+        if isinstance(e, CollectiveTimeout):
+            return True
+        dbe = getattr(torch.distributed, "DistBackendError", None)
+        if dbe is not None and isinstance(e, dbe):
+            return True
+        msg = str(e)
+        return any(s in msg for s in ("Connection closed by peer", "Connection reset by peer",
+                                      "Broken pipe", "peer rank is dead"))
+
+    @property
+    def dead(self):
+        """The fatal error that stopped this server (None while healthy)."""
+        return self._dead
+
     def submit(self, prompt_ids: list, params: SamplingParams, on_tokens=None) -> Future:
         """Queue a request.  on_tokens(list[int]) is called from the engine thread with
         every batch of newly generated tokens (streaming), before the future resolves."""
         fut = Future()
+        if self._dead is not None:
+            fut.set_exception(RuntimeError("engine replica is down: %s" % self._dead))
+            return fut
         with self._lock:
             self._pending.append((list(prompt_ids), params, fut, time.perf_counter_ns(),
                                   on_tokens))
@@ -235,9 +260,20 @@ class EngineServer:
                     if not r["future"].done():
                         r["future"].set_exception(e)
                     self.sched.cancel(rid)
-                self.sched.take_finished()
+                for rid in self.sched.take_finished():
+                    self.sched.release(rid)  # scheduler entries + KV pages
                 self._reqs.clear()
+                self.errors += 1
+                if self.fatal(e):  # a TP peer is gone: this replica cannot serve again
+                    self._dead = e
+                    break
             self.stats["busy_s"] += time.perf_counter() - t_busy
+        if self._dead is not None:  # nothing queued may wait forever on a dead replica
+            with self._lock:
+                pend, self._pending = self._pending, []
+            for _p, _params, fut, _t, _cb in pend:
+                if not fut.done():
+                    fut.set_exception(RuntimeError("engine replica is down: %s" % self._dead))
 
     def _apply_cancels(self):
         with self._lock:
@@ -272,6 +308,7 @@ class EngineServer:
             with span("server.prefill", batch=len(plan.prefill), decode_rows=len(ride)):
                 first = eng.prefill(prompts, pages, sampling=[self._reqs[i]["params"] for i in ids],
                                     starts=starts if ride else None).cpu().tolist()
+            eng.check_comm()
             t1 = time.perf_counter_ns()
             self.stats["prefill_tokens"] += sum(len(self._reqs[i]["prompt"]) for i in plan.prefill)
             for i, tkn in zip(plan.prefill, first):
@@ -290,21 +327,13 @@ class EngineServer:
     def _decode(self, eng: Engine, running: list):
         reqs = [self.sched.get(i) for i in running]
         params = [self._reqs[i]["params"] for i in running]
-        greedy = all(p.greedy for p in params)
         ctx = max(r.prompt_len + r.max_new for r in reqs)
-        g = eng.decode_graph(len(running), ctx, greedy=greedy)
-        st = g.state
-        st.load([r.tokens[-1] for r in reqs], [r.pos for r in reqs], [list(r.pages) for r in reqs])
         remaining = min(r.max_new - len(r.tokens) for r in reqs)
         waiting = self.sched.n_waiting + len(self._pending)
         k = max(1, min(self.decode_chunk if not waiting else 2, remaining))
         with span("server.decode", batch=len(running), steps=k):
-            if greedy:
-                g.replay(k)
-            else:
-                g.step_sampled(params, k)
-        hist = st.hist[:len(running), :k].cpu().tolist()
-        eng.model.check_faults(st.ws)
+            hist = eng.decode_steps([r.tokens[-1] for r in reqs], [r.pos for r in reqs],
+                                    [list(r.pages) for r in reqs], ctx, k, params)
         self.stats["decode_steps"] += k
         self.sched.on_decode_tokens(running, hist)
         self._stream(running)

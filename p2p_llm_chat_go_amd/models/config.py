@@ -79,7 +79,17 @@ TINY_MIXTRAL = ModelConfig("tiny-mixtral", hidden=256, n_layers=2, n_heads=2, n_
                            ffn=256, vocab=512, max_pos=4096, rope_theta=1e6, rope_llama3=None,
                            n_experts=4, top_k=2, bos_id=1, eos_ids=(2,))
 
-PRESETS = {c.name: c for c in (LLAMA31_8B, LLAMA31_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL)}
+# CPU config with the 8B/70B head structure at 8 ranks (8 kv heads -> one per TP rank,
+# 4 query heads per kv head) and 8 experts (Mixtral EP=8: one expert per rank).
+TINY_LLAMA_GQA = ModelConfig("tiny-llama-gqa", hidden=256, n_layers=2, n_heads=32, n_kv_heads=8,
+                             ffn=1024, vocab=1024, max_pos=4096, rope_theta=10000.0,
+                             rope_llama3=None, bos_id=1, eos_ids=(2,))
+TINY_MIXTRAL_8E = ModelConfig("tiny-mixtral-8e", hidden=256, n_layers=2, n_heads=8, n_kv_heads=8,
+                              ffn=256, vocab=512, max_pos=4096, rope_theta=1e6, rope_llama3=None,
+                              n_experts=8, top_k=2, bos_id=1, eos_ids=(2,))
+
+PRESETS = {c.name: c for c in (LLAMA31_8B, LLAMA31_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL,
+                               TINY_LLAMA_GQA, TINY_MIXTRAL_8E)}
 ALIASES = {"llama3.1": "llama3.1-8b", "llama3.1:8b": "llama3.1-8b", "llama3.1:70b": "llama3.1-70b",
            "mixtral": "mixtral-8x7b", "mixtral:8x7b": "mixtral-8x7b", "tiny": "tiny-llama"}
 

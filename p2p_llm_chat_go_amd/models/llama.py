@@ -186,11 +186,14 @@ class LlamaModel:
         return logits
 
     def check_faults(self, ws: Workspace):
-        """Raise if a fused kernel's bounded cross-workgroup wait timed out (its results
-        would be wrong); costs one small device read, call where the host syncs anyway."""
+        """Raise if a bounded wait timed out -- a fused kernel's cross-workgroup hand-off or
+        a one-shot TP collective whose peer never arrived (the tokens would be wrong);
+        costs one small device read, call where the host syncs anyway."""
         if self.device.type == "cuda" and int(ws.err.item()) != 0:
             ws.err.zero_()
             raise RuntimeError("fused attention/o_proj hand-off timed out (results invalid)")
+        if self.comm is not None and hasattr(self.comm, "check"):
+            self.comm.check()
 
     def finalize_greedy(self, ws: Workspace, n: int, out=None):
         """keys -> token ids (TP: all-reduce MAX of the keys across vocab shards first)."""

@@ -72,6 +72,11 @@ class EngineWeights:
                     n += nb(t)
         return n
 
+    def shallow_copy(self) -> "EngineWeights":
+        """New weight store sharing every tensor, with its own layer objects (so swapping a
+        projection -- e.g. quantize_fp8 -- does not touch the caller's store)."""
+        return dataclasses.replace(self, layers=[dataclasses.replace(lw) for lw in self.layers])
+
     def quantize_fp8(self, names=("qkv", "o", "gate_up", "down"), lm_head=True) -> "EngineWeights":
         """Weight-only FP8 (e4m3, per-output-channel scale) for the dense projections and
         the LM head, in place: the decode weight stream -- the roofline of batch-1 decode --

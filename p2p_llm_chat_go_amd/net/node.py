@@ -15,6 +15,11 @@ STRICT_SENDER, UI_FILE) and the engine knobs:
   ENGINE_MAX_TOKENS  default num_predict (default 128)
   ENGINE_WARMUP   1 (default on GPUs): autotune GEMMs + capture decode graphs at start
   TOKENIZER_PATH  tokenizer.json (default: synthetic offline tokenizer)
+  ENGINE_GPUS     GPUs to serve on (default 1): ENGINE_GPUS / (ENGINE_TP * ENGINE_EP)
+                  data-parallel replicas, least-loaded routing (engine.cluster)
+  ENGINE_TP       tensor-parallel ranks per replica (default 1; 8 for 70B over xGMI)
+  ENGINE_EP       expert-parallel ranks per replica (MoE models, default 1)
+  ENGINE_WEIGHTS  bf16 (default) / fp8 (weight-only e4m3 projections)
 
 The libp2p host, HTTP API and Directory client are the C++ ``Node``; this
 process only adds the GPU engine behind the node's /api/generate, /api/chat
@@ -29,6 +34,16 @@ import threading
 
 
 def build_engine_server(model: str | None = None, device: str | None = None):
+    gpus = int(os.environ.get("ENGINE_GPUS", "1"))
+    tp = int(os.environ.get("ENGINE_TP", "1"))
+    ep = int(os.environ.get("ENGINE_EP", "1"))
+    if gpus > 1 or tp > 1 or ep > 1 or os.environ.get("ENGINE_CLUSTER", "0") == "1":
+        # one process per GPU, started before this process touches any GPU
+        from ..engine import cluster
+
+        if model:
+            os.environ["ENGINE_MODEL"] = model
+        return cluster.from_env(device)
     import torch
 
     from ..engine import Engine
@@ -72,6 +87,8 @@ FLAGS = [
     ("--engine-checkpoint", "ENGINE_CHECKPOINT"), ("--engine-max-batch", "ENGINE_MAX_BATCH"),
     ("--engine-max-tokens", "ENGINE_MAX_TOKENS"), ("--tokenizer", "TOKENIZER_PATH"),
     ("--engine-url", "ENGINE_URL"), ("--security", "SECURITY"), ("--nat-pmp", "NAT_PMP"), ("--upnp", "UPNP"),
+    ("--engine-gpus", "ENGINE_GPUS"), ("--engine-tp", "ENGINE_TP"), ("--engine-ep", "ENGINE_EP"),
+    ("--engine-weights", "ENGINE_WEIGHTS"),
 ]
 
 

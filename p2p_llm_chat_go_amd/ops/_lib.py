@@ -46,6 +46,11 @@ _SIGS = {
     "p2p_car_handle_size": [],
     "p2p_car_allreduce_add": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p, c_int,
                               c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_car_allreduce_max_u64": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p,
+                                  c_int, c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_car_all_gather": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p,
+                           ctypes.c_longlong, c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_car_set_timeout_ms": [c_int],
     "p2p_attn_oproj": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                        c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_void_p,
                        c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p],

@@ -71,6 +71,9 @@ class TPComm:
 
     def allreduce_max_u64_(self, keys: torch.Tensor):
         """MAX all-reduce of unsigned 64-bit argmax keys stored in int64."""
+        if (self.car is not None and keys.device.type == "cuda" and keys.is_contiguous()
+                and self.car.fits_bytes(keys.numel() * 8) and keys.numel() % 2 == 0):
+            return self.car.allreduce_max_u64_(keys)  # one-shot, graph-capturable
         keys.bitwise_xor_(_SIGN)  # unsigned order -> signed order
         dist.all_reduce(keys, op=dist.ReduceOp.MAX, group=self.group)
         keys.bitwise_xor_(_SIGN)
@@ -102,6 +105,25 @@ class TPComm:
             a.copy_(ah)
             return out
         dist.all_to_all_single(a, b, group=self.group)
+        return out
+
+    def check(self):
+        """Raise if a one-shot collective timed out waiting for a peer."""
+        if self.car is not None:
+            self.car.check()
+
+    def all_gather_rows_into(self, out: torch.Tensor, t: torch.Tensor):
+        """out [world * n, ...] = every rank's t [n, ...] (rank-major); one-shot on GPUs."""
+        if (self.car is not None and t.device.type == "cuda" and t.is_contiguous()
+                and self.car.fits_bytes(t.numel() * t.element_size())):
+            return self.car.all_gather_(out, t)
+        if t.device.type == "cuda" and self.backend != "nccl":  # gloo: host copies
+            parts = [torch.empty_like(t, device="cpu") for _ in range(self.world)]
+            dist.all_gather(parts, t.cpu(), group=self.group)
+            out.copy_(torch.cat(parts, 0))
+            return out
+        parts = list(out.view(self.world, *t.shape).unbind(0))
+        dist.all_gather(parts, t.contiguous(), group=self.group)
         return out
 
     def all_gather_cols(self, t: torch.Tensor):

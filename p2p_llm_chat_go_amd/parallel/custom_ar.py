@@ -8,8 +8,15 @@ peers' flags on its own memory and sums locally -- one hop.  The kernel is an
 ordinary launch on the current stream, so it is captured in the decode
 hipGraph with the GEMMs around it.  See ``csrc/kernels/custom_allreduce.hip``.
 
+The same buffers carry the two small per-step exchanges of vocab-parallel
+sampling: a MAX all-reduce of the greedy argmax keys (u64) and an all-gather
+of per-shard top-k candidates.  With those, a TP decode graph holds no RCCL
+call at all (one-shot kernels only).
+
 Handles are exchanged with ``dist.all_gather_object`` over the TP group (any
 backend).  Messages above ``max_bytes`` fall back to the caller's RCCL path.
+Timeouts are loud: ``check()`` raises once a peer failed to arrive within the
+spin bound (``LlamaModel.check_faults`` calls it wherever the host syncs).
 """
 from __future__ import annotations
 
@@ -19,6 +26,10 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _lib
+
+
+class CollectiveTimeout(RuntimeError):
+    """A one-shot collective gave up waiting for a peer rank (dead or hung)."""
 
 
 class CustomAllReduce:
@@ -65,6 +76,36 @@ class CustomAllReduce:
         return (t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() % 8 == 0
                 and t.numel() * 2 <= self.max_bytes)
 
+    def fits_bytes(self, nbytes: int) -> bool:
+        return nbytes % 16 == 0 and nbytes <= self.max_bytes
+
+    def allreduce_max_u64_(self, keys: torch.Tensor, blocks: int = 0):
+        """keys = elementwise max over ranks (int64 storage, unsigned order), in place."""
+        assert keys.dtype == torch.int64 and keys.is_contiguous() and self.fits_bytes(keys.numel() * 8)
+        _lib.check(self.L.p2p_car_allreduce_max_u64(self._bases, self.rank, self.world,
+                                                    self.max_bytes, keys.data_ptr(),
+                                                    keys.data_ptr(), keys.numel(),
+                                                    self.counters.data_ptr(), self.err.data_ptr(),
+                                                    blocks, _lib.stream_ptr(keys.device)),
+                   "car_allreduce_max_u64")
+        return keys
+
+    def all_gather_(self, out: torch.Tensor, t: torch.Tensor, blocks: int = 0):
+        """out (world x t's bytes, rank-major) = every rank's t."""
+        nb = t.numel() * t.element_size()
+        assert t.is_contiguous() and out.is_contiguous() and self.fits_bytes(nb)
+        assert out.numel() * out.element_size() == self.world * nb
+        _lib.check(self.L.p2p_car_all_gather(self._bases, self.rank, self.world, self.max_bytes,
+                                             t.data_ptr(), out.data_ptr(), nb,
+                                             self.counters.data_ptr(), self.err.data_ptr(),
+                                             blocks, _lib.stream_ptr(t.device)), "car_all_gather")
+        return out
+
+    @staticmethod
+    def set_timeout_ms(ms: int):
+        """Spin bound of the one-shot kernels (default 5 s); fault-injection tests lower it."""
+        _lib.check(_lib.lib().p2p_car_set_timeout_ms(int(ms)), "car_set_timeout_ms")
+
     def allreduce_add_(self, h: torch.Tensor, partial: torch.Tensor, blocks: int = 0):
         """h += sum over ranks of partial (bf16, same shape, contiguous)."""
         assert self.fits(partial) and h.is_contiguous() and h.numel() == partial.numel()
@@ -78,7 +119,8 @@ class CustomAllReduce:
     def check(self):
         """Raise if any call timed out waiting for a peer (numbers would be wrong)."""
         if int(self.err.item()) != 0:
-            raise RuntimeError("custom all-reduce: a peer never arrived (timeout)")
+            raise CollectiveTimeout("custom all-reduce: a peer never arrived (timeout); "
+                                    "the TP group is broken")
 
     def close(self):
         if self._own is None:

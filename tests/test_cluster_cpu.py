@@ -1,0 +1,176 @@
+"""Multi-GPU serving behind the node (engine.cluster) on the CPU: gloo groups of
+world 2/4/8 with the leader/follower lockstep, the DP replica router, and loud
+failure of a group whose rank dies.  Replies must equal the unsharded single-
+process engine's (greedy and seeded sampling)."""
+import json
+import threading
+
+import pytest
+import torch
+
+from p2p_llm_chat_go_amd.engine import Engine
+from p2p_llm_chat_go_amd.engine.cluster import ClusterServer
+from p2p_llm_chat_go_amd.engine.server import EngineServer
+from p2p_llm_chat_go_amd.models.config import get_config
+from p2p_llm_chat_go_amd.models.reference import random_state_dict
+from p2p_llm_chat_go_amd.models.weights import EngineWeights
+
+SEED = 3
+MSG = "Did you see the game last night? That last-minute goal was unbelievable!"
+
+
+def _req(options, prompt=MSG, **kw):
+    return json.dumps(dict({"model": "llama3.1", "prompt": prompt, "stream": False,
+                            "options": options}, **kw))
+
+
+def _reference(model, reqs):
+    cfg = get_config(model)
+    sd = random_state_dict(cfg, seed=SEED)
+    eng = Engine(cfg, weights=EngineWeights.from_state_dict(sd, cfg, "cpu"), device="cpu",
+                 kv_pages=256)
+    srv = EngineServer(eng)
+    try:
+        return [json.loads(srv.handle_json(r))["response"] for r in reqs]
+    finally:
+        srv.close()
+
+
+REQS = [_req({"temperature": 0, "num_predict": 8}),
+        _req({"temperature": 0.8, "top_k": 40, "top_p": 0.9, "seed": 7, "num_predict": 8}),
+        _req({"temperature": 0, "num_predict": 6}, prompt="Hey! How's it going?")]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tp_cluster_matches_single_engine(world):
+    torch.set_num_threads(2)
+    ref = _reference("tiny-llama-gqa", REQS)
+    cs = ClusterServer("tiny-llama-gqa", gpus=world, tp=world, device="cpu", sd_seed=SEED,
+                       warmup=False)
+    try:
+        got = [json.loads(cs.handle_json(r))["response"] for r in REQS]
+        m = cs.metrics()
+        assert m["replicas"] == 1 and m["group_size"] == world and m["live_replicas"] == 1
+    finally:
+        cs.close()
+    assert got == ref
+
+
+def test_ep_cluster_matches_single_engine():
+    torch.set_num_threads(2)
+    reqs = REQS[:1] + REQS[2:]
+    ref = _reference("tiny-mixtral-8e", reqs)
+    cs = ClusterServer("tiny-mixtral-8e", gpus=8, ep=8, device="cpu", sd_seed=SEED, warmup=False)
+    try:
+        got = [json.loads(cs.handle_json(r))["response"] for r in reqs]
+    finally:
+        cs.close()
+    assert got == ref
+
+
+def test_dp_router_spreads_and_streams():
+    """4 concurrent peers over 2 replicas of a TP=2 group (4 ranks): every reply equals
+    the single engine's, both replicas served, streaming relays chunks."""
+    torch.set_num_threads(2)
+    reqs = [REQS[0], REQS[2], REQS[0], REQS[1]]
+    ref = _reference("tiny-llama-gqa", reqs)
+    cs = ClusterServer("tiny-llama-gqa", gpus=4, tp=2, device="cpu", sd_seed=SEED, warmup=False)
+    try:
+        out = [None] * len(reqs)
+
+        def go(i):
+            out[i] = json.loads(cs.handle_json(reqs[i]))["response"]
+
+        ts = [threading.Thread(target=go, args=(i,)) for i in range(len(reqs))]
+        [t.start() for t in ts]
+        [t.join(120) for t in ts]
+        assert out == ref
+        chunks = []
+        final = json.loads(cs.handle_json_stream(REQS[0], lambda c: chunks.append(c) or True))
+        assert final["done"] is True
+        streamed = "".join(json.loads(c)["response"] for c in chunks)
+        assert streamed == ref[0]
+        m = cs.metrics()
+        assert m["replicas"] == 2 and m["live_replicas"] == 2
+        assert all(r["routed"] > 0 for r in m["per_replica"])
+    finally:
+        cs.close()
+
+
+def test_dead_rank_fails_loudly():
+    """Killing a follower rank: the group's next request errors (no silent tokens), the
+    router marks the replica dead, and later requests fail fast."""
+    torch.set_num_threads(2)
+    cs = ClusterServer("tiny-llama-gqa", gpus=2, tp=2, device="cpu", sd_seed=SEED, warmup=False)
+    try:
+        json.loads(cs.handle_json(REQS[0]))
+        rep = cs._replicas[0]
+        rep.procs[1].kill()
+        rep.procs[1].join(10)
+        with pytest.raises(RuntimeError):
+            cs.handle_json(REQS[0])
+        rep.procs[0].join(30)
+        assert rep.procs[0].exitcode not in (None, 0)  # the leader exited non-zero
+        assert not rep.alive
+        with pytest.raises(RuntimeError, match="no live engine replica"):
+            cs.handle_json(REQS[0])
+    finally:
+        cs.close()
+
+
+def test_tp_node_suggest_over_http(tmp_path):
+    """`python -m p2p_llm_chat_go_amd.net.node` with ENGINE_GPUS=2 ENGINE_TP=2 (CPU ranks):
+    a chat message sent by node A gets a /suggest reply on node B equal to the unsharded
+    engine's, and /api/generate answers through the same TP group."""
+    import os
+    import subprocess
+    import sys
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from netutil import BIN, Procs, free_port, http, wait_http
+
+    if not os.path.exists(os.path.join(BIN, "p2p-node")):
+        pytest.skip("native daemons not built")
+    procs = Procs()
+    try:
+        dport = free_port()
+        procs.spawn("p2p-directory", {"ADDR": "127.0.0.1:%d" % dport})
+        d = "http://127.0.0.1:%d" % dport
+        wait_http(d + "/health")
+        urls = []
+        for name, engine in (("A", "0"), ("B", "1")):
+            port = free_port()
+            env = dict(os.environ, MYNAMEIS=name, HTTP_ADDR="127.0.0.1:%d" % port,
+                       DIRECTORY_URL=d, KEY_TYPE="ed25519", LISTEN_ADDRS="/ip4/127.0.0.1/tcp/0",
+                       ENGINE=engine, ENGINE_DEVICE="cpu", ENGINE_MODEL="tiny-llama-gqa",
+                       ENGINE_GPUS="2", ENGINE_TP="2", ENGINE_SD_SEED=str(SEED),
+                       PYTHONPATH=os.path.dirname(BIN))
+            p = subprocess.Popen([sys.executable, "-m", "p2p_llm_chat_go_amd.net.node"], env=env,
+                                 stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            procs.procs.append(p)
+            urls.append("http://127.0.0.1:%d" % port)
+            wait_http(urls[-1] + "/me", timeout=120)
+        a, b = urls
+        st, body, _ = http("POST", a + "/send", {"to_username": "B", "content": MSG})
+        assert st == 200, body
+        mid = json.loads(body)["id"]
+        for _ in range(100):
+            if json.loads(http("GET", b + "/inbox")[1]):
+                break
+            import time
+            time.sleep(0.05)
+        st, body, _ = http("POST", b + "/suggest", {"id": mid, "options": {"temperature": 0,
+                                                                            "num_predict": 8}},
+                           timeout=120)
+        assert st == 200, body
+        sug = json.loads(body)["suggestion"]
+        from p2p_llm_chat_go_amd.engine.tokenizer import suggest_prompt
+
+        # (same request order: the synthetic tokenizer's decode table grows as it encodes)
+        ref = _reference("tiny-llama-gqa", [_req({"temperature": 0, "num_predict": 8},
+                                                 prompt=suggest_prompt(MSG)), REQS[0]])
+        assert sug == ref[0]
+        st, body, _ = http("POST", b + "/api/generate", json.loads(REQS[0]), timeout=120)
+        assert st == 200 and json.loads(body)["response"] == ref[1]
+    finally:
+        procs.close()

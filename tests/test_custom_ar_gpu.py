@@ -78,7 +78,44 @@ def _worker(rank, world, port, q):
         want = 12 * sum(r + 1 for r in range(world))
         graph_ok = bool((h.float() == want).all().item())
         car.check()
-        q.put((rank, max(errs) < 1e-2 and graph_ok, (max(errs), graph_ok)))
+        # back-to-back calls alternating above / below 32768 vectors (slices of different
+        # block counts) with one rank delayed on the GPU: no host sync between calls
+        dist.barrier()
+        sizes = [1 << 19, 8, 300008, 4096, 1 << 19, 16, 262152, 8, 1 << 19, 4096] * 2
+        outs, refs = [], []
+        for i, n in enumerate(sizes):
+            call += 1
+            h0 = _data(7 + call, n)
+            h = h0.cuda()
+            p = _data(1000 * call + rank, n).cuda()
+            if rank == 1 and i % 3 == 0:
+                torch.cuda._sleep(2_000_000)  # the slow peer
+            car.allreduce_add_(h, p)
+            outs.append(h)
+            refs.append(_expect(h0, world, n, call))
+        torch.cuda.synchronize()
+        stress = max(((o.cpu().float() - r.float()).abs().max() / (r.float().abs().max() + 1e-6)).item()
+                     for o, r in zip(outs, refs))
+        # u64 MAX (unsigned order: keys with the top bit set are the largest) and all-gather
+        g = torch.Generator().manual_seed(rank + 5)
+        keys = torch.randint(-2 ** 62, 2 ** 62, (64, 32), generator=g, dtype=torch.int64)
+        keys[rank, 0] = -5  # 0xFFFF...FB: the unsigned maximum of row `rank`
+        allk = [None] * world
+        dist.all_gather_object(allk, keys)
+        kd = keys.cuda()
+        car.allreduce_max_u64_(kd)
+        u = torch.stack([k for k in allk]).view(torch.int64) ^ (-(2 ** 63))
+        want_k = (u.max(0).values ^ (-(2 ** 63)))
+        max_ok = bool((kd.cpu() == want_k).all().item())
+        t = (torch.arange(1000, dtype=torch.float32) + 10000 * rank).cuda()
+        out = torch.empty(world * 1000, dtype=torch.float32, device="cuda")
+        car.all_gather_(out, t)
+        torch.cuda.synchronize()
+        gat_ok = bool((out.cpu() == torch.cat([torch.arange(1000, dtype=torch.float32) + 10000 * r
+                                               for r in range(world)])).all().item())
+        car.check()
+        q.put((rank, max(errs) < 1e-2 and graph_ok and stress < 1e-2 and max_ok and gat_ok,
+               (max(errs), graph_ok, stress, max_ok, gat_ok)))
     except Exception:
         import traceback
 
@@ -88,6 +125,64 @@ def _worker(rank, world, port, q):
             dist.barrier()
             car.close()
         dist.destroy_process_group()
+
+
+def _dead_peer_worker(rank, world, port, q):
+    """Rank 1 stops calling: rank 0's one-shot kernel must give up within the spin bound,
+    set the error word, and skip later waits; check() raises."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    car = None
+    try:
+        from p2p_llm_chat_go_amd.parallel.custom_ar import CollectiveTimeout, CustomAllReduce
+
+        torch.cuda.set_device(0)
+        car = CustomAllReduce(device="cuda:0", max_bytes=1 << 20)
+        CustomAllReduce.set_timeout_ms(300)
+        h = torch.zeros(4096, dtype=torch.bfloat16, device="cuda")
+        p = torch.ones_like(h)
+        car.allreduce_add_(h, p)
+        torch.cuda.synchronize()
+        car.check()
+        dist.barrier()
+        if rank == 1:  # stop calling; keep the buffer mapped until rank 0 is done
+            q.put((rank, True, "peer left"))
+            dist.barrier()
+            return
+        t0 = time.time()
+        for _ in range(20):  # one timeout, then every later call returns at once
+            car.allreduce_add_(h, p)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        try:
+            car.check()
+            q.put((rank, False, "no error after a dead peer"))
+        except CollectiveTimeout:
+            q.put((rank, dt < 5.0, "raised after %.2fs" % dt))
+        dist.barrier()
+    except Exception:
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        if car is not None:
+            car.close()
+        dist.destroy_process_group()
+
+
+def test_custom_allreduce_dead_peer_raises():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = [q.get(timeout=300) for _ in range(2)]
+    [p.join(timeout=60) for p in ps]
+    [p.terminate() for p in ps if p.is_alive()]
+    for rank, ok, info in res:
+        assert ok, (rank, info)
 
 
 def test_custom_allreduce_two_ranks_one_gpu():

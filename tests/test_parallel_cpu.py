@@ -1,6 +1,8 @@
-"""Tensor-parallel correctness on CPU: gloo, world_size 2 (and 4), Megatron
+"""Tensor-parallel correctness on CPU: gloo, world_size 2, 4 and 8, Megatron
 sharding of qkv / o / gate_up / down / vocab-parallel LM head against the
-unsharded engine (SURVEY §4.2 distributed tier (a))."""
+unsharded engine (SURVEY §4.2 distributed tier (a)).  The TP model has the
+8B/70B head structure (32 q / 8 kv heads: one kv head per rank at world 8) and
+the EP model 8 experts (one per rank at world 8, Mixtral EP=8)."""
 import os
 import socket
 
@@ -9,9 +11,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from p2p_llm_chat_go_amd.models import TINY_LLAMA
+from p2p_llm_chat_go_amd.models.config import TINY_LLAMA_GQA, TINY_MIXTRAL_8E
 
-TP_CFG = TINY_LLAMA.replace(name="tiny-tp", n_heads=4, n_kv_heads=4, ffn=512, n_layers=2)
+TP_CFG = TINY_LLAMA_GQA
 
 
 def _port():
@@ -24,6 +26,7 @@ def _port():
 
 def _worker(rank, world, port, q, moe, a2a=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from p2p_llm_chat_go_amd.engine import Engine
@@ -33,8 +36,7 @@ def _worker(rank, world, port, q, moe, a2a=False):
 
         cfg = TP_CFG
         if moe:
-            from p2p_llm_chat_go_amd.models import TINY_MIXTRAL
-            cfg = TINY_MIXTRAL.replace(n_heads=4, n_kv_heads=4)
+            cfg = TINY_MIXTRAL_8E
         sd = random_state_dict(cfg, seed=3)
         prompts = [[1, 2, 3, 4, 5], list(range(10, 50))]
         if a2a:  # DP attention: every rank serves its own peers (equal lengths: lockstep)
@@ -90,16 +92,17 @@ def _run(world, moe=False, a2a=False):
         assert ok, (rank, got, ref)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_tensor_parallel_matches_single(world):
     _run(world)
 
 
-def test_expert_parallel_matches_single():
-    _run(2, moe=True)
+@pytest.mark.parametrize("world", [2, 8])
+def test_expert_parallel_matches_single(world):
+    _run(world, moe=True)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_expert_parallel_all_to_all_dp_attention(world):
     """EP with token dispatch/return by all-to-all (DP attention, distinct prompts per rank)."""
     _run(world, moe=True, a2a=True)
@@ -112,3 +115,49 @@ def test_u64_max_allreduce_ordering():
     k = torch.tensor([[0x7FFFFFFF_00000001, -0x7FFFFFFF_00000000]], dtype=torch.int64)
     flipped = k ^ comm._SIGN
     assert int(flipped.max()) == int(flipped[0, 1])  # the "negative" int64 is the larger u64
+
+
+def _dying_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from p2p_llm_chat_go_amd.engine import Engine
+    from p2p_llm_chat_go_amd.parallel.comm import TPComm
+
+    comm = TPComm()
+    eng = Engine(TP_CFG, device="cpu", kv_pages=32, comm=comm, tp_rank=rank, tp_size=world)
+    prompts = [[1, 2, 3, 4, 5]]
+    eng.generate(prompts, 4, stop_on_eos=False)
+    if rank == 1:  # die mid-decode: after a few collectives of the next reply
+        calls = [0]
+        orig = comm.allreduce_add_
+
+        def dying(h, p):
+            calls[0] += 1
+            if calls[0] == 12:
+                os._exit(3)
+            return orig(h, p)
+
+        comm.allreduce_add_ = dying
+    import time
+    t0 = time.time()
+    try:
+        eng.generate(prompts, 16, stop_on_eos=False)
+        q.put((rank, False, "tokens returned with a dead peer"))
+    except Exception as e:
+        q.put((rank, True, "%s after %.1fs" % (type(e).__name__, time.time() - t0)))
+    os._exit(0)
+
+
+def test_tp_peer_death_raises_cpu():
+    """A TP rank dying mid-decode makes the survivor raise (no silent tokens)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_dying_worker, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    rank, ok, info = q.get(timeout=300)
+    [p.join(timeout=60) for p in ps]
+    [p.terminate() for p in ps if p.is_alive()]
+    assert rank == 0 and ok, info
+    assert ps[1].exitcode == 3

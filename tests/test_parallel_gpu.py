@@ -1,7 +1,10 @@
 """Tensor / expert parallelism on the GPU kernels with *virtual ranks*: two
-processes share the one MI355X of the test box (SURVEY §4.2 tier (b)), their
-collectives run over gloo (RCCL refuses two ranks on one device), graphs off.
-Sharded engines must reproduce the unsharded engine's greedy tokens."""
+processes share the one MI355X of the test box (SURVEY §4.2 tier (b)).  Their
+host-side collectives run over gloo (RCCL refuses two ranks on one device);
+the TP decode step's collectives are the one-shot IPC kernels (row-parallel
+sums, argmax-key MAX), so dense TP decode runs captured in hipGraphs exactly as
+on 8 GPUs.  Sharded engines must reproduce the unsharded engine's greedy tokens;
+a rank that stops mid-decode must make its peer raise, not emit tokens."""
 import os
 import socket
 
@@ -21,7 +24,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q, moe, a2a=False, overlap=False):
+def _worker(rank, world, port, q, moe, a2a=False, overlap=False, graphs=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if overlap:  # prefill row-parallel sums chunked onto a communication stream
         os.environ["P2P_TP_OVERLAP_MIN_ROWS"] = "16"
@@ -45,9 +48,14 @@ def _worker(rank, world, port, q, moe, a2a=False, overlap=False):
         kw = dict(ep_rank=rank, ep_size=world) if moe else dict(tp_rank=rank, tp_size=world)
         w = EngineWeights.from_state_dict(sd, cfg, "cuda", **kw)
         eng = Engine(cfg, weights=w, device="cuda", kv_pages=32, comm=TPComm(),
-                     tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=False,
+                     tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=graphs,
                      ep_mode="a2a" if a2a else "allreduce")
         got = [r.tokens for r in eng.generate(prompts, 6, stop_on_eos=False)]
+        if graphs:
+            gs = list(eng._graphs.values())
+            assert gs and all(g.graph is not None for g in gs), "TP decode graph not captured"
+            got2 = [r.tokens for r in eng.generate(prompts, 6, stop_on_eos=False)]  # replays
+            assert got2 == got, (got2, got)
         q.put((rank, got == ref, got, ref))
     except Exception:
         import traceback
@@ -56,17 +64,68 @@ def _worker(rank, world, port, q, moe, a2a=False, overlap=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("moe,a2a,overlap", [(False, False, False), (False, False, True),
-                                              (True, False, False), (True, True, False)])
-def test_virtual_rank_parallel_gpu(moe, a2a, overlap):
+@pytest.mark.parametrize("moe,a2a,overlap,graphs", [
+    (False, False, False, False), (False, False, False, True), (False, False, True, False),
+    (True, False, False, False), (True, True, False, False)])
+def test_virtual_rank_parallel_gpu(moe, a2a, overlap, graphs):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     world = 2
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a, overlap))
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a, overlap, graphs))
           for r in range(world)]
     [p.start() for p in ps]
     res = [q.get(timeout=600) for _ in range(world)]
     [p.join(timeout=60) for p in ps]
     for rank, ok, got, ref in res:
         assert ok, (rank, got, ref)
+
+
+def _dead_rank_worker(rank, world, port, q, hold):
+    """TP decode with graphs; rank 1 stops participating after its first reply: rank 0's
+    next generate must raise (one-shot collective timeout) instead of returning tokens."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from p2p_llm_chat_go_amd.engine import Engine
+        from p2p_llm_chat_go_amd.models import TINY_LLAMA
+        from p2p_llm_chat_go_amd.parallel.comm import TPComm
+        from p2p_llm_chat_go_amd.parallel.custom_ar import CollectiveTimeout, CustomAllReduce
+
+        cfg = TINY_LLAMA.replace(n_heads=4, n_kv_heads=4)
+        eng = Engine(cfg, device="cuda", kv_pages=32, comm=TPComm(), tp_rank=rank, tp_size=world,
+                     seed=5)
+        CustomAllReduce.set_timeout_ms(300)
+        prompts = [[1, 2, 3, 4, 5]]
+        eng.generate(prompts, 4, stop_on_eos=False)
+        eng.decode_graph(1, 16)  # both ranks capture before one leaves
+        dist.barrier()
+        if rank == 1:
+            q.put((rank, True, "left"))
+            hold.wait(120)  # alive (buffers mapped) but silent
+            return
+        try:
+            eng.generate(prompts, 8, stop_on_eos=False)
+            q.put((rank, False, "tokens returned with a dead peer"))
+        except CollectiveTimeout as e:
+            q.put((rank, True, str(e)))
+        finally:
+            hold.set()
+    except Exception:
+        import traceback
+        q.put((rank, False, traceback.format_exc()))
+        hold.set()
+
+
+def test_tp_dead_rank_raises():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    hold = ctx.Event()
+    port = _port()
+    ps = [ctx.Process(target=_dead_rank_worker, args=(r, 2, port, q, hold)) for r in range(2)]
+    [p.start() for p in ps]
+    res = [q.get(timeout=600) for _ in range(2)]
+    [p.join(timeout=60) for p in ps]
+    [p.terminate() for p in ps if p.is_alive()]
+    for rank, ok, info in res:
+        assert ok, (rank, info)
