@@ -270,6 +270,53 @@ PYBIND11_MODULE(_native, m) {
     py::gil_scoped_release rel;
     return quic_echo(kt, in, drop, streams);
   }, py::arg("key_type"), py::arg("payload"), py::arg("drop_rate") = 0.0, py::arg("streams") = 1);
+  m.def("quic_protocol_violation", [](const std::string& kind) {
+    // a client sends a frame past the server's advertised limits; returns the client's
+    // view of the close (the server must answer with the RFC 9000 error code)
+    PrivateKey ka = PrivateKey::generate(KeyType::Ed25519), kb = PrivateKey::generate(KeyType::Ed25519);
+    const PeerId idb = PeerId::from_public_key(kb.public_key());
+    auto srv = QuicTransport::create("127.0.0.1", 0, kb);
+    auto cli = QuicTransport::create("127.0.0.1", 0, ka);
+    srv->set_accept([](QuicConnPtr c) { c->start([](StreamPtr) {}); });
+    std::string why;
+    bool closed = false;
+    {
+      py::gil_scoped_release nogil;
+      auto c = cli->dial("127.0.0.1", srv->port(), idb, 10000);
+      c->start(nullptr);
+      Bytes f;
+      if (kind == "stream") {  // STREAM (OFF|LEN) on our stream 0 at 64 MiB: past the 4 MiB window
+        f.push_back(0x0e);
+        quic_put_varint(f, 0);
+        quic_put_varint(f, 64ull << 20);
+        quic_put_varint(f, 16);
+        f.insert(f.end(), 16, 0x61);
+      } else if (kind == "conn") {  // many streams, each inside its window, together past MAX_DATA
+        for (int i = 0; i < 5; ++i) {
+          Bytes g{0x0e};
+          quic_put_varint(g, (uint64_t)i << 2);
+          quic_put_varint(g, (4ull << 20) - 16);
+          quic_put_varint(g, 16);
+          g.insert(g.end(), 16, 0x62);
+          c->send_raw_frame_for_test(g);
+        }
+      } else {  // CRYPTO far ahead of the handshake stream
+        f.push_back(0x06);
+        quic_put_varint(f, 1ull << 30);
+        quic_put_varint(f, 16);
+        f.insert(f.end(), 16, 0x63);
+      }
+      if (!f.empty()) c->send_raw_frame_for_test(f);
+      for (int i = 0; i < 200 && !c->closed(); ++i)
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      closed = c->closed();
+      why = c->error_text();
+      c->close();
+      cli->close();
+      srv->close();
+    }
+    return py::make_tuple(closed, why);
+  });
   m.def("quic_initial_keys", [](const py::bytes& dcid) {
     QuicKeys c, s;
     quic_initial_keys(U(dcid), &c, &s);

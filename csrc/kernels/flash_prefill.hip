@@ -14,8 +14,8 @@
 //
 // Replaces the per-row decode kernel for long prompts, whose K/V traffic is
 // O(T^2): here each K/V tile is read once per 16 query tokens x G heads.
-// Behavioural parity: the reference delegates prompt processing to the Ollama
-// server (`llm/ollama.go:40`), see SURVEY.md §1 L0.
+// Behavioural parity: the reference delegates prompt processing to an external
+// Ollama server (`web/streamlit_app.py:89-101`), see SURVEY.md §2B.2 B2.3.
 #include "common.h"
 
 namespace {

@@ -75,12 +75,13 @@ Inbox::Inbox(std::string persist_path, size_t cap) : path_(std::move(persist_pat
     } catch (...) {
     }
   }
+  while (cap_ && q_.size() > cap_) q_.pop_front();
 }
 
 void Inbox::push(const ChatMessage& m) {
   std::lock_guard<std::mutex> lk(mu_);
   q_.push_back(m);
-  if (cap_ && q_.size() > cap_) q_.erase(q_.begin(), q_.begin() + (q_.size() - cap_));
+  while (cap_ && q_.size() > cap_) q_.pop_front();
   if (!path_.empty()) {
     FILE* f = fopen(path_.c_str(), "a");
     if (f) {
@@ -93,7 +94,7 @@ void Inbox::push(const ChatMessage& m) {
 
 std::vector<ChatMessage> Inbox::drain(const std::string& after) {
   std::lock_guard<std::mutex> lk(mu_);
-  if (after.empty()) return q_;
+  if (after.empty()) return std::vector<ChatMessage>(q_.begin(), q_.end());
   std::vector<ChatMessage> out;
   bool found = false;
   for (auto& m : q_) {
@@ -224,6 +225,7 @@ NodeConfig NodeConfig::from_env() {
   c.key_type = env_or("KEY_TYPE", c.key_type);
   c.identity_file = env_or("IDENTITY_FILE", "");
   c.inbox_file = env_or("INBOX_FILE", "");
+  c.inbox_cap = (size_t)atoll(env_or("INBOX_CAP", std::to_string(c.inbox_cap)).c_str());
   c.engine_url = env_or("ENGINE_URL", "");
   c.llm_model = env_or("LLM_MODEL", c.llm_model);
   c.ui_file = env_or("UI_FILE", "");
@@ -281,7 +283,7 @@ static PrivateKey load_or_make_identity(const NodeConfig& cfg) {
 }
 
 Node::Node(NodeConfig cfg)
-    : cfg_(std::move(cfg)), inbox_(cfg_.inbox_file), http_("GIN") {}
+    : cfg_(std::move(cfg)), inbox_(cfg_.inbox_file, cfg_.inbox_cap), http_("GIN") {}
 
 Node::~Node() { stop(); }
 

@@ -5,6 +5,7 @@
 // the HTTP API (`:213-283`) and the suggest-reply engine hook together.
 #pragma once
 #include <atomic>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -43,7 +44,7 @@ class Inbox {
 
  private:
   std::mutex mu_;
-  std::vector<ChatMessage> q_;
+  std::deque<ChatMessage> q_;  // newest cap_ messages (O(1) trim at the front)
   std::string path_;
   size_t cap_;
 };
@@ -90,6 +91,7 @@ struct NodeConfig {
   std::string key_type = "rsa";  // reference: RSA-2048, regenerated each run
   std::string identity_file;     // opt-in persistence (libp2p PrivateKey protobuf)
   std::string inbox_file;        // opt-in JSONL persistence
+  size_t inbox_cap = 100000;     // INBOX_CAP: newest messages kept (0 = unbounded, as the reference)
   std::string engine_url;        // forward /api/generate here when no in-process engine
   std::string llm_model = "llama3.1";
   std::string ui_file;           // optional browser UI served at GET / and GET /ui

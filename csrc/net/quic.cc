@@ -30,6 +30,13 @@ constexpr uint64_t kConnWindow = 16ull << 20;
 constexpr uint64_t kStreamLimit = 256;  // concurrent peer-opened bidi streams
 constexpr size_t kMaxInFlight = 256;     // ack-eliciting 1-RTT packets outstanding
 constexpr int kIdleMs = 30000, kKeepAliveMs = 10000;
+constexpr uint64_t kMaxCryptoBuffer = 64 << 10;  // out-of-order CRYPTO bytes per space
+
+// A peer's protocol violation with its RFC 9000 §20.1 transport error code.
+struct QuicProtoError : std::runtime_error {
+  uint64_t code;
+  QuicProtoError(const std::string& m, uint64_t c) : std::runtime_error(m), code(c) {}
+};
 const uint8_t kInitialSalt[20] = {0x38, 0x76, 0x2c, 0xf7, 0xf5, 0x59, 0x34, 0xb3, 0x4d, 0x17,
                                   0x9a, 0xe6, 0xa4, 0xc8, 0x0c, 0xad, 0xcc, 0xbb, 0x7f, 0x0a};
 const unsigned char kAlpnLibp2p[] = "\x06libp2p";
@@ -608,6 +615,17 @@ void QuicConn::on_handshake_complete(Events& ev) {
   cv_.notify_all();
 }
 
+void QuicConn::send_raw_frame_for_test(const Bytes& frame) {
+  std::lock_guard<std::mutex> lk(mu_);  // flush() runs under the connection lock
+  sp_[APP].queued.push_back(frame);
+  flush();
+}
+
+std::string QuicConn::error_text() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return error_;
+}
+
 void QuicConn::fail(const std::string& why, uint64_t code, Events& ev) {
   if (error_.empty() || error_.rfind("tls alert", 0) == 0) error_ = "quic: " + why;
   close_locked(code, false, ev);
@@ -700,6 +718,8 @@ void QuicConn::handle_packet(Bytes pkt, size_t pn_off, int space, bool long_hdr,
   bool elicit = false;
   try {
     process_frames(space, pt.data(), pt.size(), &elicit, ev);
+  } catch (const QuicProtoError& e) {
+    return fail(std::string("protocol error: ") + e.what(), e.code, ev);
   } catch (const std::exception& e) {
     return fail(std::string("frame error: ") + e.what(), 0x07, ev);
   }
@@ -849,7 +869,13 @@ void QuicConn::on_ack(int space, const uint8_t* p, size_t n, size_t* pos, bool e
 void QuicConn::on_crypto(int space, uint64_t off, const uint8_t* data, size_t len, Events& ev) {
   Space& S = sp_[space];
   if (off + len <= S.crypto_in_off) return;  // retransmitted
-  S.crypto_in[off] = Bytes(data, data + len);
+  // RFC 9000 §7.5: bound what an (unauthenticated) peer can make us buffer ahead
+  if (off + len > S.crypto_in_off + kMaxCryptoBuffer || S.crypto_in_bytes + len > kMaxCryptoBuffer)
+    throw QuicProtoError("CRYPTO data beyond the buffer", 0x0d);  // CRYPTO_BUFFER_EXCEEDED
+  Bytes& slot = S.crypto_in[off];
+  if (slot.size() >= len) return;
+  S.crypto_in_bytes += len - slot.size();
+  slot.assign(data, data + len);
   Bytes ready;
   while (!S.crypto_in.empty() && S.crypto_in.begin()->first <= S.crypto_in_off) {
     auto it = S.crypto_in.begin();
@@ -859,6 +885,7 @@ void QuicConn::on_crypto(int space, uint64_t off, const uint8_t* data, size_t le
       ready.insert(ready.end(), b.begin() + (S.crypto_in_off - o), b.end());
       S.crypto_in_off = o + b.size();
     }
+    S.crypto_in_bytes -= b.size();
     S.crypto_in.erase(it);
   }
   if (ready.empty()) return;
@@ -914,6 +941,16 @@ void QuicConn::on_stream_frame(uint64_t id, uint64_t off, const uint8_t* data, s
                                bool fin, Events& ev) {
   auto s = peer_stream(id, ev);
   if (!s) return;
+  // RFC 9000 §4: data past the advertised stream / connection limits is a
+  // FLOW_CONTROL_ERROR (never buffered: rbuf_/ooo_ stay bounded by our windows)
+  const uint64_t end = off + len;
+  if (end > s->recv_limit_) throw QuicProtoError("stream data beyond MAX_STREAM_DATA", 0x03);
+  if (end > s->recv_high_) {
+    if (recv_total_ + (end - s->recv_high_) > recv_max_data_)
+      throw QuicProtoError("data beyond MAX_DATA", 0x03);
+    recv_total_ += end - s->recv_high_;
+    s->recv_high_ = end;
+  }
   if (fin) s->fin_off_ = off + len;
   if (s->local_closed_ || s->reset_) {
     // input discarded, but the credit is returned so the peer is never blocked
@@ -1489,5 +1526,7 @@ void QuicTransport::close() {
   std::lock_guard<std::mutex> lk(mu_);
   by_cid_.clear();
 }
+
+void quic_put_varint(Bytes& b, uint64_t v) { put_varint(b, v); }
 
 }  // namespace p2p

@@ -56,6 +56,9 @@
 namespace p2p {
 
 class QuicConn;
+
+// RFC 9000 §16 variable-length integer (exposed for frame-level tests).
+void quic_put_varint(Bytes& b, uint64_t v);
 class QuicTransport;
 
 class QuicStream : public MuxStream {
@@ -81,6 +84,7 @@ class QuicStream : public MuxStream {
   Bytes rbuf_;
   size_t rpos_ = 0;
   uint64_t recv_off_ = 0;            // next in-order offset
+  uint64_t recv_high_ = 0;           // highest offset received (flow-control accounting)
   uint64_t fin_off_ = ~0ull;         // final size once the FIN arrived
   uint64_t consumed_ = 0, recv_limit_ = 0;
   Bytes sq_;                         // queued, not yet packetised (from sq_head_)
@@ -125,6 +129,9 @@ class QuicConn : public MuxSession, public std::enable_shared_from_this<QuicConn
   void tls_keylog(const char* line);
   Bytes tp_encode() const { return transport_params(); }
   void tp_parse(const uint8_t* p, size_t n) { parse_transport_params(p, n); }
+  // test hooks: queue one raw 1-RTT frame (protocol-violation tests); the close reason
+  void send_raw_frame_for_test(const Bytes& frame);
+  std::string error_text();
 
  private:
   friend class QuicTransport;
@@ -146,6 +153,7 @@ class QuicConn : public MuxSession, public std::enable_shared_from_this<QuicConn
     uint64_t crypto_send_off = 0;
     std::map<uint64_t, Bytes> crypto_in;
     uint64_t crypto_in_off = 0;
+    size_t crypto_in_bytes = 0;      // buffered out-of-order CRYPTO bytes (capped)
     std::vector<Bytes> undecryptable;  // packets that arrived before their keys
   };
   struct Events {  // callbacks run after the connection mutex is released
@@ -223,6 +231,7 @@ class QuicConn : public MuxSession, public std::enable_shared_from_this<QuicConn
   uint64_t next_local_idx_ = 0, next_remote_idx_ = 0;
   uint64_t remote_closed_ = 0, max_remote_streams_ = 0;
   uint64_t sent_data_ = 0, recv_consumed_ = 0, recv_max_data_ = 0;
+  uint64_t recv_total_ = 0;  // sum of every stream's recv_high_ (connection flow control)
   std::function<void(StreamPtr)> on_stream_;
   std::function<void()> on_close_;
   // recovery

@@ -128,9 +128,7 @@ class EngineServer:
             return json.dumps(self.metrics())
         params = SamplingParams.from_ollama(req.get("options"), self.default_max_tokens)
         if req.get("endpoint") == "chat":
-            msgs = req.get("messages") or []
-            text = "\n".join(m.get("content", "") for m in msgs if m.get("role") != "system")
-            ids = self.tok.chat_ids(text)
+            ids = self.tok.chat_messages_ids(req.get("messages") or [])
         elif req.get("raw"):
             ids = self.tok.encode(req.get("prompt", ""), bos=True)
         else:
@@ -159,9 +157,7 @@ class EngineServer:
         params = SamplingParams.from_ollama(req.get("options"), self.default_max_tokens)
         chat = req.get("endpoint") == "chat"
         if chat:
-            msgs = req.get("messages") or []
-            ids = self.tok.chat_ids("\n".join(m.get("content", "") for m in msgs
-                                               if m.get("role") != "system"))
+            ids = self.tok.chat_messages_ids(req.get("messages") or [])
         elif req.get("raw"):
             ids = self.tok.encode(req.get("prompt", ""), bos=True)
         else:

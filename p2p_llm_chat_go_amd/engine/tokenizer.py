@@ -32,6 +32,37 @@ def suggest_prompt(message: str) -> str:
     return SUGGEST_TEMPLATE.format(prompt=message)
 
 
+def _render_messages(tok, messages: list, special) -> list:
+    """Ollama ``/api/chat`` messages -> prompt ids, per-message roles kept.
+
+    llama3.x (Ollama's llama3.1 template): ``<|begin_of_text|>`` then, per message,
+    ``<|start_header_id|>{role}<|end_header_id|>\n\n{content}<|eot_id|>``, then an open
+    assistant header.  [INST] models (Mixtral): a system message is prepended to the
+    first user turn; assistant turns close with ``</s>``."""
+    msgs = [m for m in messages or [] if isinstance(m, dict)]
+    if tok.llama3:
+        ids = [tok.bos_id]
+        for m in msgs:
+            ids += [special("<|start_header_id|>")] + tok.encode(str(m.get("role", "user")))
+            ids += [special("<|end_header_id|>")] + tok.encode("\n\n" + str(m.get("content", "")))
+            ids += [special("<|eot_id|>")]
+        return ids + [special("<|start_header_id|>")] + tok.encode("assistant") + [
+            special("<|end_header_id|>")] + tok.encode("\n\n")
+    ids = [tok.bos_id]
+    system = "\n\n".join(str(m.get("content", "")) for m in msgs if m.get("role") == "system")
+    for m in msgs:
+        role, content = m.get("role", "user"), str(m.get("content", ""))
+        if role == "system":
+            continue
+        if role == "assistant":
+            ids += tok.encode(" " + content) + list(tok.eos_ids[:1])
+            continue
+        if system:
+            content, system = system + "\n\n" + content, ""
+        ids += tok.encode("[INST] " + content + " [/INST]")
+    return ids
+
+
 class SyntheticTokenizer:
     _pat = re.compile(r"\s*\w+|\s*[^\w\s]|\s+")
 
@@ -75,6 +106,9 @@ class SyntheticTokenizer:
             return ids + self.encode("assistant") + [S["<|end_header_id|>"]] + self.encode("\n\n")
         return [self.bos_id] + self.encode("[INST] " + user_text + " [/INST]")
 
+    def chat_messages_ids(self, messages: list) -> list:
+        return _render_messages(self, messages, LLAMA3_SPECIAL.__getitem__)
+
 
 class HFTokenizer:
     def __init__(self, path: str, eos_ids=None):
@@ -108,6 +142,9 @@ class HFTokenizer:
                     + [t("<|eot_id|>"), t("<|start_header_id|>")] + self.encode("assistant")
                     + [t("<|end_header_id|>")] + self.encode("\n\n"))
         return [self.bos_id] + self.encode("[INST] " + user_text + " [/INST]")
+
+    def chat_messages_ids(self, messages: list) -> list:
+        return _render_messages(self, messages, self.tok.token_to_id)
 
 
 def get_tokenizer(cfg=None, path: str | None = None):

@@ -577,3 +577,20 @@ def test_dial_ranking_tcp_and_quic(procs, prefer, transport):
     assert http("POST", a + "/send", {"to_username": "B", "content": "hi"})[0] == 200
     assert _wait_inbox(b, 1)[0]["content"] == "hi"
     assert json.loads(http("GET", a + "/peers")[1])[0]["transport"] == transport
+
+
+def test_inbox_cap_keeps_newest(procs):
+    """INBOX_CAP bounds the inbox (the reference's slice grows without bound,
+    `go/cmd/node/main.go:102-106`): the newest messages are kept, in order."""
+    d = start_directory(procs)
+    a = start_node(procs, "A", d)
+    b = start_node(procs, "B", d, {"INBOX_CAP": "3"})
+    for i in range(5):  # one at a time: each delivered before the next is sent
+        st, body, _ = http("POST", a + "/send", {"to_username": "B", "content": "m%d" % i})
+        assert st == 200, body
+        for _ in range(200):
+            inbox = json.loads(http("GET", b + "/inbox")[1])
+            if inbox and inbox[-1]["content"] == "m%d" % i:
+                break
+            time.sleep(0.02)
+    assert [m["content"] for m in inbox] == ["m2", "m3", "m4"]

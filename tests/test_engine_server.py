@@ -111,6 +111,31 @@ def test_server_sampling_and_chat():
         srv.close()
 
 
+def test_chat_keeps_roles():
+    """/api/chat renders every message with its role (system and assistant turns are
+    part of the prompt, Ollama's llama3.1 / [INST] templates), not one joined user turn."""
+    from p2p_llm_chat_go_amd.engine.tokenizer import SyntheticTokenizer
+
+    srv, _, cfg = make_server()
+    try:
+        def chat(msgs):
+            return json.loads(srv.handle_json(json.dumps(
+                {"endpoint": "chat", "messages": msgs, "options": {"num_predict": 2}})))
+
+        user = [{"role": "user", "content": "hey there"}]
+        base = chat(user)["prompt_eval_count"]
+        sys_ = chat([{"role": "system", "content": "answer in French"}] + user)
+        multi = chat(user + [{"role": "assistant", "content": "hello"},
+                             {"role": "user", "content": "how are you"}])
+        assert sys_["prompt_eval_count"] > base and multi["prompt_eval_count"] > base
+    finally:
+        srv.close()
+    tok = SyntheticTokenizer()  # llama3 template: header per message, open assistant header
+    ids = tok.chat_messages_ids([{"role": "system", "content": "s"}, {"role": "user", "content": "u"}])
+    assert ids[0] == 128000 and ids.count(128006) == 3 and ids.count(128009) == 2
+    assert tok.chat_messages_ids([{"role": "user", "content": "x y"}]) == tok.chat_ids("x y")
+
+
 def test_nodes_with_inprocess_engine():
     """Two native nodes in this process, node B with the engine as its LLM hook."""
     N = load()

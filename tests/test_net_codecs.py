@@ -162,3 +162,12 @@ def test_quic_echo(N, key, size, drop, streams):
     assert rtt > 0  # PING acknowledged
     if drop > 0:
         assert retx > 0
+
+
+@pytest.mark.parametrize("kind,code", [("stream", 3), ("conn", 3), ("crypto", 13)])
+def test_quic_rejects_data_past_advertised_limits(N, kind, code):
+    """RFC 9000 §4 / §7.5: STREAM data past MAX_STREAM_DATA or MAX_DATA closes the
+    connection with FLOW_CONTROL_ERROR (0x03) and CRYPTO data far ahead of the handshake
+    stream with CRYPTO_BUFFER_EXCEEDED (0x0d) -- nothing past the windows is buffered."""
+    closed, why = N.quic_protocol_violation(kind)
+    assert closed and ("code %d" % code) in why, why
