@@ -142,30 +142,35 @@ __global__ __launch_bounds__(NT) void attn_oproj_kernel(
       }
     }
     __syncthreads();
-    for (int i = tid; i < G * HD; i += NT) {
-      const int g = i / HD, d = i % HD;
+    // two dims per thread, one 4-byte write-through (sc1) store each: the hand-off below
+    // needs no release fence (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1)
+    for (int i = tid; i < G * HD / 2; i += NT) {
+      const int g = i / (HD / 2), d = 2 * (i % (HD / 2));
       float M = -INFINITY;
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) M = fmaxf(M, S.sm[ww][g]);
-      float num = 0.f, den = 0.f;
+      float n0 = 0.f, n1 = 0.f, den = 0.f;
       if (M != -INFINITY) {
 #pragma unroll
         for (int ww = 0; ww < WAVES; ++ww) {
           const float e = __expf(S.sm[ww][g] - M);
-          num = fmaf(e, S.so[ww][g][d], num);
+          n0 = fmaf(e, S.so[ww][g][d], n0);
+          n1 = fmaf(e, S.so[ww][g][d + 1], n1);
           den = fmaf(e, S.sl[ww][g], den);
         }
       }
-      attn[(size_t)r * lda + (size_t)(hh * G + g) * HD + d] = f2bf(den > 0.f ? num / den : 0.f);
+      const float inv = den > 0.f ? 1.f / den : 0.f;
+      bf16x2 o2 = {f2bf(n0 * inv), f2bf(n1 * inv)};
+      unsigned bits;
+      __builtin_memcpy(&bits, &o2, 4);
+      __hip_atomic_store(reinterpret_cast<unsigned*>(attn + (size_t)r * lda + (size_t)(hh * G + g) * HD + d),
+                         bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // publish: stores retired -> agent-scope release -> arrival
+    // publish: every storing wave's write-through stores retired -> barrier -> one arrival
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0)
       __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     return;
   }
 
@@ -178,7 +183,9 @@ __global__ __launch_bounds__(NT) void attn_oproj_kernel(
   const bf16x8* wp = Wo + ((size_t)g * Ssteps + (size_t)w * KS) * 64 + lane;
 #pragma unroll
   for (int i = 0; i < KS; ++i) wr[i] = load_nt(wp + (size_t)i * 64);
-  // 2) wait for every attention block (bounded), then acquire
+  // 2) wait for every attention block (bounded): an sc1 poll by one lane, the block's
+  //    other waves behind the barrier; no acquire fence -- every load of the handed-off
+  //    rows below is an sc1 (L1-bypassing) load of write-through-stored data
   if (tid == 0) {
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
@@ -189,18 +196,26 @@ __global__ __launch_bounds__(NT) void attn_oproj_kernel(
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
   // 3) MFMA over the attention rows (A fragment: row lane&15, k 8(lane>>4)..+8)
   const int m = lane & 15;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const bf16* arow = attn + (size_t)(m < R ? m : 0) * lda + (size_t)w * KS * 32 + 8 * (lane >> 4);
+  bf16x8 af[KS];
 #pragma unroll
-  for (int i = 0; i < KS; ++i) {
-    const bf16x8 a = m < R ? *reinterpret_cast<const bf16x8*>(arow + i * 32) : zero_bf16x8();
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wr[i], acc, 0, 0, 0);
+  for (int i = 0; i < KS; ++i) {  // two 8-byte sc1 loads per fragment, all in flight
+    const unsigned long long* p8 = reinterpret_cast<const unsigned long long*>(arow + i * 32);
+    unsigned long long lo = 0, hi = 0;
+    if (m < R) {
+      lo = __hip_atomic_load(p8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      hi = __hip_atomic_load(p8 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    unsigned long long two[2] = {lo, hi};
+    __builtin_memcpy(&af[i], two, 16);
   }
+#pragma unroll
+  for (int i = 0; i < KS; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], wr[i], acc, 0, 0, 0);
   // 4) split-K reduction across the 16 waves, residual epilogue by wave 0
 #pragma unroll
   for (int j = 0; j < 4; ++j) S.red[w][j][lane] = acc[j];
