@@ -136,16 +136,26 @@ def prefill_attn_bench(Ts):
         q = torch.randn(T, nq * 128, device="cuda").to(torch.bfloat16)
         out = torch.empty_like(q)
         pos = list(range(T))
-        tiles = ops.prefill_tiles([0] * T, pos).to("cuda")
+        from p2p_llm_chat_go_amd.ops import attention as A
+
+        res = []
+        for v2 in (True, False):
+            A.FLASH_V2 = v2
+            qt = ops.flash_tile(nq, nkv)
+            tiles = ops.prefill_tiles([0] * T, pos, qt).to("cuda")
+            res.append(("flash_prefill_v2" if v2 else "flash_prefill_v1",
+                        graph_time(lambda i: ops.flash_prefill(q, kc, vc, bt, tiles, nq, nkv,
+                                                               out=out, qtile=qt), n_inner=10)))
+        A.FLASH_V2 = True
         rb = torch.zeros(T, device="cuda", dtype=torch.int32)
         ctx = torch.arange(1, T + 1, device="cuda", dtype=torch.int32)
         ws = ops.attn_workspace(T, nq, T, "cuda")
         flops = 2 * 2 * nq * 128 * T * (T + 1) / 2
-        tf = graph_time(lambda i: ops.flash_prefill(q, kc, vc, bt, tiles, nq, nkv, out=out),
-                        n_inner=10)
-        tr = graph_time(lambda i: ops.paged_attention(q, kc, vc, bt, rb, ctx, nq, nkv, T, out=out,
-                                                      workspace=ws), n_inner=10)
-        for name, t in (("flash_prefill", tf), ("per_row_paged", tr)):
+        if T <= 8192:
+            res.append(("per_row_paged", graph_time(
+                lambda i: ops.paged_attention(q, kc, vc, bt, rb, ctx, nq, nkv, T, out=out,
+                                              workspace=ws), n_inner=10)))
+        for name, t in res:
             print(json.dumps({"prefill_attn_T": T, "kernel": name, "us": round(t, 1),
                               "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1)}), flush=True)
 

@@ -188,7 +188,227 @@ int launch(const bf16* q, int ldq, const bf16* kc, const bf16* vc, const int* bt
   P2P_CHECK_LAUNCH();
 }
 
+// ---------------------------------------------------------------------------------
+// v2: 256 query rows per workgroup (8 waves x 32 rows), one 64-key page per K/V tile,
+// v_mfma_f32_32x32x16_bf16 throughout.
+//
+// A workgroup = one KV head x QT = 256/G consecutive tokens of one sequence; wave w
+// owns q head kvh*G + w/(8/G) and 32 of the tokens, so every K/V page staged in LDS
+// feeds 256 (token, head) rows -- 16x the reuse of v1 (16 tokens x G heads).
+// Per 64-key tile and wave, both products keep the query row on the lane:
+//   S^T[32 keys x 32 rows] = K . Q^T   (per 32-key half: 8 MFMAs over d = 128)
+//   O^T[128 d  x 32 rows] += V^T . P^T (4 d-blocks x 2 halves x 2 k-steps = 16 MFMAs)
+// so the online-softmax statistics and the O rescale are per lane (no cross-lane
+// moves but one xor-32 for the row max / sum).  The S^T accumulator registers are
+// directly the P^T B operand (cdna_hip_programming.md §3 "An accumulator tile as the
+// next MFMA's operand"): register 8s+j of lane half h holds S^T row
+// 16s + 8(j>>2) + 4h + (j&3); the K rows are loaded permuted (row rho <- key
+// kappa(rho)) so that this row is key 16s + 8h + j, i.e. the eight keys a lane
+// contributes to one k-step are CONSECUTIVE -- the V^T A-fragment is then a single
+// 16-byte LDS read of a [d][key] image.  K is staged row-major [key][d] (272-B rows:
+// conflict-free b128 reads), V transposed to [d][key] (144-B rows) while staging.
+// The next page's global loads are issued right after the barrier and land in
+// registers while the MFMAs run (one barrier per tile, two LDS stages).
+constexpr int KLD2 = HD + 8;  // K image row stride (bf16)
+constexpr int VLD2 = 64 + 8;  // V^T image row stride (bf16)
+constexpr int KS_ELEMS = 64 * KLD2, VS_ELEMS = HD * VLD2;
+
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int kperm(int rho) {  // S^T row rho -> key within the 32-key half
+  const int s = rho >> 4, r = rho & 15;
+  return 16 * s + 8 * ((r >> 2) & 1) + 4 * (r >> 3) + (r & 3);
+}
+
+template <int G>
+__global__ __launch_bounds__(512) void flash_prefill2_kernel(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ kc,
+    const bf16* __restrict__ vc, const int* __restrict__ bt, int bt_stride,
+    const Tile* __restrict__ tiles, int n_tiles, int Hkv, float scale_log2,
+    bf16* __restrict__ out, int ldo) {
+  constexpr int WPH = 8 / G;  // waves per q head
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * (KS_ELEMS + VS_ELEMS)];
+
+  // heads outermost, heaviest (latest) tiles first; one head's tiles share an XCD's L2
+  const int nb = n_tiles * Hkv;
+  const int b = xcd_remap(blockIdx.x, nb);
+  const int kvh = b / n_tiles, ti = n_tiles - 1 - b % n_tiles;
+  const Tile T = tiles[ti];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int h = kvh * G + w / WPH;
+  const int t = (w % WPH) * 32 + r32;      // token of this lane's query row
+  const int tok = t < T.n ? t : T.n - 1;
+  const int my_pos = T.pos0 + tok;
+  const int row = T.row0 + tok;
+
+  // Q^T B fragments: k-step s covers d = 16s .. 16s+15, lane half hh holds 8hh .. 8hh+7
+  bf16x8 qf[8];
+  {
+    const bf16* qp = q + (size_t)row * ldq + h * HD + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
+  }
+  f32x16_t o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[db][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  const int last = T.pos0 + T.n - 1;
+  const int n_kt = last / PAGE + 1;
+  const int* btr = bt + (size_t)T.seq * bt_stride;
+  const size_t head_off = (size_t)kvh * PAGE * HD;
+  const size_t page_sz = (size_t)Hkv * PAGE * HD;
+  const int krow = kperm(r32);
+
+  bf16x8 kr[2], vr[2];
+  auto fetch = [&](int kt) {
+    const size_t base = (size_t)btr[kt] * page_sz + head_off;
+    const bf16x8* kp = reinterpret_cast<const bf16x8*>(kc + base);
+    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vc + base);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      kr[i] = kp[tid + 512 * i];
+      vr[i] = vp[tid + 512 * i];
+    }
+  };
+  auto stash = [&](int st) {
+    bf16* Ks = lds + st * (KS_ELEMS + VS_ELEMS);
+    bf16* Vt = Ks + KS_ELEMS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 512 * i, key = c >> 4, d0 = (c & 15) * 8;
+      *reinterpret_cast<bf16x8*>(&Ks[key * KLD2 + d0]) = kr[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Vt[(d0 + j) * VLD2 + key] = vr[i][j];
+    }
+  };
+
+  fetch(0);
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int st = kt & 1;
+    stash(st);
+    __syncthreads();  // this stage is complete; every wave is past tile kt-1 (WAR on st^1)
+    if (kt + 1 < n_kt) fetch(kt + 1);
+    const bf16* Ks = lds + st * (KS_ELEMS + VS_ELEMS);
+    const bf16* Vt = Ks + KS_ELEMS;
+
+    // ---- S^T = K . Q^T, two 32-key halves ----
+    f32x16_t sc[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[kh][i] = 0.f;
+      const bf16* kp = Ks + (32 * kh + krow) * KLD2 + 8 * hh;
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        sc[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            *reinterpret_cast<const bf16x8*>(kp + 16 * s), qf[s], sc[kh], 0, 0, 0);
+    }
+    // ---- online softmax for this lane's query row (keys of reg rr: 16(rr>>3)+8hh+(rr&7)) ----
+    const int k0 = kt * PAGE;
+    const bool diag = k0 + PAGE - 1 > T.pos0;  // some key of the tile may be in the future
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        float v = sc[kh][rr] * scale_log2;
+        if (diag) {
+          const int key = k0 + 32 * kh + 16 * (rr >> 3) + 8 * hh + (rr & 7);
+          v = key <= my_pos ? v : -INFINITY;
+        }
+        sc[kh][rr] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float ps = 0.f;
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const float p = exp2f(sc[kh][rr] - mn);
+        ps += p;
+        pf[kh][rr >> 3][rr & 7] = f2bf(p);
+      }
+    l = l * alpha + ps;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    // ---- O^T += V^T . P^T ----
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const bf16* vp = Vt + (32 * db + r32) * VLD2 + 8 * hh;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              *reinterpret_cast<const bf16x8*>(vp + 32 * kh + 16 * s2), pf[kh][s2], o[db], 0, 0, 0);
+    }
+  }
+
+  l += __shfl_xor(l, 32, 64);
+  if (t < T.n) {
+    const float inv = 1.f / l;
+    bf16* op = out + (size_t)row * ldo + h * HD + 4 * hh;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {  // regs 4g4..4g4+3 = d 32db + 8g4 + 4hh + 0..3
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = f2bf(o[db][4 * g4 + j] * inv);
+        *reinterpret_cast<bf16x4*>(op + 32 * db + 8 * g4) = v;
+      }
+  }
+}
+
+template <int G>
+int launch2(const bf16* q, int ldq, const bf16* kc, const bf16* vc, const int* bt, int bt_stride,
+            const Tile* tiles, int n_tiles, int Hkv, float scale, bf16* out, int ldo,
+            hipStream_t st) {
+  const float sl2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(flash_prefill2_kernel<G>, dim3(n_tiles * Hkv), dim3(512), 0, st, q, ldq, kc,
+                     vc, bt, bt_stride, tiles, n_tiles, Hkv, sl2, out, ldo);
+  P2P_CHECK_LAUNCH();
+}
+
 }  // namespace
+
+// v2 entry: tiles of at most 256 / (Hq/Hkv) tokens (p2p_flash_prefill_tile), otherwise as
+// p2p_flash_prefill.  K/V pages must be whole 64-key pages of the block table.
+P2P_API int p2p_flash_prefill_tile(int Hq, int Hkv) {
+  if (Hkv <= 0 || Hq % Hkv) return 0;
+  const int G = Hq / Hkv;
+  return (G == 1 || G == 2 || G == 4 || G == 8) ? 256 / G : 0;
+}
+
+P2P_API int p2p_flash_prefill2(const void* q, int ldq, const void* kc, const void* vc,
+                               const int* bt, int bt_stride, const int* tiles, int n_tiles,
+                               int Hq, int Hkv, int head_dim, float scale, void* out, int ldo,
+                               void* stream) {
+  if (head_dim != HD || Hkv <= 0 || Hq % Hkv) return 1;
+  if (n_tiles <= 0) return 0;
+  auto Q = (const bf16*)q;
+  auto K = (const bf16*)kc;
+  auto V = (const bf16*)vc;
+  auto T = (const Tile*)tiles;
+  auto O = (bf16*)out;
+  auto st = (hipStream_t)stream;
+  switch (Hq / Hkv) {
+    case 1: return launch2<1>(Q, ldq, K, V, bt, bt_stride, T, n_tiles, Hkv, scale, O, ldo, st);
+    case 2: return launch2<2>(Q, ldq, K, V, bt, bt_stride, T, n_tiles, Hkv, scale, O, ldo, st);
+    case 4: return launch2<4>(Q, ldq, K, V, bt, bt_stride, T, n_tiles, Hkv, scale, O, ldo, st);
+    case 8: return launch2<8>(Q, ldq, K, V, bt, bt_stride, T, n_tiles, Hkv, scale, O, ldo, st);
+    default: return 2;
+  }
+}
 
 // tiles: int32 [n_tiles, 4] = (first row, n tokens <= 16, sequence, first position);
 // a tile's rows are consecutive positions of one sequence whose K/V (positions

@@ -191,13 +191,14 @@ class Engine:
             seq_d, pos_d, ids_d, slots_d, ctx_d = dev_t[0], dev_t[1], dev_t[2], dev_t[3], dev_t[4]
             out_rows = torch.tensor(outs or [0], dtype=torch.int32).to(dev, non_blocking=True)
             greedy = all_logits is None and not sampled
-            tiles = tiles_h = None
+            tiles = tiles_h = qtile = None
             if self.flash_prefill_min and R >= self.flash_prefill_min:
-                tiles_h = ops.prefill_tiles(seq.tolist(), pos.tolist())
+                qtile = ops.flash_tile(self.model.nq, self.model.nkv, R)
+                tiles_h = ops.prefill_tiles(seq.tolist(), pos.tolist(), qtile)
                 tiles = tiles_h.to(dev, non_blocking=True)
             res = self.model.forward(ws, ids_d, pos_d, slots_d, bt_d, seq_d, ctx_d, R,
                                      max_ctx, out_rows=out_rows, n_out=len(outs), greedy=greedy,
-                                     tiles=tiles, tiles_host=tiles_h)
+                                     tiles=tiles, tiles_host=tiles_h, qtile=qtile)
             if not outs:
                 continue
             if greedy:

@@ -133,7 +133,7 @@ class LlamaModel:
 
     def forward(self, ws: Workspace, ids, pos, slots, block_tables, row_bt, ctx_lens, R: int,
                 max_ctx: int, out_rows=None, n_out: int | None = None, greedy: bool = False,
-                tiles=None, tiles_host=None):
+                tiles=None, tiles_host=None, qtile=None):
         """Run all layers on R query rows.
 
         out_rows: int32 [n_out] indices of rows whose logits are needed (prefill:
@@ -162,7 +162,7 @@ class LlamaModel:
             else:
                 if tiles is not None:
                     ops.flash_prefill(q, kc, vc, block_tables, tiles, self.nq, self.nkv, out=attn,
-                                      tiles_host=tiles_host)
+                                      tiles_host=tiles_host, qtile=qtile)
                 else:
                     ops.paged_attention(q, kc, vc, block_tables,
                                         row_bt[:R] if row_bt is not None else None, ctx_lens[:R],

@@ -10,7 +10,7 @@ from .gemm import (EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, Fp8Weight, argmax_fi
                    lm_head_argmax, new_argmax_keys, qkv_rope_gemm, rope_row_perm, skinny_gemm, tile_weight,
                    tiled_shape, untile_weight)
 from .attention import (PAGE, HEAD_DIM, attn_oproj, attn_oproj_ok, attn_workspace,
-                        flash_prefill, paged_attention, prefill_tiles, rope_cache)
+                        flash_prefill, flash_tile, paged_attention, prefill_tiles, rope_cache)
 from .elementwise import advance, argmax, gather_rows
 from .sampling import sample
 from ._lib import available as kernels_available, lib as kernel_lib, lib_path as kernel_lib_path
@@ -18,7 +18,7 @@ from ._lib import available as kernels_available, lib as kernel_lib, lib_path as
 __all__ = [
     "EPI_F32", "EPI_RESID", "EPI_SILU", "EPI_STORE", "fold_norm", "skinny_gemm", "tile_weight",
     "tiled_shape", "untile_weight", "argmax_finalize", "lm_head_argmax", "new_argmax_keys", "qkv_rope_gemm",
-    "rope_row_perm", "PAGE", "HEAD_DIM", "attn_workspace", "paged_attention", "flash_prefill", "prefill_tiles",
+    "rope_row_perm", "PAGE", "HEAD_DIM", "attn_workspace", "paged_attention", "flash_prefill", "flash_tile", "prefill_tiles",
     "attn_oproj", "attn_oproj_ok",
     "rope_cache", "sample", "advance", "argmax", "gather_rows", "kernels_available", "kernel_lib",
     "kernel_lib_path",

@@ -38,6 +38,9 @@ _SIGS = {
                             c_void_p, c_void_p, c_void_p],
     "p2p_flash_prefill": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                           c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
+    "p2p_flash_prefill2": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                           c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
+    "p2p_flash_prefill_tile": [c_int, c_int],
     "p2p_car_alloc": [ctypes.c_size_t, c_void_p],
     "p2p_car_free": [c_void_p],
     "p2p_car_get_handle": [c_void_p, c_void_p],

@@ -9,6 +9,7 @@ prefill (one row per prompt token) share one kernel.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -119,6 +120,25 @@ def attn_oproj(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_k
 
 
 QTILE = 16
+# v2 flash prefill (256 query rows per workgroup, 32x32x16 MFMA); P2P_FLASH_V2=0 selects v1
+FLASH_V2 = os.environ.get("P2P_FLASH_V2", "1") != "0"
+
+
+# v2 pays from about this many (query tile, kv head) workgroups; below it the 16-token
+# v1 tiles spread a short prompt over more CUs (profiles/r2_flash_prefill_v2.jsonl:
+# T=512 v1 27 us vs v2 40 us; T=2048 v2 138 us vs v1 236 us)
+FLASH_V2_MIN_BLOCKS = 128
+
+
+def flash_tile(n_heads: int, n_kv: int, rows: int | None = None) -> int:
+    """Tokens per query tile for a prefill chunk of ``rows`` tokens: v2 (256 / (Hq/Hkv))
+    when it yields enough workgroups, else v1 (16)."""
+    G = n_heads // n_kv
+    if FLASH_V2 and G in (1, 2, 4, 8):
+        t = 256 // G
+        if rows is None or -(-rows // t) * n_kv >= FLASH_V2_MIN_BLOCKS:
+            return t
+    return QTILE
 
 
 def prefill_tiles(seq, pos, tile: int = QTILE) -> torch.Tensor:
@@ -144,12 +164,16 @@ def prefill_tiles(seq, pos, tile: int = QTILE) -> torch.Tensor:
 def flash_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                   block_tables: torch.Tensor, tiles: torch.Tensor, n_heads: int, n_kv: int,
                   out: torch.Tensor | None = None, scale: float | None = None,
-                  tiles_host: torch.Tensor | None = None) -> torch.Tensor:
+                  tiles_host: torch.Tensor | None = None, qtile: int | None = None) -> torch.Tensor:
     """Causal prefill attention on MFMA for query tiles (see ``prefill_tiles``).
 
     Equivalent to :func:`paged_attention` with one row per prompt token
-    (ctx = pos + 1), but reads each K/V tile once per 16 tokens x G heads.
+    (ctx = pos + 1), but reads each K/V page once per query tile x G heads.  The
+    tiles must come from ``prefill_tiles(seq, pos, qtile)`` with ``qtile`` from
+    ``flash_tile`` (default ``flash_tile(n_heads, n_kv)``): > 16 runs the v2 kernel.
     """
+    if qtile is None:
+        qtile = flash_tile(n_heads, n_kv)
     R = q.shape[0]
     if scale is None:
         scale = 1.0 / math.sqrt(HEAD_DIM)
@@ -165,7 +189,8 @@ def flash_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         return paged_attention_ref(q, k_cache, v_cache, block_tables, row_bt, ctx, n_heads, n_kv,
                                    scale, out)
     L = _lib.lib()
-    _lib.check(L.p2p_flash_prefill(q.data_ptr(), q.stride(0), k_cache.data_ptr(),
+    fn = L.p2p_flash_prefill2 if qtile > QTILE else L.p2p_flash_prefill
+    _lib.check(fn(q.data_ptr(), q.stride(0), k_cache.data_ptr(),
                                    v_cache.data_ptr(), block_tables.data_ptr(),
                                    block_tables.stride(0), tiles.data_ptr(), tiles.shape[0],
                                    n_heads, n_kv, HEAD_DIM, float(scale), out.data_ptr(),

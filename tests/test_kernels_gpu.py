@@ -249,11 +249,15 @@ def test_attn_oproj_fused(R, Hkv, G, ctxs):
 
 
 # ------------------------------------------------------- flash prefill (MFMA)
+@pytest.mark.parametrize("v2", [True, False])
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
-@pytest.mark.parametrize("lens", [[(0, 5)], [(0, 37), (0, 16)], [(100, 70), (0, 300), (3, 1)]])
-def test_flash_prefill(G, lens):
+@pytest.mark.parametrize("lens", [[(0, 5)], [(0, 37), (0, 16)], [(100, 70), (0, 300), (3, 1)],
+                                  [(0, 600), (130, 257)]])
+def test_flash_prefill(G, lens, v2, monkeypatch):
     """Causal prefill vs the fp32 reference; (start, n) per sequence, start > 0
-    = a chunk continuing a prompt whose earlier K/V is already cached."""
+    = a chunk continuing a prompt whose earlier K/V is already cached.  v2 = the
+    256-row / 64-key-page MFMA kernel, v1 = the 16-token kernel."""
+    monkeypatch.setattr(A, "FLASH_V2", v2)
     torch.manual_seed(G * 13 + len(lens))
     Hkv = 2
     Hq = Hkv * G
@@ -273,11 +277,13 @@ def test_flash_prefill(G, lens):
     ctx = torch.tensor(pos, dtype=torch.int32) + 1
     ref = A.paged_attention_ref(q, k, v, bt, row_bt, ctx, Hq, Hkv, 1 / math.sqrt(128),
                                 torch.empty(R, Hq * 128, dtype=torch.float32))
-    tiles = ops.prefill_tiles(seq, pos)
-    assert int(tiles[:, 1].sum()) == R and int(tiles[:, 1].max()) <= 16
+    qt = ops.flash_tile(Hq, Hkv)
+    assert qt == (256 // G if v2 else 16)
+    tiles = ops.prefill_tiles(seq, pos, qt)
+    assert int(tiles[:, 1].sum()) == R and int(tiles[:, 1].max()) <= qt
     out = torch.full((R, Hq * 128), float("nan"), dtype=torch.bfloat16, device=DEV)
     ops.flash_prefill(q.to(DEV), k.to(DEV), v.to(DEV), bt.to(DEV), tiles.to(DEV), Hq, Hkv,
-                      out=out)
+                      out=out, qtile=qt)
     torch.cuda.synchronize()
     assert not out.isnan().any()
     assert _rel(out.cpu(), ref) < 1e-2
