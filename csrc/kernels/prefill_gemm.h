@@ -53,7 +53,11 @@ __device__ __forceinline__ void wait_tiles(int pending) {
   wait_vmcnt<0>();
 }
 
-template <int BM, int BN, int EPI, bool NORM, bool SPLIT, int STAGES>
+// MOE: grouped expert GEMM (ea.moe_*): blockIdx.y = local expert e, whose rows are the
+// slots rows[e][i] (i < min(cnt[e], M)); A row of slot s = X[s / x_div], output row s
+// (scaled by row_w[s]).  m-tiles past the expert's count exit at once, so one launch
+// covers every expert at any M and each expert's weights stream once per m-tile.
+template <int BM, int BN, int EPI, bool NORM, bool SPLIT, int STAGES, bool MOE = false>
 __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restrict__ Wt,
                                                           const bf16* __restrict__ X, int ldx,
                                                           int M, int K, int m_tiles, int n_tiles,
@@ -78,6 +82,14 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   const int tile = b / splitk, split = b % splitk;
   const int mt_i = tile % m_tiles, nt_i = tile / m_tiles;
   const int m0 = mt_i * BM;
+  const int* mrows = nullptr;
+  if constexpr (MOE) {
+    const int e = blockIdx.y;
+    M = min(ea.moe_cnt[e], M);
+    if (m0 >= M) return;  // block-uniform: this expert has fewer rows
+    Wt += (size_t)e * ea.w_stride;
+    mrows = ea.moe_rows + (size_t)e * ea.rows_stride;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;
   const int S = K >> 5;
@@ -101,6 +113,7 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
     const int mi = blk >> 1, ks = blk & 1;
     int row = m0 + 16 * mi + (lane & 15);
     row = row < M ? row : M - 1;
+    if constexpr (MOE) row = mrows[row] / ea.x_div;
     asrc[i] = X + (size_t)row * ldx + 32 * ks + 8 * (lane >> 4);
   }
   const bf16x8* bsrc[BI];
@@ -260,10 +273,14 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int rl = wm * (BM / 2) + 16 * i + 4 * q + jj;
-      const int m = m0 + rl;
+      int m = m0 + rl;
       const bool valid = m < M;
       float scale = 1.f;
       if constexpr (NORM) scale = rsqrtf(ss_row[rl] / (float)K + eps);
+      if constexpr (MOE) {
+        m = valid ? mrows[m] : 0;  // output row = the slot
+        if (ea.row_w && valid) scale *= ea.row_w[m];
+      }
       if constexpr (EPI == EPI_SILU) {
         constexpr int H = FN / 2;
 #pragma unroll
@@ -369,6 +386,19 @@ int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_o
   hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, false, STAGES>), dim3(tiles), dim3(NT), 0,
                      st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off,
                      out, ldo, eps, ea, none);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int EPI, bool NORM>
+int launch_moe(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off, void* out,
+               int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
+  constexpr int STAGES = stages_for<BM, BN>();
+  const int m_tiles = (M + BM - 1) / BM;
+  const int n_tiles = N / BN;
+  SplitArgs none{1, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, false, STAGES, true>),
+                     dim3(m_tiles * n_tiles, ea.n_experts), dim3(NT), 0, st, (const bf16x8*)Wt,
+                     (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, none);
   return (int)hipGetLastError();
 }
 

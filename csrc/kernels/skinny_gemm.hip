@@ -525,6 +525,13 @@ P2P_API int p2p_skinny_gemm_qkv_rope(const void* Wt, const void* X, int ldx, int
   return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_QKV_ROPE, 1, nullptr, 0, eps, waves, ea, stream);
 }
 
+// tiled_gemm.hip: the grouped mode of the LDS-tiled MFMA kernel (rows > 64)
+extern "C" int p2p_grouped_gemm_tiled(const void* Wt, long long w_stride, int n_experts,
+                                      const int* cnt, const int* rows, int rows_stride, int x_div,
+                                      const float* row_w, const void* X, int ldx, int max_rows,
+                                      int K, int N, int epi, int norm, void* out, int ldo, float eps,
+                                      hipStream_t stream);
+
 // Grouped (MoE) projection over the local experts (blockIdx.y = expert):
 //   expert e multiplies rows slot = rows[e*rows_stride + i] (i < cnt[e], <= max_rows) of
 //   X (row slot / x_div) with its weights (Wt + e*w_stride) and writes output row slot.
@@ -535,6 +542,9 @@ P2P_API int p2p_grouped_gemm(const void* Wt, long long w_stride, int n_experts, 
                              void* out, int ldo, float eps, int waves, hipStream_t stream) {
   if (n_experts <= 0 || !cnt || !rows) return (int)hipErrorInvalidValue;
   if (epi != EPI_STORE && epi != EPI_SILU) return (int)hipErrorInvalidValue;
+  if (max_rows > 64)  // prefill / big batches: the LDS-tiled MFMA kernel, grouped mode
+    return p2p_grouped_gemm_tiled(Wt, w_stride, n_experts, cnt, rows, rows_stride, x_div, row_w,
+                                  X, ldx, max_rows, K, N, epi, norm, out, ldo, eps, stream);
   EpiArgs ea = {};
   ea.moe_cnt = cnt;
   ea.moe_rows = rows;

@@ -273,3 +273,34 @@ P2P_API int p2p_tiled_gemm_argmax(const void* Wt, const void* X, int ldx, int M,
   ea.col_offset = col_offset;
   return tiled_dispatch(Wt, X, ldx, M, K, N, EPI_ARGMAX, 1, keys, 0, eps, ea, stream);
 }
+
+// Grouped (MoE) expert GEMM on the LDS-tiled MFMA kernel (prefill_gemm.h, MOE mode):
+// one launch, grid (m-tiles x n-tiles, experts); see p2p_grouped_gemm for the
+// arguments.  Every expert's weights stream once per m-tile of its own rows.
+P2P_API int p2p_grouped_gemm_tiled(const void* Wt, long long w_stride, int n_experts,
+                                   const int* cnt, const int* rows, int rows_stride, int x_div,
+                                   const float* row_w, const void* X, int ldx, int max_rows,
+                                   int K, int N, int epi, int norm, void* out, int ldo, float eps,
+                                   hipStream_t stream) {
+  using namespace pgemm;
+  if (n_experts <= 0 || max_rows <= 0 || K % pgemm::BK || N % 128) return (int)hipErrorInvalidValue;
+  EpiArgs ea = {};
+  ea.moe_cnt = cnt;
+  ea.moe_rows = rows;
+  ea.rows_stride = rows_stride;
+  ea.x_div = x_div > 0 ? x_div : 1;
+  ea.row_w = row_w;
+  ea.w_stride = w_stride;
+  ea.n_experts = n_experts;
+  if (epi == EPI_SILU) {
+    if (!norm || N % 256) return (int)hipErrorInvalidValue;
+    return launch_moe<128, 128, EPI_SILU, true>(Wt, X, ldx, max_rows, K, N, N / 32, out, ldo, eps,
+                                                ea, stream);
+  }
+  if (epi == EPI_STORE)
+    return norm ? launch_moe<128, 128, EPI_STORE, true>(Wt, X, ldx, max_rows, K, N, 0, out, ldo,
+                                                        eps, ea, stream)
+                : launch_moe<128, 128, EPI_STORE, false>(Wt, X, ldx, max_rows, K, N, 0, out, ldo,
+                                                         eps, ea, stream);
+  return (int)hipErrorInvalidValue;
+}

@@ -1,6 +1,7 @@
 """Mixtral sparse-MoE FFN on the engine kernels (replaces the dense SwiGLU MLP).
 
-Per layer, for R rows (chunks of <= 64 rows, the grouped kernel's M tile):
+Per layer, for R rows (chunks of <= 64 rows on the skinny grouped kernel; above 64 rows
+all rows at once on the LDS-tiled grouped kernel, ``moe_forward_tiled``):
     ids, w = top_k(softmax(rstd(h) h Wr'))   moe_router_route (+ per-expert slot lists)
     act[s] = silu(g) * u of expert(s)        grouped_gemm SILU | NORM
     o[s]   = w[s] * act[s] @ W2_e            grouped_gemm STORE (row-scaled)
@@ -19,12 +20,17 @@ Expert parallelism, two modes:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
 from ..ops import moe as moe_ops
 
 CHUNK = 64
+# rows above which a layer routes all rows at once onto the tiled grouped kernel
+# (P2P_MOE_TILED_MIN=100000 keeps the 64-row skinny chunks, for A/B measurements)
+TILED_MIN = int(os.environ.get("P2P_MOE_TILED_MIN", str(CHUNK + 1)))
 
 
 class MoeWorkspace:
@@ -57,6 +63,8 @@ def moe_forward(model, lw, ws, R):
     w = model.w
     if w.ep_size > 1 and getattr(model, "ep_mode", "allreduce") == "a2a":
         return moe_forward_a2a(model, lw, ws, R)
+    if R >= TILED_MIN:
+        return moe_forward_tiled(model, lw, ws, R)
     e_local = cfg.n_experts // w.ep_size
     e_lo = w.ep_rank * e_local
     if ws.moe is None:
@@ -80,6 +88,37 @@ def moe_forward(model, lw, ws, R):
             part = ws.partial[r0:r0 + rc]
             moe_ops.moe_combine(m.o, m.topk_ids, rc, K, e_lo, e_local, part, accumulate=False)
             model.comm.allreduce_add_(h, part)
+
+
+def moe_forward_tiled(model, lw, ws, R):
+    """Prefill / large batches (R > 64 rows): route all R rows at once, then each expert's
+    gate_up and down run as ONE grouped launch of the LDS-tiled MFMA kernel over its own
+    rows (``ops.moe.grouped_gemm`` with max_rows > 64), so every selected expert's weights
+    stream once per 128-row tile of its rows -- not once per 64-row chunk of the prompt."""
+    cfg, w = model.cfg, model.w
+    E, K = cfg.n_experts, cfg.top_k
+    e_local = E // w.ep_size
+    e_lo = w.ep_rank * e_local
+    m = getattr(ws, "moe_big", None)
+    if m is None:
+        m = ws.moe_big = MoeWorkspace(cfg, ws.max_rows, model.device, e_local,
+                                      lw.w13.shape[1] * 16 // 2)
+    h = ws.h[:R]
+    rt = router_tiled(lw)
+    for r0 in range(0, R, CHUNK):
+        rc = min(CHUNK, R - r0)
+        ops.skinny_gemm(rt, h[r0:r0 + rc], ops.EPI_F32, norm=True, out=m.logits[r0:r0 + rc],
+                        eps=cfg.eps)
+    moe_ops.moe_route(m.logits[:R], E, K, e_lo, e_local, m.topk_ids, m.topk_w, m.cnt, m.rows)
+    moe_ops.grouped_gemm(lw.w13, m.cnt, m.rows, h, K, R, ops.EPI_SILU, m.act, norm=True,
+                         eps=cfg.eps)
+    moe_ops.grouped_gemm(lw.w2, m.cnt, m.rows, m.act, 1, R, ops.EPI_STORE, m.o, row_w=m.topk_w)
+    if not (w.ep_size > 1 or w.tp_size > 1):
+        moe_ops.moe_combine(m.o, m.topk_ids, R, K, e_lo, e_local, h, accumulate=True)
+    else:
+        part = ws.partial[:R]
+        moe_ops.moe_combine(m.o, m.topk_ids, R, K, e_lo, e_local, part, accumulate=False)
+        model.comm.allreduce_add_(h, part)
 
 
 def moe_forward_a2a(model, lw, ws, R):
@@ -127,12 +166,11 @@ def moe_forward_a2a(model, lw, ws, R):
     Fs = lw.w13.shape[1] * 16 // 2
     act = torch.empty(n, Fs, device=dev, dtype=torch.bfloat16)
     o = torch.zeros(n, H, device=dev, dtype=torch.bfloat16)
-    for c0 in range(0, n, CHUNK):
-        cnt = (counts - c0).clamp(0, CHUNK).to(torch.int32)
-        rc = rows[:, c0:c0 + CHUNK]
-        moe_ops.grouped_gemm(lw.w13, cnt, rc, recv_x, 1, CHUNK, ops.EPI_SILU, act, norm=True,
-                             eps=cfg.eps)
-        moe_ops.grouped_gemm(lw.w2, cnt, rc, act, 1, CHUNK, ops.EPI_STORE, o, row_w=row_w)
+    # one grouped launch per projection over every received row (tiled kernel above 64)
+    cnt = counts.to(torch.int32)
+    moe_ops.grouped_gemm(lw.w13, cnt, rows, recv_x, 1, n, ops.EPI_SILU, act, norm=True,
+                         eps=cfg.eps)
+    moe_ops.grouped_gemm(lw.w2, cnt, rows, act, 1, n, ops.EPI_STORE, o, row_w=row_w)
     back = torch.empty_like(o)
     comm.all_to_all_(back, o)
     contrib = back.index_select(0, slot).float().view(R, K, H).sum(1)

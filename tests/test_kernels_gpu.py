@@ -428,8 +428,12 @@ def test_moe_router_route_fused(R, E, K, e_lo, e_local):
 
 
 
-@pytest.mark.parametrize("R,E,K,e_lo,e_local", [(1, 8, 2, 0, 8), (13, 8, 2, 0, 8), (64, 8, 2, 4, 4)])
+@pytest.mark.parametrize("R,E,K,e_lo,e_local", [(1, 8, 2, 0, 8), (13, 8, 2, 0, 8), (64, 8, 2, 4, 4),
+                                                 (65, 8, 2, 0, 8), (300, 8, 2, 0, 8),
+                                                 (517, 8, 2, 2, 2), (200, 4, 1, 0, 4)])
 def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
+    """R > 64 runs the grouped mode of the LDS-tiled MFMA kernel (one launch over every
+    expert's rows), R <= 64 the skinny grouped kernel."""
     from p2p_llm_chat_go_amd.ops import moe as M
 
     torch.manual_seed(R + E)
