@@ -53,32 +53,49 @@ __device__ __forceinline__ float uniform01(unsigned long long seed, int pos, int
   return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
 }
 
-template <typename F>
-__device__ __forceinline__ void for_each_key(const float* __restrict__ row, int V, bool vec, F f) {
-  if (vec) {
-    const float4* r4 = reinterpret_cast<const float4*>(row);
-    for (int i = threadIdx.x; i < (V >> 2); i += THREADS) {
-      const float4 x = r4[i];
-      f(4 * i + 0, x.x);
-      f(4 * i + 1, x.y);
-      f(4 * i + 2, x.z);
-      f(4 * i + 3, x.w);
-    }
-  } else {
-    for (int i = threadIdx.x; i < V; i += THREADS) f(i, row[i]);
-  }
-}
+// Entry sources of one row: a dense logits row (ids = column + id_off), or -- vocab-
+// parallel TP -- the gathered per-shard candidates: entry i of row r is slot i % seg of
+// segment i / seg (one per rank), at vals/ids[(i / seg) * seg_stride + r * seg + i % seg].
+struct Src {
+  const float* vals;
+  const int* ids;  // null: dense row
+  int ld, seg;
+  long long seg_stride;
+  int id_off;
+};
 
 __global__ __launch_bounds__(THREADS) void sample_kernel(
-    const float* __restrict__ logits, int ld, int V, const float* __restrict__ temp,
+    Src src, int V, const float* __restrict__ temp,
     const int* __restrict__ topk, const float* __restrict__ topp,
     const unsigned long long* __restrict__ seeds, const int* __restrict__ pos,
-    int* __restrict__ out) {
+    int* __restrict__ out, float* __restrict__ cand_v, int* __restrict__ cand_id) {
+  // cand_v != null: emit mode -- write this row's top-KMAX (value, id) pairs, sorted
+  // (descending value, ascending id; padding -inf / INT_MAX) instead of drawing
   const int r = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float* row = logits + (size_t)r * ld;
-  const bool vec = ((ld | V) & 3) == 0;
-  const float T = temp[r];
+  const bool emit = cand_v != nullptr;
+  const float* row = src.vals + (size_t)r * src.ld;
+  const bool vec = !src.ids && ((src.ld | V) & 3) == 0;
+  const float T = emit ? 1.f : temp[r];
+  auto for_each_key = [&](const float* __restrict__, int, bool, auto&& f) {
+    if (src.ids) {
+      for (int i = threadIdx.x; i < V; i += THREADS) {
+        const size_t o = (size_t)(i / src.seg) * src.seg_stride + (size_t)r * src.seg + i % src.seg;
+        f(src.ids[o], src.vals[o]);
+      }
+    } else if (vec) {
+      const float4* r4 = reinterpret_cast<const float4*>(row);
+      for (int i = threadIdx.x; i < (V >> 2); i += THREADS) {
+        const float4 x = r4[i];
+        f(src.id_off + 4 * i + 0, x.x);
+        f(src.id_off + 4 * i + 1, x.y);
+        f(src.id_off + 4 * i + 2, x.z);
+        f(src.id_off + 4 * i + 3, x.w);
+      }
+    } else {
+      for (int i = threadIdx.x; i < V; i += THREADS) f(src.id_off + i, row[i]);
+    }
+  };
 
   __shared__ int hist[NWAVES][256];
   __shared__ float cv[KMAX];
@@ -112,7 +129,7 @@ __global__ __launch_bounds__(THREADS) void sample_kernel(
     return;
   }
 
-  int k = topk[r];
+  int k = emit ? KMAX : topk[r];
   if (k <= 0 || k > KMAX) k = KMAX;
   if (k > V) k = V;
 
@@ -282,6 +299,14 @@ __global__ __launch_bounds__(THREADS) void sample_kernel(
     }
   }
 
+  if (emit) {
+    if (tid < KMAX) {
+      cand_v[(size_t)r * KMAX + tid] = cv[tid];
+      cand_id[(size_t)r * KMAX + tid] = ci[tid];
+    }
+    return;
+  }
+
   // ---- 4 + 5. softmax / top-p / exponential race, wave 0 (2 slots per lane) ----
   if (w == 0) {
     const float vmax = cv[0];
@@ -339,7 +364,37 @@ P2P_API int p2p_sample(const float* logits, int ld, int B, int V, const float* t
                        const int* topk, const float* topp, const unsigned long long* seeds,
                        const int* pos, int* ids, hipStream_t st) {
   if (B <= 0 || V <= 0 || ld < V) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(THREADS), 0, st, logits, ld, V, temp, topk, topp,
-                     seeds, pos, ids);
+  Src src{logits, nullptr, ld, 0, 0, 0};
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(THREADS), 0, st, src, V, temp, topk, topp,
+                     seeds, pos, ids, (float*)nullptr, (int*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// Vocab-parallel sampling, step 1 (every TP rank, its logits shard [B, V] at columns
+// id_off ..): the shard's top-128 (value, global id) pairs per row, sorted, into
+// cand_v / cand_id [B][128].  The global top-k (k <= 128, the sampler's cap) of a row is
+// contained in the union of the shards' sets, ties included (lowest ids first).
+P2P_API int p2p_topk_candidates(const float* logits, int ld, int B, int V, int id_off,
+                                float* cand_v, int* cand_id, hipStream_t st) {
+  if (B <= 0 || V <= 0 || ld < V || !cand_v || !cand_id) return (int)hipErrorInvalidValue;
+  Src src{logits, nullptr, ld, 0, 0, id_off};
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(THREADS), 0, st, src, V, (const float*)nullptr,
+                     (const int*)nullptr, (const float*)nullptr,
+                     (const unsigned long long*)nullptr, (const int*)nullptr, (int*)nullptr,
+                     cand_v, cand_id);
+  return (int)hipGetLastError();
+}
+
+// Step 2 (after the all-gather of every rank's candidates, rank-major [W][B][128]):
+// the same draw as p2p_sample over the full vocabulary row -- identical token for
+// the same (seed, position), since only ids in the union can be drawn.
+P2P_API int p2p_sample_candidates(const float* cand_v, const int* cand_id, int W, int B,
+                                  const float* temp, const int* topk, const float* topp,
+                                  const unsigned long long* seeds, const int* pos, int* ids,
+                                  hipStream_t st) {
+  if (B <= 0 || W <= 0) return (int)hipErrorInvalidValue;
+  Src src{cand_v, cand_id, 0, KMAX, (long long)B * KMAX, 0};
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(THREADS), 0, st, src, W * KMAX, temp, topk,
+                     topp, seeds, pos, ids, (float*)nullptr, (int*)nullptr);
   return (int)hipGetLastError();
 }

@@ -204,11 +204,16 @@ class Engine:
             if greedy:
                 toks = self.model.finalize_greedy(ws, len(outs))
             elif sampled:
-                from .sampling import sample
+                from .sampling import sample, sample_tp
 
-                full = res if self.model.tp == 1 else self.model.comm.all_gather_cols(res)
-                toks = sample(full, [sampling[b] for b in out_seq],
-                              [len(prompts[b]) - 1 for b in out_seq])
+                params = [sampling[b] for b in out_seq]
+                spos = [len(prompts[b]) - 1 for b in out_seq]
+                if self.model.tp == 1:
+                    toks = sample(res, params, spos)
+                elif getattr(self.model, "sample_full_gather", False):  # reference path (tests)
+                    toks = sample(self.model.comm.all_gather_cols(res), params, spos)
+                else:
+                    toks = sample_tp(self.model, res, params, spos)
             else:
                 toks = self.model.sample_greedy(ws, res)
             sel = torch.tensor(out_seq, dtype=torch.long).to(dev, non_blocking=True)

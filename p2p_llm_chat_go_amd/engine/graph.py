@@ -41,6 +41,12 @@ class DecodeState:
         from .sampling import SamplerSlots
 
         self.samp = SamplerSlots(B, dev)  # sampled graphs read these (ops.sample)
+        if model.tp > 1:  # vocab-parallel sampling: per-shard top-128 candidates, gathered
+            W = model.tp
+            self.cand_v = torch.empty(B, 128, device=dev, dtype=torch.float32)
+            self.cand_id = torch.empty(B, 128, device=dev, dtype=torch.int32)
+            self.cand_all_v = torch.empty(W * B, 128, device=dev, dtype=torch.float32)
+            self.cand_all_id = torch.empty(W * B, 128, device=dev, dtype=torch.int32)
 
     def reset_dummy(self):
         self.ids.zero_()
@@ -84,10 +90,22 @@ class DecodeState:
         self.body_logits()
         logits = self.ws.logits[:self.B]
         m = self.model
-        if m.tp > 1:  # vocab-parallel LM head: every rank samples the full row identically
-            logits = m.comm.all_gather_cols(logits)
         sp = self.samp
-        ops.sample(logits, sp.temp, sp.topk, sp.topp, sp.seeds, self.pos, out=self.ids)
+        if m.tp > 1 and getattr(m, "sample_full_gather", False):  # reference path (tests)
+            full = m.comm.all_gather_cols(logits)
+            ops.sample(full, sp.temp, sp.topk, sp.topp, sp.seeds, self.pos, out=self.ids)
+        elif m.tp > 1:
+            # vocab-parallel LM head: each rank keeps its shard's top-128 (value, id) pairs,
+            # one all-gather of B x world x 128 candidates (not B x V logits), and every rank
+            # draws the same token as the unsharded sampler (the draw is capped at top-128)
+            ops.topk_candidates(logits, m.w.tp_rank * (m.cfg.vocab // m.tp), self.cand_v,
+                                self.cand_id)
+            m.comm.all_gather_rows_into(self.cand_all_v, self.cand_v)
+            m.comm.all_gather_rows_into(self.cand_all_id, self.cand_id)
+            ops.sample_candidates(self.cand_all_v, self.cand_all_id, m.tp, sp.temp, sp.topk,
+                                  sp.topp, sp.seeds, self.pos, out=self.ids)
+        else:
+            ops.sample(logits, sp.temp, sp.topk, sp.topp, sp.seeds, self.pos, out=self.ids)
         self.advance()
 
     def body(self):

@@ -90,3 +90,28 @@ def sample(logits: torch.Tensor, params: list, pos) -> torch.Tensor:
     seeds = torch.tensor([p.resolved_seed() for p in params], dtype=torch.int64).to(dev)
     pos = torch.as_tensor(pos, dtype=torch.int32).to(dev)
     return ops.sample(logits, temp, topk, topp, seeds, pos)
+
+
+def sample_tp(model, logits: torch.Tensor, params: list, pos) -> torch.Tensor:
+    """Vocab-parallel ``sample`` (TP prefill): per-shard top-128 candidates, one all-gather,
+    then the same draw on every rank (see DecodeState.body_sampled)."""
+    from .. import ops
+
+    B = logits.shape[0]
+    params = list(params[:B]) + [SamplingParams()] * (B - len(params))
+    dev = logits.device
+    W = model.tp
+    temp = torch.tensor([p.temperature for p in params], dtype=torch.float32).to(dev)
+    topk = torch.tensor([p.top_k for p in params], dtype=torch.int32).to(dev)
+    topp = torch.tensor([p.top_p for p in params], dtype=torch.float32).to(dev)
+    seeds = torch.tensor([p.resolved_seed() for p in params], dtype=torch.int64).to(dev)
+    posd = torch.tensor(list(pos), dtype=torch.int32).to(dev)
+    cv = torch.empty(B, 128, device=dev, dtype=torch.float32)
+    ci = torch.empty(B, 128, device=dev, dtype=torch.int32)
+    ops.topk_candidates(logits, model.w.tp_rank * (model.cfg.vocab // W), cv, ci)
+    av = torch.empty(W * B, 128, device=dev, dtype=torch.float32)
+    ai = torch.empty(W * B, 128, device=dev, dtype=torch.int32)
+    model.comm.all_gather_rows_into(av, cv)
+    model.comm.all_gather_rows_into(ai, ci)
+    out = torch.empty(B, dtype=torch.int32, device=dev)
+    return ops.sample_candidates(av, ai, W, temp, topk, topp, seeds, posd, out)

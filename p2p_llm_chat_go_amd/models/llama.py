@@ -81,6 +81,9 @@ class LlamaModel:
         self.overlap_min_rows = int(os.environ.get("P2P_TP_OVERLAP_MIN_ROWS", "256"))
         self.overlap_chunks = int(os.environ.get("P2P_TP_OVERLAP_CHUNKS", "4"))
         self._comm_stream = None
+        # TP sampling reference path: gather the full logits row instead of per-shard top-128
+        # candidates (same draw; tests compare the two on the same sharded numerics)
+        self.sample_full_gather = False
 
     def new_workspace(self, max_rows, max_ctx, max_out_rows=None) -> Workspace:
         return Workspace(self.cfg, max_rows, max_ctx, self.device, self.tp, max_out_rows)

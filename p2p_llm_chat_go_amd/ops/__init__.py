@@ -12,7 +12,7 @@ from .gemm import (EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, Fp8Weight, argmax_fi
 from .attention import (PAGE, HEAD_DIM, attn_oproj, attn_oproj_ok, attn_workspace,
                         flash_prefill, flash_tile, paged_attention, prefill_tiles, rope_cache)
 from .elementwise import advance, argmax, gather_rows
-from .sampling import sample
+from .sampling import sample, sample_candidates, topk_candidates
 from ._lib import available as kernels_available, lib as kernel_lib, lib_path as kernel_lib_path
 
 __all__ = [
@@ -20,6 +20,6 @@ __all__ = [
     "tiled_shape", "untile_weight", "argmax_finalize", "lm_head_argmax", "new_argmax_keys", "qkv_rope_gemm",
     "rope_row_perm", "PAGE", "HEAD_DIM", "attn_workspace", "paged_attention", "flash_prefill", "flash_tile", "prefill_tiles",
     "attn_oproj", "attn_oproj_ok",
-    "rope_cache", "sample", "advance", "argmax", "gather_rows", "kernels_available", "kernel_lib",
+    "rope_cache", "sample", "sample_candidates", "topk_candidates", "advance", "argmax", "gather_rows", "kernels_available", "kernel_lib",
     "kernel_lib_path",
 ]

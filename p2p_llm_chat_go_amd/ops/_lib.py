@@ -71,6 +71,9 @@ _SIGS = {
                                  c_int, c_void_p, c_void_p],
     "p2p_sample": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                    c_void_p, c_void_p],
+    "p2p_topk_candidates": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "p2p_sample_candidates": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p],
     "p2p_tiled_gemm": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                        c_int, c_float, c_void_p],
     "p2p_tiled_gemm_qkv_rope": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,

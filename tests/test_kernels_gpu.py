@@ -575,6 +575,41 @@ def test_sample_kernel_matches_reference(V):
     assert agree >= B - 2, (agree, B)
 
 
+@pytest.mark.parametrize("W", [2, 8])
+def test_vocab_parallel_sampling_matches_full_row(W):
+    """TP sampling: per-shard top-128 candidates (p2p_topk_candidates) + the draw over the
+    gathered candidates (p2p_sample_candidates) pick exactly the token p2p_sample picks
+    from the whole row -- same keep set, same (seed, pos, id) random numbers."""
+    from p2p_llm_chat_go_amd.ops import sampling as S
+
+    torch.manual_seed(W)
+    B, V = 24, 1024 * W
+    lg = torch.randn(B, V) * 3
+    lg[3, :300] = 6.0  # a top tie spanning shards
+    lg[4] = torch.round(lg[4])
+    temp = torch.tensor([0.0, 0.8, 1.0, 0.3, 2.0, 0.8] * 4)
+    topk = torch.tensor([40, 40, 1, 5, 128, 0, 200, 64] * 3, dtype=torch.int32)
+    topp = torch.tensor([0.9, 0.9, 0.5, 1.0, 0.99, 0.7] * 4)
+    seeds = torch.arange(B, dtype=torch.int64) * 104729 + 3
+    pos = torch.arange(B, dtype=torch.int32) + 11
+    d = [t.to(DEV) for t in (temp, topk, topp, seeds, pos)]
+    full = ops.sample(lg.to(DEV), *d).cpu()
+    Vl = V // W
+    cv = torch.empty(W * B, 128, device=DEV)
+    ci = torch.empty(W * B, 128, device=DEV, dtype=torch.int32)
+    for r in range(W):  # each "rank" emits its shard's candidates (rank-major slots)
+        ops.topk_candidates(lg[:, r * Vl:(r + 1) * Vl].contiguous().to(DEV), r * Vl,
+                            cv[r * B:(r + 1) * B], ci[r * B:(r + 1) * B])
+    got = ops.sample_candidates(cv, ci, W, *d, out=torch.empty(B, dtype=torch.int32,
+                                                                  device=DEV)).cpu()
+    assert torch.equal(got, full), (got, full)
+    # the CPU reference of the candidate path agrees with the CPU full-row reference
+    ref_full = S.sample_ref(lg, temp, topk, topp, seeds, pos, torch.empty(B, dtype=torch.int32))
+    ref_c = ops.sample_candidates(cv.cpu(), ci.cpu(), W, temp, topk, topp, seeds, pos,
+                                  torch.empty(B, dtype=torch.int32))
+    assert torch.equal(ref_c, ref_full)
+
+
 def test_split_k_workspace_survives_growth_under_captured_graph():
     """A hipGraph that captured a split-K tiled GEMM keeps working after a later, larger
     split-K launch grows the workspace (the old buffer must not be freed: the graph holds

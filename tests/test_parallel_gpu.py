@@ -56,12 +56,39 @@ def _worker(rank, world, port, q, moe, a2a=False, overlap=False, graphs=False):
             assert gs and all(g.graph is not None for g in gs), "TP decode graph not captured"
             got2 = [r.tokens for r in eng.generate(prompts, 6, stop_on_eos=False)]  # replays
             assert got2 == got, (got2, got)
+            if got == ref:
+                # sampled decode in the graph (per-shard top-128 + one-shot candidate gather)
+                # == the full-logit-gather sampler on the same sharded engine numerics (bf16
+                # TP sums round differently from TP=1, so a sampled draw may legitimately
+                # differ from the unsharded engine's; the CPU test pins that in fp32)
+                ref_eng = Engine(cfg, weights=w, device="cuda", kv_pages=32, comm=eng.model.comm,
+                                 tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=False)
+                ref_eng.model.sample_full_gather = True
+                ref, got = _sampled(ref_eng, prompts), _sampled(eng, prompts)
+                gs = [g for k, g in eng._graphs.items() if not k[2]]
+                assert gs and all(g.graph is not None for g in gs), "sampled graph not captured"
         q.put((rank, got == ref, got, ref))
     except Exception:
         import traceback
         q.put((rank, False, traceback.format_exc(), None))
     finally:
         dist.destroy_process_group()
+
+
+def _sampled(eng, prompts, n=5):
+    from p2p_llm_chat_go_amd.engine.sampling import SamplingParams
+
+    params = [SamplingParams(temperature=1.1, top_k=30, top_p=0.95, seed=21 + b)
+              for b in range(len(prompts))]
+    pages = [eng.kv.allocator.alloc(2) for _ in prompts]
+    first = eng.prefill(prompts, pages, sampling=params).tolist()
+    g = eng.decode_graph(len(prompts), 128, greedy=False)
+    g.state.load(first, [len(p) for p in prompts], pages)
+    g.step_sampled(params, n)
+    out = [[first[b]] + g.state.hist[b, :n].tolist() for b in range(len(prompts))]
+    for p in pages:
+        eng.kv.allocator.free(p)
+    return out
 
 
 @pytest.mark.parametrize("moe,a2a,overlap,graphs", [
