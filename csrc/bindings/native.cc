@@ -270,6 +270,30 @@ PYBIND11_MODULE(_native, m) {
     py::gil_scoped_release rel;
     return quic_echo(kt, in, drop, streams);
   }, py::arg("key_type"), py::arg("payload"), py::arg("drop_rate") = 0.0, py::arg("streams") = 1);
+  m.def("relay_voucher_check", []() {
+    // {good voucher verifies, wrong peer rejected, wrong expiry rejected, foreign signer
+    // rejected, tampered signature rejected}
+    PrivateKey rk = PrivateKey::generate(KeyType::Ed25519), pk = PrivateKey::generate(KeyType::Ed25519);
+    PrivateKey other = PrivateKey::generate(KeyType::RSA);
+    const PeerId relay = PeerId::from_public_key(rk.public_key());
+    const PeerId peer = PeerId::from_public_key(pk.public_key());
+    const PeerId stranger = PeerId::from_public_key(other.public_key());
+    const Bytes v = test_make_voucher(rk, relay, peer, 1234567);
+    auto ok = [&](const Bytes& env, const PeerId& r, const PeerId& p, uint64_t e) {
+      try {
+        verify_voucher(env, r, p, e);
+        return true;
+      } catch (const NetError&) {
+        return false;
+      }
+    };
+    Bytes tampered = v;
+    tampered[tampered.size() - 3] ^= 0x40;
+    return py::make_tuple(ok(v, relay, peer, 1234567), ok(v, relay, stranger, 1234567),
+                          ok(v, relay, peer, 1234568),
+                          ok(test_make_voucher(other, relay, peer, 1234567), relay, peer, 1234567),
+                          ok(tampered, relay, peer, 1234567));
+  });
   m.def("quic_protocol_violation", [](const std::string& kind) {
     // a client sends a frame past the server's advertised limits; returns the client's
     // view of the close (the server must answer with the RFC 9000 error code)

@@ -19,6 +19,7 @@ struct RelayMsg {
   std::vector<Bytes> peer_addrs;
   uint64_t expire = 0;
   std::vector<Bytes> resv_addrs;
+  Bytes voucher;  // Reservation.voucher: signed envelope of a ReservationVoucher
   uint32_t limit_duration = 0;
   uint64_t limit_data = 0;
   int status = 0;
@@ -53,6 +54,7 @@ RelayMsg parse(const Bytes& b, bool hop) {
       for (auto& g : pb_parse(f.bytes)) {
         if (g.field == 1 && g.wire == 0) m.expire = g.varint;
         if (g.field == 2 && g.wire == 2) m.resv_addrs.push_back(g.bytes);
+        if (g.field == 3 && g.wire == 2) m.voucher = g.bytes;
       }
     } else if (((hop && f.field == 4) || (!hop && f.field == 3)) && f.wire == 2) {
       for (auto& g : pb_parse(f.bytes)) {
@@ -66,6 +68,84 @@ RelayMsg parse(const Bytes& b, bool hop) {
   return m;
 }
 
+// ---- reservation vouchers (circuit relay v2 spec, "Reservation Vouchers") ----
+// ReservationVoucher {relay=1 (peer id bytes), peer=2 (peer id bytes), expiration=3}
+// carried in a libp2p signed envelope (RFC 0002): Envelope {public_key=1, payload_type=2,
+// payload=3, signature=5}, signature over
+//   uvarint(len(domain)) domain uvarint(len(type)) type uvarint(len(payload)) payload
+// with domain "libp2p-relay-rsvp" and payload type = multicodec 0x0302 (uvarint bytes).
+const char* kVoucherDomain = "libp2p-relay-rsvp";
+
+Bytes voucher_type() { return uvarint(0x0302); }
+
+Bytes envelope_signed_data(const Bytes& type, const Bytes& payload) {
+  Bytes d;
+  const std::string dom = kVoucherDomain;
+  put_uvarint(d, dom.size());
+  d.insert(d.end(), dom.begin(), dom.end());
+  put_uvarint(d, type.size());
+  append(d, type);
+  put_uvarint(d, payload.size());
+  append(d, payload);
+  return d;
+}
+
+Bytes voucher_payload(const PeerId& relay, const PeerId& peer, uint64_t expire) {
+  PbWriter w;
+  w.bytes_field(1, relay.bytes());
+  w.bytes_field(2, peer.bytes());
+  w.varint_field(3, expire);
+  return w.buf;
+}
+
+Bytes make_voucher(const PrivateKey& key, const PeerId& relay, const PeerId& peer,
+                   uint64_t expire) {
+  const Bytes type = voucher_type();
+  const Bytes payload = voucher_payload(relay, peer, expire);
+  PbWriter env;
+  env.bytes_field(1, key.public_key().marshal());
+  env.bytes_field(2, type);
+  env.bytes_field(3, payload);
+  env.bytes_field(5, key.sign(envelope_signed_data(type, payload)));
+  return env.buf;
+}
+}  // namespace
+
+// Verifies a reservation voucher envelope: signed by the relay's key (the envelope key
+// must hash to `relay`), payload type ReservationVoucher, relay/peer fields matching, and
+// the expiration equal to the reservation's.  Throws NetError on any mismatch.
+void verify_voucher(const Bytes& env, const PeerId& relay, const PeerId& peer, uint64_t expire) {
+  Bytes pk, type, payload, sig;
+  for (auto& f : pb_parse(env)) {
+    if (f.wire != 2) continue;
+    if (f.field == 1) pk = f.bytes;
+    if (f.field == 2) type = f.bytes;
+    if (f.field == 3) payload = f.bytes;
+    if (f.field == 5) sig = f.bytes;
+  }
+  if (pk.empty() || sig.empty()) throw NetError("voucher: malformed envelope");
+  const PublicKey key = PublicKey::unmarshal(pk);
+  if (!(PeerId::from_public_key(key) == relay)) throw NetError("voucher: not signed by the relay");
+  if (type != voucher_type()) throw NetError("voucher: wrong payload type");
+  if (!key.verify(envelope_signed_data(type, payload), sig))
+    throw NetError("voucher: bad signature");
+  PeerId vr, vp;
+  uint64_t exp = 0;
+  for (auto& f : pb_parse(payload)) {
+    if (f.field == 1 && f.wire == 2) vr = PeerId::from_bytes(f.bytes);
+    if (f.field == 2 && f.wire == 2) vp = PeerId::from_bytes(f.bytes);
+    if (f.field == 3 && f.wire == 0) exp = f.varint;
+  }
+  if (!(vr == relay) || !(vp == peer) || exp != expire)
+    throw NetError("voucher: fields do not match the reservation");
+}
+
+Bytes test_make_voucher(const PrivateKey& key, const PeerId& relay, const PeerId& peer,
+                        uint64_t expire) {
+  return make_voucher(key, relay, peer, expire);
+}
+
+namespace {
 Bytes hop_status(int status, const Bytes& extra = Bytes()) {
   PbWriter w;
   w.varint_field(1, HOP_STATUS);
@@ -130,8 +210,10 @@ void RelayService::on_hop(StreamCtx& c) {
       resv_[c.peer] = now + res_.reservation_ttl_s;
     }
     PbWriter rv;
-    rv.varint_field(1, (uint64_t)(now + res_.reservation_ttl_s));
+    const uint64_t expire = (uint64_t)(now + res_.reservation_ttl_s);
+    rv.varint_field(1, expire);
     for (auto& a : h_->addrs()) rv.bytes_field(2, a.with_peer(h_->id()).bytes());
+    rv.bytes_field(3, make_voucher(h_->key(), h_->id(), c.peer, expire));
     PbWriter extra;
     extra.bytes_field(3, rv.buf);
     extra.bytes_field(4, limit_pb(res_.limit_duration_s, res_.limit_data));
@@ -215,6 +297,10 @@ int64_t RelayClient::reserve(const Multiaddr& relay_addr, int timeout_ms) {
   c.stream->close();
   if (r.type != HOP_STATUS || r.status != RS_OK)
     throw NetError("relay reservation refused (status " + std::to_string(r.status) + ")");
+  // go-libp2p's client requires the voucher; so do we (an unsigned reservation could be
+  // a relay impersonating another one)
+  if (r.voucher.empty()) throw NetError("relay reservation without a voucher");
+  verify_voucher(r.voucher, rid, h_->id(), r.expire);
   h_->add_advertised_addr(
       Multiaddr::parse(bare.str() + "/p2p/" + rid.to_base58() + "/p2p-circuit"));
   return (int64_t)r.expire;

@@ -29,6 +29,12 @@ struct RelayResources {  // go-libp2p relayv2.DefaultResources()
   uint64_t limit_data = 1 << 17;
 };
 
+// Reservation vouchers (signed envelopes, domain "libp2p-relay-rsvp"): verify throws
+// NetError unless `env` is a ReservationVoucher for (relay, peer, expire) signed by relay.
+void verify_voucher(const Bytes& env, const PeerId& relay, const PeerId& peer, uint64_t expire);
+Bytes test_make_voucher(const PrivateKey& key, const PeerId& relay, const PeerId& peer,
+                        uint64_t expire);
+
 class RelayService {
  public:
   RelayService(std::shared_ptr<Host> h, RelayResources r = RelayResources());

@@ -171,3 +171,12 @@ def test_quic_rejects_data_past_advertised_limits(N, kind, code):
     stream with CRYPTO_BUFFER_EXCEEDED (0x0d) -- nothing past the windows is buffered."""
     closed, why = N.quic_protocol_violation(kind)
     assert closed and ("code %d" % code) in why, why
+
+
+def test_relay_reservation_voucher(N):
+    """Circuit relay v2 reservation vouchers: a signed envelope (domain
+    libp2p-relay-rsvp, payload type 0x0302) binding (relay, peer, expiration), as
+    go-libp2p's relayv2 issues (`go/cmd/relay/main.go:37`).  Only the exact voucher
+    signed by the relay's own key verifies."""
+    good, wrong_peer, wrong_exp, foreign, tampered = N.relay_voucher_check()
+    assert good and not wrong_peer and not wrong_exp and not foreign and not tampered
