@@ -142,8 +142,12 @@ std::string secure_echo(const std::string& key_type, const std::string& payload,
 // QUIC self-test on loopback: two transports, client dials, opens `streams`
 // streams in parallel and each echoes `payload` through a multistream-negotiated
 // "/echo/1.0.0" handler.  Returns {echo ok, client retransmitted frames, rtt us}.
-std::tuple<bool, uint64_t, long> quic_echo(const std::string& kt, const std::string& payload,
-                                           double drop_rate, int streams) {
+std::tuple<bool, uint64_t, long, uint64_t, uint64_t> quic_echo(const std::string& kt,
+                                                               const std::string& payload,
+                                                               double drop_rate, int streams,
+                                                               uint64_t ku_interval) {
+  // ku_interval > 0: both endpoints start a 1-RTT key update every ku_interval packets
+  quic_set_key_update_interval(ku_interval ? ku_interval : (1ull << 22));
   const KeyType t = kt == "rsa" ? KeyType::RSA : KeyType::Ed25519;
   PrivateKey ka = PrivateKey::generate(t), kb = PrivateKey::generate(t);
   const PeerId idb = PeerId::from_public_key(kb.public_key());
@@ -175,7 +179,7 @@ std::tuple<bool, uint64_t, long> quic_echo(const std::string& kt, const std::str
   });
   bool ok = true;
   long rtt = -1;
-  uint64_t retx = 0;
+  uint64_t retx = 0, kus = 0, cong = 0;
   try {
     auto c = cli->dial("127.0.0.1", srv->port(), idb, 10000);
     c->start(nullptr);
@@ -202,6 +206,8 @@ std::tuple<bool, uint64_t, long> quic_echo(const std::string& kt, const std::str
     for (int g : good) ok = ok && g;
     rtt = c->ping(2000);
     retx = c->retransmitted();
+    kus = c->key_updates();
+    cong = c->congestion_events();
     c->close();
   } catch (const std::exception& e) {
     cli->close();
@@ -210,8 +216,9 @@ std::tuple<bool, uint64_t, long> quic_echo(const std::string& kt, const std::str
   }
   cli->close();
   srv->close();
+  quic_set_key_update_interval(1ull << 22);
   if (!err.empty()) throw NetError(err);
-  return {ok, retx, rtt};
+  return {ok, retx, rtt, kus, cong};
 }
 
 }  // namespace
@@ -265,11 +272,13 @@ PYBIND11_MODULE(_native, m) {
     }
     return py::bytes(out);
   }, py::arg("key_type"), py::arg("payload"), py::arg("security") = "noise");
-  m.def("quic_echo", [](const std::string& kt, const py::bytes& payload, double drop, int streams) {
+  m.def("quic_echo", [](const std::string& kt, const py::bytes& payload, double drop, int streams,
+                        uint64_t ku_interval) {
     std::string in = payload;
     py::gil_scoped_release rel;
-    return quic_echo(kt, in, drop, streams);
-  }, py::arg("key_type"), py::arg("payload"), py::arg("drop_rate") = 0.0, py::arg("streams") = 1);
+    return quic_echo(kt, in, drop, streams, ku_interval);
+  }, py::arg("key_type"), py::arg("payload"), py::arg("drop_rate") = 0.0, py::arg("streams") = 1,
+     py::arg("key_update_interval") = 0);
   m.def("relay_voucher_check", []() {
     // {good voucher verifies, wrong peer rejected, wrong expiry rejected, foreign signer
     // rejected, tampered signature rejected}

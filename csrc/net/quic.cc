@@ -31,6 +31,11 @@ constexpr uint64_t kStreamLimit = 256;  // concurrent peer-opened bidi streams
 constexpr size_t kMaxInFlight = 256;     // ack-eliciting 1-RTT packets outstanding
 constexpr int kIdleMs = 30000, kKeepAliveMs = 10000;
 constexpr uint64_t kMaxCryptoBuffer = 64 << 10;  // out-of-order CRYPTO bytes per space
+// NewReno (RFC 9002 §7.2, B.2): windows in bytes of max_datagram_size
+constexpr uint64_t kInitialWindow = 10 * kMaxDatagram;
+constexpr uint64_t kMinWindow = 2 * kMaxDatagram;
+constexpr uint64_t kPacketThreshold = 3;  // RFC 9002 §6.1.1
+std::atomic<uint64_t> g_key_update_interval{1ull << 22};
 
 // A peer's protocol violation with its RFC 9000 §20.1 transport error code.
 struct QuicProtoError : std::runtime_error {
@@ -98,6 +103,17 @@ Bytes hkdf_expand_label(const Bytes& secret, const std::string& label, size_t le
   }
   out.resize(len);
   return out;
+}
+
+// RFC 9001 §6.1: next-generation 1-RTT secret; its key/iv replace the old ones, the
+// header protection key is never updated.
+Bytes next_secret(const Bytes& secret) { return hkdf_expand_label(secret, "quic ku", secret.size()); }
+
+void derive_keys(const Bytes& secret, QuicKeys* k);
+
+void next_keys(const Bytes& secret, const QuicKeys& cur, QuicKeys* out) {
+  derive_keys(secret, out);
+  memcpy(out->hp, cur.hp, 16);
 }
 
 void derive_keys(const Bytes& secret, QuicKeys* k) {
@@ -345,6 +361,7 @@ QuicConn::QuicConn(std::shared_ptr<QuicTransport> t, bool client, const sockaddr
     : tr_(t), fd_(t->fd_), client_(client), peer_(peer), key_(key) {
   last_recv_ = last_send_ = Clock::now();
   recv_max_data_ = kConnWindow;
+  cwnd_ = kInitialWindow;
   max_remote_streams_ = kStreamLimit;
 }
 
@@ -558,9 +575,44 @@ void QuicConn::install_keys() {
   if (!sp_[HANDSHAKE].rx.ok && !sec_[0][peer].empty()) derive_keys(sec_[0][peer], &sp_[HANDSHAKE].rx);
   // 1-RTT keys: the server may send (0.5-RTT) once its Finished is out; both sides
   // accept 1-RTT packets as soon as the keys exist.
-  if (!sp_[APP].tx.ok && !sec_[1][me].empty() && (tls_done_ || !client_))
+  if (!sp_[APP].tx.ok && !sec_[1][me].empty() && (tls_done_ || !client_)) {
     derive_keys(sec_[1][me], &sp_[APP].tx);
-  if (!sp_[APP].rx.ok && !sec_[1][peer].empty()) derive_keys(sec_[1][peer], &sp_[APP].rx);
+    app_sec_tx_ = sec_[1][me];
+  }
+  if (!sp_[APP].rx.ok && !sec_[1][peer].empty()) {
+    derive_keys(sec_[1][peer], &sp_[APP].rx);
+    app_sec_rx_ = sec_[1][peer];
+    next_keys(next_secret(app_sec_rx_), sp_[APP].rx, &rx_next_);
+  }
+}
+
+void quic_set_key_update_interval(uint64_t packets) { g_key_update_interval = packets ? packets : 1; }
+
+void QuicConn::update_tx_keys() {
+  app_sec_tx_ = next_secret(app_sec_tx_);
+  QuicKeys k;
+  next_keys(app_sec_tx_, sp_[APP].tx, &k);
+  sp_[APP].tx = k;
+  key_phase_ ^= 1;
+  phase_first_pn_ = sp_[APP].next_pn;
+  phase_sent_ = 0;
+  phase_acked_ = false;
+  ++key_updates_;
+}
+
+void QuicConn::update_rx_keys() {
+  rx_prev_ = sp_[APP].rx;
+  sp_[APP].rx = rx_next_;
+  app_sec_rx_ = next_secret(app_sec_rx_);
+  next_keys(next_secret(app_sec_rx_), sp_[APP].rx, &rx_next_);
+}
+
+bool QuicConn::force_key_update() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!established_ || !sp_[APP].tx.ok || !sp_[APP].rx.ok || !phase_acked_) return false;
+  update_tx_keys();
+  update_rx_keys();
+  return true;
 }
 
 void QuicConn::tls_drive(Events& ev) {
@@ -707,8 +759,21 @@ void QuicConn::handle_packet(Bytes pkt, size_t pn_off, int space, bool long_hdr,
   else if (pn > expected + hwin && pn >= win) pn -= win;
   Bytes pt;
   const size_t hl = pn_off + pnl;
-  if (!aead_open(S.rx.key, S.rx.iv, pn, pkt.data(), hl, pkt.data() + hl, pkt.size() - hl, &pt))
-    return;  // undecryptable (corrupt / stale keys): drop
+  const int kp = (pkt[0] >> 2) & 1;
+  if (space != APP || kp == key_phase_) {
+    if (!aead_open(S.rx.key, S.rx.iv, pn, pkt.data(), hl, pkt.data() + hl, pkt.size() - hl, &pt))
+      return;  // undecryptable (corrupt / stale keys): drop
+  } else if (rx_prev_.ok && aead_open(rx_prev_.key, rx_prev_.iv, pn, pkt.data(), hl,
+                                      pkt.data() + hl, pkt.size() - hl, &pt)) {
+    // a late packet of the previous key phase
+  } else if (rx_next_.ok && aead_open(rx_next_.key, rx_next_.iv, pn, pkt.data(), hl,
+                                      pkt.data() + hl, pkt.size() - hl, &pt)) {
+    // the peer started a key update (RFC 9001 §6.2): follow it on both directions
+    update_rx_keys();
+    update_tx_keys();
+  } else {
+    return;
+  }
   if (pn < S.recv_floor || S.recvd.count(pn)) return;  // duplicate
   S.recvd.insert(pn);
   while (S.recvd.size() > 512) {
@@ -845,8 +910,11 @@ void QuicConn::on_ack(int space, const uint8_t* p, size_t n, size_t* pos, bool e
   for (auto& r : ranges) {
     auto it = S.sent.lower_bound(r.first);
     while (it != S.sent.end() && it->first <= r.second) {
+      on_packet_acked(it->second);
+      if (space == APP && it->first >= phase_first_pn_) phase_acked_ = true;
       if (it->first == largest) {  // RTT sample (RFC 9002 §5.3, ack delay ignored)
         const double rtt = ms_since(it->second.t, now);
+        latest_rtt_ms_ = rtt;
         if (srtt_ms_ == 0) {
           srtt_ms_ = rtt;
           rttvar_ms_ = rtt / 2;
@@ -862,7 +930,10 @@ void QuicConn::on_ack(int space, const uint8_t* p, size_t n, size_t* pos, bool e
       for (auto pi = pings_.lower_bound(r.first); pi != pings_.end() && pi->first <= r.second; ++pi)
         pi->second = true;
   }
-  if (newly) pto_count_ = 0;
+  if (newly) {
+    pto_count_ = 0;
+    detect_lost(space, largest, now);
+  }
   cv_.notify_all();
 }
 
@@ -1064,7 +1135,7 @@ void QuicConn::send_packet(int space, const Bytes& payload_in, bool elicit,
     hdr.push_back((uint8_t)(0x40 | (len >> 8)));
     hdr.push_back((uint8_t)len);
   } else {
-    hdr.push_back(0x40 | 0x03);
+    hdr.push_back((uint8_t)(0x40 | (key_phase_ << 2) | 0x03));
     hdr.insert(hdr.end(), dcid_.begin(), dcid_.end());
   }
   pn_off = hdr.size();
@@ -1079,9 +1150,54 @@ void QuicConn::send_packet(int space, const Bytes& payload_in, bool elicit,
   ::sendto(fd_, pkt.data(), pkt.size(), 0, (const sockaddr*)&peer_, sizeof(peer_));
   const auto now = Clock::now();
   if (elicit) {
-    S.sent[pn] = SentPkt{now, std::move(frames)};
+    S.sent[pn] = SentPkt{now, std::move(frames), pkt.size()};
+    bytes_in_flight_ += pkt.size();
     last_send_ = now;
   }
+  if (space == APP && ++phase_sent_ >= g_key_update_interval && phase_acked_ && sp_[APP].rx.ok) {
+    update_tx_keys();  // AEAD usage limit: next packets go out in the new phase
+    update_rx_keys();
+  }
+}
+
+// ---- NewReno (RFC 9002 §7, Appendix B)
+void QuicConn::on_packet_acked(const SentPkt& p) {
+  bytes_in_flight_ -= std::min<uint64_t>(bytes_in_flight_, p.bytes);
+  if (p.t <= recovery_start_) return;  // no growth for packets sent before the recovery
+  if (cwnd_ < ssthresh_) cwnd_ += p.bytes;                              // slow start
+  else cwnd_ += std::max<uint64_t>(1, kMaxDatagram * p.bytes / cwnd_);  // congestion avoidance
+}
+
+void QuicConn::on_packets_lost(int, Clock::time_point newest_lost_sent) {
+  if (newest_lost_sent <= recovery_start_) return;  // one reduction per round trip
+  recovery_start_ = Clock::now();
+  ssthresh_ = std::max(cwnd_ / 2, kMinWindow);
+  cwnd_ = ssthresh_;
+  ++congestion_events_;
+}
+
+// RFC 9002 §6.1: a packet is lost once kPacketThreshold later packets were acknowledged,
+// or it was sent more than 9/8 of an RTT before an acknowledged one.
+void QuicConn::detect_lost(int space, uint64_t largest_acked, Clock::time_point now) {
+  Space& S = sp_[space];
+  const double rtt = std::max(srtt_ms_, latest_rtt_ms_);
+  const double thr_ms = std::max(9.0 / 8.0 * (rtt > 0 ? rtt : 50.0), 1.0);
+  bool any = false;
+  Clock::time_point newest{};
+  for (auto it = S.sent.begin(); it != S.sent.end() && it->first < largest_acked;) {
+    if (it->first + kPacketThreshold <= largest_acked || ms_since(it->second.t, now) > thr_ms) {
+      for (auto f = it->second.frames.rbegin(); f != it->second.frames.rend(); ++f)
+        S.queued.push_front(*f);
+      retx_count_ += it->second.frames.size();
+      bytes_in_flight_ -= std::min<uint64_t>(bytes_in_flight_, it->second.bytes);
+      newest = std::max(newest, it->second.t);
+      any = true;
+      it = S.sent.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  if (any) on_packets_lost(space, newest);
 }
 
 void QuicConn::flush() {
@@ -1117,8 +1233,9 @@ void QuicConn::flush() {
         S.crypto_send_off += k;
         add(std::move(f));
       }
-      // stream data is paced by a fixed in-flight window (no congestion controller)
-      if (space == APP && established_ && S.sent.size() < kMaxInFlight) {
+      // stream data: NewReno congestion window (bytes in flight), plus a packet cap
+      if (space == APP && established_ && S.sent.size() < kMaxInFlight &&
+          bytes_in_flight_ + kMaxDatagram <= cwnd_) {
         for (auto it = send_ready_.begin(); it != send_ready_.end() && pl.size() + 32 < kMaxPayload;) {
           auto si = streams_.find(*it);
           if (si == streams_.end()) {
@@ -1185,15 +1302,22 @@ void QuicConn::tick(Clock::time_point now) {
         Space& S = sp_[s];
         if (S.sent.empty() || ms_since(S.sent.begin()->second.t, now) < pto) continue;
         std::deque<Bytes> again;
-        for (auto& kv : S.sent)
+        for (auto& kv : S.sent) {
           for (auto& f : kv.second.frames) again.push_back(f);
+          bytes_in_flight_ -= std::min<uint64_t>(bytes_in_flight_, kv.second.bytes);
+        }
         S.sent.clear();
         if (again.empty()) again.push_back(Bytes{0x01});  // PING probe
         for (auto it = again.rbegin(); it != again.rend(); ++it) S.queued.push_front(*it);
         retx_count_ += again.size();
         fired = true;
       }
-      if (fired) ++pto_count_;
+      if (fired && ++pto_count_ >= 3 && cwnd_ > kMinWindow) {
+        // RFC 9002 §7.6: repeated probe timeouts = persistent congestion
+        cwnd_ = kMinWindow;
+        recovery_start_ = now;
+        ++congestion_events_;
+      }
       if (established_ && ms_since(last_send_, now) > kKeepAliveMs) sp_[APP].queued.push_back(Bytes{0x01});
       flush();
     }

@@ -140,6 +140,7 @@ class QuicConn : public MuxSession, public std::enable_shared_from_this<QuicConn
   struct SentPkt {
     std::chrono::steady_clock::time_point t;
     std::vector<Bytes> frames;  // retransmittable frames (raw encodings)
+    size_t bytes = 0;           // datagram bytes (congestion accounting)
   };
   struct Space {
     uint64_t next_pn = 0;
@@ -235,12 +236,39 @@ class QuicConn : public MuxSession, public std::enable_shared_from_this<QuicConn
   std::function<void(StreamPtr)> on_stream_;
   std::function<void()> on_close_;
   // recovery
-  double srtt_ms_ = 0, rttvar_ms_ = 0;
+  double srtt_ms_ = 0, rttvar_ms_ = 0, latest_rtt_ms_ = 0;
   int pto_count_ = 0;
   std::atomic<uint64_t> retx_count_{0};
   std::chrono::steady_clock::time_point last_recv_, last_send_;
   std::map<uint64_t, bool> pings_;  // app packet number -> acked
+  // NewReno congestion control (RFC 9002 §7)
+  uint64_t cwnd_ = 0, ssthresh_ = ~0ull, bytes_in_flight_ = 0;
+  std::chrono::steady_clock::time_point recovery_start_{};
+  std::atomic<uint64_t> congestion_events_{0};
+  void on_packet_acked(const SentPkt& p);
+  void on_packets_lost(int space, std::chrono::steady_clock::time_point newest_lost_sent);
+  void detect_lost(int space, uint64_t largest_acked, std::chrono::steady_clock::time_point now);
+  // 1-RTT key update (RFC 9001 §6): current generation secrets, the key phase bit, the
+  // previous generation's receive keys (late packets) and the next generation's
+  Bytes app_sec_tx_, app_sec_rx_;
+  QuicKeys rx_prev_, rx_next_;
+  int key_phase_ = 0;
+  uint64_t phase_first_pn_ = 0, phase_sent_ = 0;
+  bool phase_acked_ = true;
+  std::atomic<uint64_t> key_updates_{0};
+  void update_tx_keys();
+  void update_rx_keys();
+
+ public:
+  // Start a key update now (if the current phase is acknowledged); returns whether it did.
+  bool force_key_update();
+  uint64_t key_updates() const { return key_updates_; }
+  uint64_t congestion_events() const { return congestion_events_; }
+  uint64_t cwnd() const { return cwnd_; }
 };
+// Packets sent per key phase before an endpoint starts a key update (AES-128-GCM
+// confidentiality limit is 2^23 packets; tests lower it).
+void quic_set_key_update_interval(uint64_t packets);
 using QuicConnPtr = std::shared_ptr<QuicConn>;
 
 class QuicTransport : public std::enable_shared_from_this<QuicTransport> {

@@ -157,11 +157,23 @@ def test_quic_initial_keys_rfc9001_appendix_a(N):
 ])
 def test_quic_echo(N, key, size, drop, streams):
     payload = os.urandom(size)
-    ok, retx, rtt = N.quic_echo(key, payload, drop, streams)
+    ok, retx, rtt, _ku, cong = N.quic_echo(key, payload, drop, streams)
     assert ok
     assert rtt > 0  # PING acknowledged
     if drop > 0:
         assert retx > 0
+        assert cong > 0  # NewReno: losses shrank the congestion window
+
+
+@pytest.mark.parametrize("drop", [0.0, 0.05])
+def test_quic_key_update(N, drop):
+    """RFC 9001 §6: both endpoints roll the 1-RTT keys every 64 packets during a 2 MiB
+    echo (key phase bit, next-generation secrets via "quic ku", previous-phase keys kept
+    for late packets); the payload survives every update, with and without loss."""
+    payload = os.urandom(2 << 20)
+    ok, retx, rtt, ku, _cong = N.quic_echo("ed25519", payload, drop, 2, key_update_interval=64)
+    assert ok and rtt > 0
+    assert ku >= 5, ku
 
 
 @pytest.mark.parametrize("kind,code", [("stream", 3), ("conn", 3), ("crypto", 13)])
