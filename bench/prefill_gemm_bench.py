@@ -22,9 +22,11 @@ def main():
     ap.add_argument("--M", type=int, nargs="*", default=[36, 64, 288, 512, 2048, 8192])
     a = ap.parse_args()
     H, F = LLAMA31_8B.hidden, LLAMA31_8B.ffn
-    variants = [("v1", (1, 0, 0)), ("v2_auto", (2, 0, 0)), ("v2_256x256", (2, 1, 1)),
+    variants = [("v2_auto", (2, 0, 0)), ("v2_256x256_phased", (2, 1, 1)),
+                ("v2_256x256_2stage", (2, 1, 1, 0)),
                 ("v2_128x256", (2, 2, 1)), ("v2_128x128", (2, 3, 1)),
                 ("v2_128x128_s2", (2, 3, 2)), ("v2_128x128_s4", (2, 3, 4))]
+    L = __import__("p2p_llm_chat_go_amd.ops._lib", fromlist=["lib"]).lib()
     for M in a.M:
         x = torch.randn(M, H, device="cuda").to(torch.bfloat16)
         xf = torch.randn(M, F, device="cuda").to(torch.bfloat16)
@@ -46,7 +48,8 @@ def main():
             for vname, cfg in vs:
                 set_tiled_min_m(65 if cfg is None else 1)
                 if cfg is not None:
-                    tiled_config(*cfg)
+                    tiled_config(*cfg[:3])
+                    L.p2p_prefill_phased(cfg[3] if len(cfg) > 3 else 1)
                 t = graph_time(lambda i: fn(W), n_inner=10)
                 print(json.dumps({"M": M, "gemm": name, "variant": vname, "us": round(t, 1),
                                   "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1),

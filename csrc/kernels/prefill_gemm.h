@@ -154,7 +154,6 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   float ss[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) ss[i] = 0.f;
-  const bool do_ss = NORM && wn == 0;
 
   // ---- STAGES-deep LDS-DMA pipeline: counted vmcnt + raw barriers, so the
   // younger stages stay in flight across the barrier (no vmcnt(0) drain) ----
@@ -183,14 +182,16 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      if (do_ss) {
+      if constexpr (NORM) {  // RMSNorm sums: fragment i by wave wn == i % 4 (VALU spread)
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i) {
+          if ((i & 3) != wn) continue;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float v = (float)af[i][e];
             ss[i] = fmaf(v, v, ss[i]);
           }
+        }
       }
     }
   }
@@ -200,18 +201,17 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   // ---- row rstd (NORM): column-0 waves publish through LDS (stages are free now) ----
   float* ss_row = reinterpret_cast<float*>(lds);
   if constexpr (NORM) {
-    if (wn == 0) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        float v = ss[i];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        if (lane < 16) {
-          if constexpr (SPLIT)
-            sp.ss_slab[((size_t)tile * splitk + split) * BM + wm * (BM / 2) + 16 * i + lane] = v;
-          else
-            ss_row[wm * (BM / 2) + 16 * i + lane] = v;
-        }
+    for (int i = 0; i < FM; ++i) {
+      if ((i & 3) != wn) continue;
+      float v = ss[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) {
+        if constexpr (SPLIT)
+          sp.ss_slab[((size_t)tile * splitk + split) * BM + wm * (BM / 2) + 16 * i + lane] = v;
+        else
+          ss_row[wm * (BM / 2) + 16 * i + lane] = v;
       }
     }
     if constexpr (!SPLIT) __syncthreads();
@@ -287,6 +287,247 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
         for (int j = 0; j < H; ++j)
           epi_store<EPI>(m, valid, nt_i * (BN / 32) + wn * H + j, r, acc[i][j][jj] * scale,
                          acc[i][j + H][jj] * scale, out, ldo, ea);
+      } else if constexpr (EPI == EPI_QKV_ROPE) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int g = nt_i * (BN / 16) + bgi[j];
+          const int kk = g & 7;
+          const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+          float2 c = float2{1.f, 0.f};
+          int slot = -1;
+          if (valid) {
+            c = ea.cs[(size_t)ea.pos[m] * 64 + dd];
+            slot = ea.slots[m];
+          }
+          epi_store<EPI>(m, valid, g, r, acc[i][j][jj] * scale, 0.f, out, ldo, ea, c, slot);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          epi_store<EPI>(m, valid, nt_i * (BN / 16) + bgi[j], r, acc[i][j][jj] * scale, 0.f, out,
+                         ldo, ea);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// 256 x 256 tile, phased pipeline (cdna_hip_programming.md §5 "The 256² 8-phase
+// template", re-derived for the fragment-major LDS image).  A K-tile (BK = 64) is
+// staged as four 16 KiB units -- A0/A1 (the two 64-row halves of every wave's 128
+// rows) and B0/B1 (the two 32-column halves of every wave's 64 columns) -- and
+// consumed in four phases of 16 MFMAs per wave, one C quadrant each:
+//   p0: (A0, B0)   p1: (A0, B1)   p2: (A1, B1)   p3: (A1, B0)
+// (B0 fragments stay in registers from p0 to p3).  Each phase issues ONE unit's
+// LDS-DMA (2 instructions per thread), in the order
+//   p0: A1(t+1)   p1: A0(t+2)   p2: B0(t+2)   p3: B1(t+2)
+// so a unit is re-staged one phase after its last read (behind that phase's
+// lgkmcnt(0) + barrier) and lands about five phases (> 1 K-tile) before it is
+// read: the counted vmcnt before a reading phase leaves 10 DMA instructions in
+// flight in the steady state and never drains the queue inside the loop.
+template <int EPI, bool NORM>
+__global__ __launch_bounds__(NT) void prefill_gemm8_kernel(const bf16x8* __restrict__ Wt,
+                                                           const bf16* __restrict__ X, int ldx,
+                                                           int M, int K, int m_tiles, int n_tiles,
+                                                           int up_off, void* __restrict__ out,
+                                                           int ldo, float eps, EpiArgs ea) {
+  constexpr int BM = 256, BN = 256, FM = 8, FN = 4;
+  constexpr int AB = 32, BB = 32, STAGE = (AB + BB) * 64;
+  __shared__ __attribute__((aligned(16))) bf16x8 lds[2 * STAGE];
+
+  const int nb = m_tiles * n_tiles;
+  const int b = xcd_remap(blockIdx.x, nb);
+  const int mt_i = b % m_tiles, nt_i = b / m_tiles;
+  const int m0 = mt_i * BM;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+  const int S = K >> 5;
+  const int n = K / BK;
+
+  auto group_of = [&](int gi) -> int {
+    if constexpr (EPI == EPI_SILU) {
+      constexpr int H = BN / 32;
+      return gi < H ? nt_i * H + gi : nt_i * H + (gi - H) + up_off;
+    }
+    return nt_i * (BN / 16) + gi;
+  };
+  int bgi[FN];  // LDS B group slot of the wave's column fragment j
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    if constexpr (EPI == EPI_SILU) {
+      bgi[j] = j < 2 ? wn * 2 + j : BN / 32 + wn * 2 + (j - 2);
+    } else {
+      bgi[j] = wn * FN + j;
+    }
+  }
+  // this thread's two DMA instructions of each unit: list index l = w + 8k (k = 0, 1)
+  //   A unit qa (full 128-B lines): 8 rows (l>>3)*128 + 64qa + 8(l&7) .. +7, lane ->
+  //     row + (lane>>3), LDS chunk p = lane&7 holding global chunk p ^ (row & 7)
+  //     (XOR swizzle: the A-fragment ds_read_b128 of 16 rows is conflict-free)
+  //   B unit qb: l = (wnb*2 + j2)*2 + ks -> slot of (wn = wnb, j = 2qb + j2)
+  const bf16* asrc[2][2];
+  int aslot[2][2];  // A: LDS offset in bf16x8 units
+  const bf16x8* bsrc[2][2];
+  int bslot[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int l = w + 8 * k, ks = l & 1, x = l >> 1;
+      const int R = (l >> 3) * 128 + 64 * q + 8 * (l & 7) + (lane >> 3);
+      int row = m0 + R;
+      row = row < M ? row : M - 1;
+      asrc[q][k] = X + (size_t)row * ldx + 8 * ((lane & 7) ^ (R & 7));
+      aslot[q][k] = R * 8 + (lane & 7) - lane;  // + lane (per-lane DMA slot) = R*8 + p
+      const int wnb = x >> 1, j = 2 * q + (x & 1);
+      int gs;
+      if constexpr (EPI == EPI_SILU) gs = j < 2 ? wnb * 2 + j : BN / 32 + wnb * 2 + (j - 2);
+      else gs = wnb * FN + j;
+      bsrc[q][k] = Wt + ((size_t)group_of(gs) * S + ks) * 64 + lane;
+      bslot[q][k] = AB + gs * 2 + ks;
+    }
+  auto issue_a = [&](int q, int kt) {
+    bf16x8* base = lds + (kt & 1) * STAGE;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)  // wave-uniform LDS base: lane 0's slot (lane*16 B added by HW)
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[q][k] + kt * BK),
+                                       (lds_ptr_t)(base + __builtin_amdgcn_readfirstlane(aslot[q][k])),
+                                       16, 0, 0);
+  };
+  auto issue_b = [&](int q, int kt) {
+    bf16x8* base = lds + (kt & 1) * STAGE;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[q][k] + (size_t)kt * 2 * 64),
+                                       (lds_ptr_t)(base + bslot[q][k] * 64), 16, 0, 0);
+  };
+  auto wait_units = [&](int units) {  // at most `units` of this thread's units in flight
+    switch (units) {
+      case 0: wait_vmcnt<0>(); break;
+      case 1: wait_vmcnt<2>(); break;
+      case 2: wait_vmcnt<4>(); break;
+      case 3: wait_vmcnt<6>(); break;
+      case 4: wait_vmcnt<8>(); break;
+      default: wait_vmcnt<10>(); break;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) ss[i] = 0.f;
+
+  // prologue: A0 B0 B1 A1 of tile 0, A0 B0 B1 of tile 1 (the steady-state order)
+  issue_a(0, 0);
+  issue_b(0, 0);
+  issue_b(1, 0);
+  issue_a(1, 0);
+  if (n > 1) {
+    issue_a(0, 1);
+    issue_b(0, 1);
+    issue_b(1, 1);
+  }
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  const int ar = lane & 15, aq = lane >> 4;
+  auto read_a = [&](const bf16x8* sa, int q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)  // row (rg*16 + ar), global chunk 4ks + aq, swizzled
+        af[i][ks] = sa[((wm * FM + 4 * q + i) * 16 + ar) * 8 + ((4 * ks + aq) ^ (ar & 7))];
+    if constexpr (NORM) {  // RMSNorm sums: fragment i of a quadrant by wave wn == i
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i != wn) continue;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = (float)af[i][ks][e];
+            ss[4 * q + i] = fmaf(v, v, ss[4 * q + i]);
+          }
+      }
+    }
+  };
+  auto read_b = [&](const bf16x8* sb, int q, bf16x8(&bfr)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = sb[(bgi[2 * q + j] * 2 + ks) * 64 + lane];
+  };
+  auto mma = [&](int qa, int qb, const bf16x8(&bfr)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qa + i][2 * qb + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af[i][ks], bfr[j][ks], acc[4 * qa + i][2 * qb + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  for (int t = 0; t < n; ++t) {
+    const bf16x8* sa = lds + (t & 1) * STAGE;
+    const bf16x8* sb = sa + AB * 64;
+    const int more1 = t + 1 < n, more2 = t + 2 < n;
+    // p0: A0, B0
+    wait_units(2 + 3 * more1);
+    read_a(sa, 0);
+    read_b(sb, 0, bf0);
+    if (more1) issue_a(1, t + 1);
+    mma(0, 0, bf0);
+    // p1: B1 (A0 kept)
+    wait_units(1 + 4 * more1);
+    read_b(sb, 1, bf1);
+    if (more2) issue_a(0, t + 2);
+    mma(0, 1, bf1);
+    // p2: A1 (B1 kept)
+    wait_units(4 * more1 + more2);
+    read_a(sa, 1);
+    if (more2) issue_b(0, t + 2);
+    mma(1, 1, bf1);
+    // p3: (A1, B0), both in registers
+    if (more2) issue_b(1, t + 2);
+    mma(1, 0, bf0);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  float* ss_row = reinterpret_cast<float*>(lds);
+  if constexpr (NORM) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if ((i & 3) != wn) continue;  // fragment i's rows were squared by wave (wm, i & 3)
+      float v = ss[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) ss_row[wm * (BM / 2) + 16 * i + lane] = v;
+    }
+    __syncthreads();
+  }
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int rl = wm * (BM / 2) + 16 * i + 4 * q + jj;
+      const int m = m0 + rl;
+      const bool valid = m < M;
+      float scale = 1.f;
+      if constexpr (NORM) scale = rsqrtf(ss_row[rl] / (float)K + eps);
+      if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          epi_store<EPI>(m, valid, nt_i * (BN / 32) + wn * 2 + j, r, acc[i][j][jj] * scale,
+                         acc[i][j + 2][jj] * scale, out, ldo, ea);
       } else if constexpr (EPI == EPI_QKV_ROPE) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -402,11 +643,27 @@ int launch_moe(const void* Wt, const void* X, int ldx, int M, int K, int N, int 
   return (int)hipGetLastError();
 }
 
+static int g_phased = 1;  // 256x256 tiles: phased pipeline (1) or the 2-stage kernel (0)
+
+template <int EPI, bool NORM>
+int launch_phased(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off,
+                  void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
+  const int m_tiles = (M + 255) / 256, n_tiles = N / 256;
+  hipLaunchKernelGGL((prefill_gemm8_kernel<EPI, NORM>), dim3(m_tiles * n_tiles), dim3(NT), 0, st,
+                     (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out,
+                     ldo, eps, ea);
+  return (int)hipGetLastError();
+}
+
 template <int EPI, bool NORM>
 int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off,
                 void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
   switch (tile) {
-    case 1: return launch<256, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 1:
+      // the phased kernel has no split-K: take it where the tiles already fill the chip
+      if (g_phased && (g_splitk == 1 || (!g_splitk && ((M + 255) / 256) * (N / 256) >= 160)))
+        return launch_phased<EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+      return launch<256, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 2: return launch<128, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 3: return launch<128, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 4: return launch<64, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
@@ -425,7 +682,8 @@ int pick_tile(int M, int N) {
     if (N % c[2]) continue;
     const long blocks = (long)((M + c[1] - 1) / c[1]) * (N / c[2]);
     if (!best) best = c[0];
-    if (blocks >= 200) return c[0];
+    // the phased 256x256 kernel pays from ~160 tiles (profiles/r2_prefill_gemm_phased.jsonl)
+    if (blocks >= (c[0] == 1 ? 160 : 200)) return c[0];
     best = c[0];
   }
   return best;

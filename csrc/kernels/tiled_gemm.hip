@@ -206,6 +206,9 @@ static int g_tiled_version = 2;  // 2 = LDS-DMA 8-wave kernel (prefill_gemm.h), 
 // Benchmarks / A-B tests: version 1|2, tile 0 (heuristic) or 1..5 (256x256, 128x256, 128x128,
 // 64x128, 64x256),
 // splitk 0 (heuristic), 1 (off) or a forced K-slice count.
+// 256x256 prefill tiles: 1 = phased pipeline (default), 0 = the 2-stage kernel (A/B).
+P2P_API void p2p_prefill_phased(int on) { pgemm::g_phased = on ? 1 : 0; }
+
 P2P_API void p2p_tiled_gemm_config(int version, int tile, int splitk) {
   if (version == 1 || version == 2) g_tiled_version = version;
   g_prefill_tile = (tile >= 0 && tile <= 5) ? tile : 0;

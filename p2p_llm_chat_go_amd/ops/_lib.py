@@ -122,6 +122,10 @@ def lib():
         if fn is not None:
             fn.argtypes = [c_int, c_int, c_int]
             fn.restype = None
+        fn = getattr(L, "p2p_prefill_phased", None)
+        if fn is not None:
+            fn.argtypes = [c_int]
+            fn.restype = None
         fn = getattr(L, "p2p_skinny_gemm_tune", None)
         if fn is not None:
             fn.argtypes = [c_int, c_int]
