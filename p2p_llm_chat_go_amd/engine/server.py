@@ -30,6 +30,23 @@ from .sampling import SamplingParams
 from .tokenizer import get_tokenizer
 
 
+class _RiderRow:
+    """A running sequence riding in a prefill batch as one row: behaves like a prompt of
+    length pos + 1 whose only read position is ``pos`` (O(1), not an O(context) list)."""
+    __slots__ = ("pos", "tok")
+
+    def __init__(self, pos: int, tok: int):
+        self.pos, self.tok = pos, tok
+
+    def __len__(self):
+        return self.pos + 1
+
+    def __getitem__(self, i):
+        if i != self.pos:
+            raise IndexError("rider rows only expose their last position")
+        return self.tok
+
+
 class EngineServer:
     def __init__(self, engine: Engine, tokenizer=None, model_name: str = "llama3.1",
                  max_batch: int | None = None, decode_chunk: int = 8,
@@ -294,7 +311,7 @@ class EngineServer:
             starts = [0] * len(prompts)
             for i in ride:  # running sequences: one decode row each (last token at r.pos)
                 r = self.sched.get(i)
-                prompts.append([0] * r.pos + [r.tokens[-1]])
+                prompts.append(_RiderRow(r.pos, r.tokens[-1]))
                 pages.append(list(r.pages))
                 starts.append(r.pos)
             ids = list(plan.prefill) + ride
