@@ -303,6 +303,77 @@ PYBIND11_MODULE(_native, m) {
                           ok(test_make_voucher(other, relay, peer, 1234567), relay, peer, 1234567),
                           ok(tampered, relay, peer, 1234567));
   });
+  m.def("rcmgr_check", [](const std::string& transport, int peer_streams, int proto_streams,
+                          int attempts) {
+    // A server host with small resource limits; a client holds `attempts` streams of one
+    // protocol open.  Returns (accepted, refused, a stream after release works, stats).
+    int accepted = 0, refused = 0;
+    bool reopened = false;
+    std::string stats;
+    {
+    py::gil_scoped_release rel;
+    auto srv = std::make_shared<Host>(PrivateKey::generate(KeyType::Ed25519));
+    auto cli = std::make_shared<Host>(PrivateKey::generate(KeyType::Ed25519));
+    ResourceLimits l;
+    l.peer_streams_inbound = peer_streams;
+    l.protocol_streams_inbound = proto_streams;
+    srv->resources().set_limits(l);
+    srv->set_stream_handler("/hold/1.0.0", [](StreamCtx& c) {
+      uint8_t b = 0;
+      c.io->set_read_timeout(20000);
+      try {
+        if (c.io->read_some(&b, 1) != 1) return;
+        c.io->write_all(&b, 1);
+        while (c.io->read_some(&b, 1) == 1) {
+        }
+      } catch (...) {
+      }
+      c.stream->close();
+    });
+    srv->listen(Multiaddr::parse(transport == "quic" ? "/ip4/127.0.0.1/udp/0/quic-v1"
+                                                     : "/ip4/127.0.0.1/tcp/0"));
+    std::vector<StreamCtx> held;
+    try {
+      cli->connect(srv->id(), srv->addrs(), 10000);
+      auto open_one = [&]() {
+        StreamCtx c = cli->new_stream(srv->id(), "/hold/1.0.0", 10000);
+        uint8_t b = 7;
+        c.io->write_all(&b, 1);
+        c.io->set_read_timeout(10000);
+        if (c.io->read_some(&b, 1) != 1 || b != 7) throw NetError("no echo");
+        return c;
+      };
+      for (int i = 0; i < attempts; ++i) {
+        try {
+          held.push_back(open_one());
+          ++accepted;
+        } catch (const std::exception&) {
+          ++refused;
+        }
+      }
+      for (auto& c : held) c.stream->close();
+      held.clear();
+      for (int i = 0; i < 100 && !reopened; ++i) {  // the server releases as handlers end
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        try {
+          StreamCtx c = open_one();
+          c.stream->close();
+          reopened = true;
+        } catch (const std::exception&) {
+        }
+      }
+    } catch (...) {
+      cli->close();
+      srv->close();
+      throw;
+    }
+    stats = srv->resources().stats().dump();
+    cli->close();
+    srv->close();
+    }
+    return py::make_tuple(accepted, refused, reopened, stats);
+  }, py::arg("transport") = "tcp", py::arg("peer_streams") = 4, py::arg("proto_streams") = 2048,
+     py::arg("attempts") = 8);
   m.def("quic_protocol_violation", [](const std::string& kind) {
     // a client sends a frame past the server's advertised limits; returns the client's
     // view of the close (the server must answer with the RFC 9000 error code)

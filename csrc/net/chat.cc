@@ -565,6 +565,10 @@ Json Node::metrics_json() {
   j.set("inbox_size", (long)inbox_.size());
   j.set("connected_peers", (long)(host_ ? host_->peers().size() : 0));
   j.set("connections_trimmed_total", (long)(host_ ? host_->trimmed() : 0));
+  if (host_) {
+    const Json rc = host_->resources().stats();
+    for (auto& kv : rc.fields()) j.set("rcmgr_" + kv.first, kv.second);
+  }
   return j;
 }
 

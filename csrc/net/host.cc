@@ -17,7 +17,8 @@ static constexpr int kUpgradeTimeoutMs = 10000;
 
 Host::Host(PrivateKey key, std::string agent)
     : key_(std::move(key)), id_(PeerId::from_public_key(key_.public_key())),
-      agent_(std::move(agent)) {
+      agent_(std::move(agent)),
+      rcmgr_(std::make_shared<ResourceManager>(ResourceLimits::from_env())) {
   set_stream_handler(kIdentifyProto, [this](StreamCtx& c) { identify_handler(c); });
   set_stream_handler(kPingProto, [](StreamCtx& c) {
     uint8_t buf[32];
@@ -79,7 +80,11 @@ void Host::listen(const Multiaddr& ma) {
         return;
       }
       Busy b(this);
-      add_session(c->remote_peer(), c, false);
+      try {
+        add_session(c->remote_peer(), c, false, true);
+      } catch (const std::exception&) {
+        c->close();
+      }
     });
     listen_addrs_.push_back(
         Multiaddr::parse("/ip4/" + host + "/udp/" + std::to_string(quic_->port()) + "/quic-v1"));
@@ -236,7 +241,7 @@ SessionPtr Host::upgrade_outbound(ConnPtr raw, const PeerId& expected, bool rela
   if (sec.early_muxer.empty()) ms_select(*b2, kYamuxProto);
   raw->set_read_timeout(0);
   auto sess = std::make_shared<YamuxSession>(b2, true);
-  add_session(sec.peer, sess, relayed);
+  add_session(sec.peer, sess, relayed, false);
   return sess;
 }
 
@@ -250,7 +255,7 @@ SessionPtr Host::upgrade_inbound(ConnPtr raw, bool relayed) {
   if (sec.early_muxer.empty()) ms_handle(*b2, {kYamuxProto});
   raw->set_read_timeout(0);
   auto sess = std::make_shared<YamuxSession>(b2, false);
-  add_session(sec.peer, sess, relayed);
+  add_session(sec.peer, sess, relayed, true);
   return sess;
 }
 
@@ -298,7 +303,12 @@ void Host::trim_connections(const PeerId& keep) {
   }
 }
 
-void Host::add_session(const PeerId& p, SessionPtr s, bool relayed) {
+void Host::add_session(const PeerId& p, SessionPtr s, bool relayed, bool inbound) {
+  std::shared_ptr<ResourceManager::Conn> rc = rcmgr_->open_conn(p, inbound);
+  if (!rc) {
+    s->close();
+    throw NetError("resource limit exceeded: connection from/to " + p.to_base58());
+  }
   SessionPtr old;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -316,9 +326,10 @@ void Host::add_session(const PeerId& p, SessionPtr s, bool relayed) {
              Busy b(this);
              handle_stream(st, p, relayed);
            },
-           [this, p, ws] {
+           [this, p, ws, rc]() mutable {
              Busy b(this);
              busy_--;
+             rc.reset();
              std::lock_guard<std::mutex> lk(mu_);
              auto it = sessions_.find(p);
              auto sp = ws.lock();
@@ -354,6 +365,11 @@ void Host::accept_loop(std::shared_ptr<TcpListener> l) {
 
 void Host::handle_stream(StreamPtr s, PeerId peer, bool relayed) {
   touch(peer);
+  std::shared_ptr<ResourceManager::Stream> rc = rcmgr_->open_stream(peer, true);
+  if (!rc) {  // system / transient / peer scope full
+    s->reset();
+    return;
+  }
   auto io = std::make_shared<BufConn>(s);
   std::set<std::string> protos;
   {
@@ -376,11 +392,11 @@ void Host::handle_stream(StreamPtr s, PeerId peer, bool relayed) {
     auto it = handlers_.find(proto);
     if (it != handlers_.end()) h = it->second;
   }
-  if (!h) {
+  if (!h || !rc->set_protocol(proto)) {  // unknown protocol, or its scope is full
     s->reset();
     return;
   }
-  StreamCtx ctx{s, io, peer, proto, relayed};
+  StreamCtx ctx{s, io, peer, proto, relayed, rc};
   h(ctx);
 }
 
@@ -486,7 +502,7 @@ SessionPtr Host::connect(const PeerId& p, const std::vector<Multiaddr>& addrs, i
       int port;
       if (a.quic_host_port(&h, &port)) {
         auto c = quic_for_dial()->dial(h, port, p, std::min(left, 5000));
-        add_session(p, c, false);
+        add_session(p, c, false, false);
         return c;
       }
       if (!a.tcp_host_port(&h, &port)) {
@@ -526,6 +542,8 @@ StreamCtx Host::new_stream(const PeerId& p, const std::string& proto, int timeou
     if (p == id_) throw NetError("failed to dial: dial to self attempted");
     s = connect(p, {}, timeout_ms);
   }
+  std::shared_ptr<ResourceManager::Stream> rc = rcmgr_->open_stream(p, false);
+  if (!rc) throw NetError("resource limit exceeded: outbound stream to " + p.to_base58());
   StreamPtr st = s->open_stream();
   auto io = std::make_shared<BufConn>(st);
   st->set_read_timeout(timeout_ms);
@@ -537,7 +555,8 @@ StreamCtx Host::new_stream(const PeerId& p, const std::string& proto, int timeou
   }
   st->set_read_timeout(0);
   st->protocol = proto;
-  return StreamCtx{st, io, p, proto, false};
+  rc->set_protocol(proto);
+  return StreamCtx{st, io, p, proto, false, rc};
 }
 
 long Host::ping(const PeerId& p, int timeout_ms) {

@@ -15,6 +15,7 @@
 #include "conn.h"
 #include "multiaddr.h"
 #include "quic.h"
+#include "rcmgr.h"
 #include "yamux.h"
 
 namespace p2p {
@@ -30,6 +31,7 @@ struct StreamCtx {
   PeerId peer;
   std::string protocol;
   bool relayed = false;
+  std::shared_ptr<ResourceManager::Stream> rc;  // resource-manager reservation
 };
 using StreamHandler = std::function<void(StreamCtx&)>;
 
@@ -105,6 +107,11 @@ class Host {
   void set_prefer_quic(bool on) { prefer_quic_ = on; }
   long trimmed() const { return trimmed_; }
 
+  // Resource manager (rcmgr.h): limits default to go-libp2p-like values with RCMGR_*
+  // environment overrides; inbound streams / connections over a limit are reset.
+  ResourceManager& resources() { return *rcmgr_; }
+
+
   void close();
   bool closed() const { return closed_; }
 
@@ -112,7 +119,7 @@ class Host {
   void accept_loop(std::shared_ptr<TcpListener> l);
   std::shared_ptr<QuicTransport> quic_for_dial();
   void handle_stream(StreamPtr s, PeerId peer, bool relayed);
-  void add_session(const PeerId& p, SessionPtr s, bool relayed);
+  void add_session(const PeerId& p, SessionPtr s, bool relayed, bool inbound);
   void run_identify(const PeerId& p, SessionPtr s);
   void touch(const PeerId& p);
   void trim_connections(const PeerId& keep);
@@ -138,6 +145,7 @@ class Host {
   std::vector<std::shared_ptr<TcpListener>> listeners_;
   std::shared_ptr<QuicTransport> quic_;  // the QUIC listener, or a dial-only socket
   bool prefer_quic_ = true;
+  std::shared_ptr<ResourceManager> rcmgr_;
   std::vector<Multiaddr> listen_addrs_;
   std::vector<Multiaddr> extra_addrs_;
   std::vector<std::thread> threads_;

@@ -12,6 +12,7 @@ import time
 import pytest
 
 from netutil import BIN, Procs, free_port, http, wait_http
+from p2p_llm_chat_go_amd.native import load as native
 
 pytestmark = pytest.mark.skipif(not os.path.exists(os.path.join(BIN, "p2p-node")),
                                 reason="native daemons not built")
@@ -523,6 +524,39 @@ def test_connection_manager_trims_to_low_watermark(procs):
         time.sleep(0.05)
     assert sorted(x["content"] for x in json.loads(http("GET", a + "/inbox")[1])) == \
         ["hi B", "hi C", "hi D", "hi E"]
+
+
+def test_resource_manager_refuses_inbound_connections(procs):
+    """RCMGR_* limits (go-libp2p's resource manager): with no inbound connection
+    allowed, B cannot open a connection to A; A can still dial B, and B then reaches A
+    over that connection.  The refusal shows in A's /metrics."""
+    d = start_directory(procs)
+    a = start_node(procs, "A", d, {"RCMGR_SYSTEM_CONNS_INBOUND": "0"})
+    b = start_node(procs, "B", d)
+    assert http("POST", b + "/send", {"to_username": "A", "content": "blocked"})[0] != 200
+
+    def metric(name):
+        for line in http("GET", a + "/metrics")[1].splitlines():
+            if line.startswith("p2p_" + name + " "):
+                return int(line.split()[1])
+        return -1
+
+    assert metric("rcmgr_refused_conns") >= 1
+    assert http("POST", a + "/send", {"to_username": "B", "content": "hi B"})[0] == 200
+    assert http("POST", b + "/send", {"to_username": "A", "content": "hi A"})[0] == 200
+    assert [x["content"] for x in _wait_inbox(a, 1)] == ["hi A"]
+    assert metric("rcmgr_conns_outbound") == 1 and metric("rcmgr_conns_inbound") == 0
+
+
+@pytest.mark.parametrize("transport", ["tcp", "quic"])
+def test_resource_manager_stream_limits(transport):
+    """Per-peer and per-protocol inbound stream scopes: streams past the limit are
+    reset, and the slots come back once the held streams close."""
+    accepted, refused, reopened, stats = native().rcmgr_check(transport, 4, 2048, 7)
+    assert (accepted, refused, reopened) == (4, 3, True), stats
+    assert json.loads(stats)["refused_streams"] == 3
+    accepted, refused, reopened, _ = native().rcmgr_check(transport, 100, 3, 6)
+    assert (accepted, refused, reopened) == (3, 3, True)
 
 
 # ------------------------------------------------------------------ QUIC transport

@@ -3,6 +3,7 @@ sharding of qkv / o / gate_up / down / vocab-parallel LM head against the
 unsharded engine (SURVEY §4.2 distributed tier (a)).  The TP model has the
 8B/70B head structure (32 q / 8 kv heads: one kv head per rank at world 8) and
 the EP model 8 experts (one per rank at world 8, Mixtral EP=8)."""
+import datetime
 import os
 import socket
 
@@ -120,7 +121,9 @@ def test_u64_max_allreduce_ordering():
 def _dying_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a bounded collective timeout: a survivor blocked on a dead peer's socket still raises
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
     from p2p_llm_chat_go_amd.engine import Engine
     from p2p_llm_chat_go_amd.parallel.comm import TPComm
 
