@@ -11,7 +11,7 @@ from .gemm import (EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, Fp8Weight, argmax_fi
                    tiled_shape, untile_weight)
 from .attention import (PAGE, HEAD_DIM, attn_oproj, attn_oproj_ok, attn_workspace,
                         flash_prefill, flash_tile, paged_attention, prefill_tiles, rope_cache)
-from .elementwise import advance, argmax, gather_rows
+from .elementwise import advance, argmax, gather_rows, l3_prefetch
 from .sampling import sample, sample_candidates, topk_candidates
 from ._lib import available as kernels_available, lib as kernel_lib, lib_path as kernel_lib_path
 

@@ -21,6 +21,23 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None =
     return out
 
 
+_SINKS = {}
+
+
+def l3_prefetch(t: torch.Tensor, nbytes: int | None = None, grid: int = 0):
+    """Pull t's bytes (its first nbytes) into the Infinity Cache with a discarded
+    streaming read (l3_prefetch.hip); no effect on values.  CPU tensors: no-op."""
+    if t.device.type != "cuda":
+        return
+    n = t.numel() * t.element_size() if nbytes is None else int(nbytes)
+    sink = _SINKS.get(t.device)
+    if sink is None:
+        sink = _SINKS[t.device] = torch.zeros(256 * 4, dtype=torch.int32, device=t.device)
+    L = _lib.lib()
+    _lib.check(L.p2p_l3_prefetch(t.data_ptr(), n, grid, sink.data_ptr(),
+                                 _lib.stream_ptr(t.device)), "l3_prefetch")
+
+
 def argmax(logits: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     M, V = logits.shape
     if out is None:
