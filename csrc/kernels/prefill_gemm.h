@@ -26,6 +26,7 @@ namespace pgemm {
 
 constexpr int BK = 64;
 constexpr int NT = 512;
+typedef int v4i __attribute__((ext_vector_type(4)));
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -34,7 +35,28 @@ struct SplitArgs {
   f32x4* slab;         // [tiles][splitk][FM*FN][NT] partial accumulators
   float* ss_slab;      // [tiles][splitk][BM] partial row sums of squares
   unsigned* counters;  // [tiles], zeroed before the launch
+  // parallel reduction (every slice reduces 8/splitk of the tile's waves; all slices of a
+  // tile must be resident together -- the host enables it only for grids <= the CU count):
+  unsigned* gen;       // [tiles] generation, bumped by each tile's last arriver
+  int* err;            // set if a slice waited past the spin bound (results invalid)
+  int parallel;
 };
+
+constexpr long long SPLIT_SPIN_TICKS = 20000000;  // 200 ms at the 100 MHz constant clock
+
+// Write-through (sc1) 16-byte store / load through a raw buffer resource (aux 16 = sc1):
+// hand-off payload that needs no release fence and is read past stale L1/L2 copies
+// (cdna_hip_programming.md Guideline 16, R1).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFFF,
+                                           0x00020000);
+}
+__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, int off, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, off, 0, 16);
+}
+__device__ __forceinline__ f32x4 load_sc1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -209,18 +231,145 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
       v += __shfl_xor(v, 32, 64);
       if (lane < 16) {
         if constexpr (SPLIT)
-          sp.ss_slab[((size_t)tile * splitk + split) * BM + wm * (BM / 2) + 16 * i + lane] = v;
+          __hip_atomic_store(&sp.ss_slab[((size_t)tile * splitk + split) * BM + wm * (BM / 2) + 16 * i + lane],
+                             v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
         else
           ss_row[wm * (BM / 2) + 16 * i + lane] = v;
       }
     }
     if constexpr (!SPLIT) __syncthreads();
   }
+  // ---- epilogue of one wave's accumulators (wave grid position wm_, wn_) ----
+  const int r = lane & 15, q = lane >> 4;
+  auto epilogue = [&](int wm_, int wn_, const f32x4 (&ac)[FM][FN], auto&& scale_of) {
+    int bg[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (EPI == EPI_SILU) {
+        constexpr int H = FN / 2;
+        bg[j] = j < H ? wn_ * H + j : BN / 32 + wn_ * H + (j - H);
+      } else {
+        bg[j] = wn_ * FN + j;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int rl = wm_ * (BM / 2) + 16 * i + 4 * q + jj;
+        int m = m0 + rl;
+        const bool valid = m < M;
+        float scale = scale_of(i, jj);
+        if constexpr (MOE) {
+          m = valid ? mrows[m] : 0;  // output row = the slot
+          if (ea.row_w && valid) scale *= ea.row_w[m];
+        }
+        if constexpr (EPI == EPI_SILU) {
+          constexpr int H = FN / 2;
+#pragma unroll
+          for (int j = 0; j < H; ++j)
+            epi_store<EPI>(m, valid, nt_i * (BN / 32) + wn_ * H + j, r, ac[i][j][jj] * scale,
+                           ac[i][j + H][jj] * scale, out, ldo, ea);
+        } else if constexpr (EPI == EPI_QKV_ROPE) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int g = nt_i * (BN / 16) + bg[j];
+            const int kk = g & 7;
+            const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+            float2 c = float2{1.f, 0.f};
+            int slot = -1;
+            if (valid) {
+              c = ea.cs[(size_t)ea.pos[m] * 64 + dd];
+              slot = ea.slots[m];
+            }
+            epi_store<EPI>(m, valid, g, r, ac[i][j][jj] * scale, 0.f, out, ldo, ea, c, slot);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            epi_store<EPI>(m, valid, nt_i * (BN / 16) + bg[j], r, ac[i][j][jj] * scale, 0.f, out,
+                           ldo, ea);
+        }
+      }
+    }
+  };
+  auto rstd_of = [&](float t) { return rsqrtf(t / (float)K + eps); };
+
   if constexpr (SPLIT) {
-    // split-K hand-off (agent-scope release/acquire through a per-tile ticket):
-    // every slice stores its fp32 partial tile, the last arriver reduces all
-    // slices in slice order (deterministic) and runs the epilogue.
     f32x4* my = sp.slab + ((size_t)tile * splitk + split) * (FM * FN) * NT;
+    // (the 256x256 tile keeps the serial reduction: a second set of 128 accumulator
+    // registers for the shared reduction would spill its main loop)
+    if (BM * BN <= 128 * 256 && sp.parallel) {
+      // ---- parallel split-K: write-through slabs, one generation flip per tile, then
+      // every slice reduces and stores 8/splitk of the tile's waves (no serial reducer,
+      // no release fence) ----
+      const __amdgpu_buffer_rsrc_t rsl = raw_rsrc(sp.slab);
+      const size_t tile_v = (size_t)tile * splitk * (FM * FN) * NT;  // f32x4 index of slice 0
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          store_sc1(rsl, (int)((tile_v + ((size_t)split * FM * FN + i * FN + j) * NT + tid) * 16),
+                    acc[i][j]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned g0 = __hip_atomic_load(&sp.gen[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // read the generation BEFORE arriving
+        const unsigned t = __hip_atomic_fetch_add(&sp.counters[tile], 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if (t == (unsigned)splitk - 1) {
+          (void)__hip_atomic_exchange(&sp.counters[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // re-armed before the flip
+          __hip_atomic_store(&sp.gen[tile], g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          const long long t0 = wall_clock64();
+          while (__hip_atomic_load(&sp.gen[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
+            if (wall_clock64() - t0 > SPLIT_SPIN_TICKS) {
+              __hip_atomic_store(sp.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+      }
+      __syncthreads();
+      constexpr int kWavesPerTile = NT / 64;
+      const int vw_n = kWavesPerTile / splitk;  // host guarantees splitk | 8
+      if (w >= vw_n) return;
+      const int vw = split * vw_n + w;  // the tile wave whose accumulators this wave finishes
+      // acc is dead after the slab stores: it becomes the total (one fragment row of
+      // loads in flight at a time keeps the 256x256 tile inside its register budget)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s2 = 0; s2 < splitk; ++s2) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          f32x4 part[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            part[j] = load_sc1(rsl, (int)((tile_v + ((size_t)s2 * FM * FN + i * FN + j) * NT +
+                                           vw * 64 + lane) * 16));
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] += part[j];
+        }
+      }
+      epilogue(vw >> 2, vw & 3, acc, [&](int i, int jj) {
+        if constexpr (!NORM) return 1.f;
+        const int rl = (vw >> 2) * (BM / 2) + 16 * i + 4 * q + jj;
+        float t = 0.f;
+        for (int s2 = 0; s2 < splitk; ++s2)
+          t += __hip_atomic_load(&sp.ss_slab[((size_t)tile * splitk + s2) * BM + rl],
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return rstd_of(t);
+      });
+      return;
+    }
+    // ---- serial split-K: agent-scope release/acquire through a per-tile ticket; every
+    // slice stores its fp32 partial tile, the last arriver reduces all slices in slice
+    // order (deterministic) and runs the epilogue ----
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -266,49 +415,10 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
     if (tid == 0) sp.counters[tile] = 0;
   }
 
-  // ---- epilogue ----
-  const int r = lane & 15, q = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int rl = wm * (BM / 2) + 16 * i + 4 * q + jj;
-      int m = m0 + rl;
-      const bool valid = m < M;
-      float scale = 1.f;
-      if constexpr (NORM) scale = rsqrtf(ss_row[rl] / (float)K + eps);
-      if constexpr (MOE) {
-        m = valid ? mrows[m] : 0;  // output row = the slot
-        if (ea.row_w && valid) scale *= ea.row_w[m];
-      }
-      if constexpr (EPI == EPI_SILU) {
-        constexpr int H = FN / 2;
-#pragma unroll
-        for (int j = 0; j < H; ++j)
-          epi_store<EPI>(m, valid, nt_i * (BN / 32) + wn * H + j, r, acc[i][j][jj] * scale,
-                         acc[i][j + H][jj] * scale, out, ldo, ea);
-      } else if constexpr (EPI == EPI_QKV_ROPE) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int g = nt_i * (BN / 16) + bgi[j];
-          const int kk = g & 7;
-          const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
-          float2 c = float2{1.f, 0.f};
-          int slot = -1;
-          if (valid) {
-            c = ea.cs[(size_t)ea.pos[m] * 64 + dd];
-            slot = ea.slots[m];
-          }
-          epi_store<EPI>(m, valid, g, r, acc[i][j][jj] * scale, 0.f, out, ldo, ea, c, slot);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          epi_store<EPI>(m, valid, nt_i * (BN / 16) + bgi[j], r, acc[i][j][jj] * scale, 0.f, out,
-                         ldo, ea);
-      }
-    }
-  }
+  epilogue(wm, wn, acc, [&](int i, int jj) {
+    if constexpr (!NORM) return 1.f;
+    return rstd_of(ss_row[wm * (BM / 2) + 16 * i + 4 * q + jj]);
+  });
 }
 
 // ---------------------------------------------------------------------------------
@@ -585,6 +695,21 @@ static bool split_ws(size_t bytes, hipStream_t st, char** out) {
 }
 
 static int g_splitk = 0;  // 0 = heuristic, 1 = never split, >1 = forced
+static int g_split_parallel = 1;  // parallel split-K reduction where residency allows
+
+// CUs of the current device (cached per device): the parallel reduction needs every slice
+// of a tile resident at once, so it is used only for grids of at most one block per CU.
+static int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cached[dev] = n > 0 ? n : -1;
+  }
+  return cached[dev] > 0 ? cached[dev] : 0;
+}
 
 // LDS stages per tile shape.  Measured on MI355X (bench/prefill_gemm_bench.py): the
 // 64-row tiles are latency-bound streams and want 3-4 stages in flight; the 128/256-row
@@ -607,23 +732,28 @@ int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_o
   // (measured on MI355X at 8B shapes: ~400 blocks, >= 16 k-tiles per slice)
   int splitk = g_splitk ? g_splitk : std::min(8, std::max(1, std::min(400 / tiles, nk / 16)));
   splitk = std::max(1, std::min(splitk, nk / 4));
-  if (splitk > 1 && (size_t)tiles * sizeof(unsigned) <= kCounterBytes) {
+  if (splitk > 1 && (size_t)tiles * sizeof(unsigned) < kCounterBytes / 2) {
     constexpr int FM = BM / 32, FN = BN / 64;
     const size_t slab = (size_t)tiles * splitk * FM * FN * NT * sizeof(f32x4);
     const size_t ssb = (size_t)tiles * splitk * BM * sizeof(float);
     char* ws = nullptr;
-    if (split_ws(slab + ssb, st, &ws)) {
+    if (split_ws(slab + ssb, st, &ws) && slab + ssb < 0x7FFFFFFF) {
       // counters live at the END of the workspace at a fixed offset from the end so a
-      // grown workspace keeps them zeroed; see split_ws
-      SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab),
-                   (unsigned*)(ws + g_split_ws.bytes - kCounterBytes)};
+      // grown workspace keeps them zeroed; see split_ws.  Layout of that region (u32):
+      // [0, n/2) arrival tickets, [n/2, n-1) generations, [n-1] the fault word.
+      unsigned* ctr = (unsigned*)(ws + g_split_ws.bytes - kCounterBytes);
+      constexpr size_t nw = kCounterBytes / sizeof(unsigned);
+      const int cus = cu_count();
+      const int par = g_split_parallel && (8 % splitk) == 0 && cus > 0 && tiles * splitk <= cus;
+      SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), ctr, ctr + nw / 2,
+                   (int*)(ctr + nw - 1), par};
       hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, true, STAGES>),
                          dim3(tiles * splitk), dim3(NT), 0, st, (const bf16x8*)Wt,
                          (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, sp);
       return (int)hipGetLastError();
     }
   }
-  SplitArgs none{1, nullptr, nullptr, nullptr};
+  SplitArgs none{1, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, false, STAGES>), dim3(tiles), dim3(NT), 0,
                      st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off,
                      out, ldo, eps, ea, none);
@@ -636,7 +766,7 @@ int launch_moe(const void* Wt, const void* X, int ldx, int M, int K, int N, int 
   constexpr int STAGES = stages_for<BM, BN>();
   const int m_tiles = (M + BM - 1) / BM;
   const int n_tiles = N / BN;
-  SplitArgs none{1, nullptr, nullptr, nullptr};
+  SplitArgs none{1, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, false, STAGES, true>),
                      dim3(m_tiles * n_tiles, ea.n_experts), dim3(NT), 0, st, (const bf16x8*)Wt,
                      (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, none);

@@ -209,6 +209,24 @@ static int g_tiled_version = 2;  // 2 = LDS-DMA 8-wave kernel (prefill_gemm.h), 
 // 256x256 prefill tiles: 1 = phased pipeline (default), 0 = the 2-stage kernel (A/B).
 P2P_API void p2p_prefill_phased(int on) { pgemm::g_phased = on ? 1 : 0; }
 
+// Split-K reduction mode (A/B): 1 = parallel (every slice reduces a share, default where
+// residency allows), 0 = serial (the last arriving slice reduces the whole tile).
+P2P_API void p2p_tiled_split_parallel(int on) { pgemm::g_split_parallel = on ? 1 : 0; }
+
+// Nonzero if a parallel split-K slice waited past its spin bound since the last call
+// (its tile's output is invalid); clears the word.  Synchronises the current device.
+P2P_API int p2p_tiled_split_fault() {
+  if (!pgemm::g_split_ws.buf) return 0;
+  int* w = (int*)((char*)pgemm::g_split_ws.buf + pgemm::g_split_ws.bytes - sizeof(unsigned));
+  int v = 0;
+  if (hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (v) {
+    const int z = 0;
+    (void)hipMemcpy(w, &z, sizeof(int), hipMemcpyHostToDevice);
+  }
+  return v;
+}
+
 P2P_API void p2p_tiled_gemm_config(int version, int tile, int splitk) {
   if (version == 1 || version == 2) g_tiled_version = version;
   g_prefill_tile = (tile >= 0 && tile <= 5) ? tile : 0;

@@ -195,6 +195,8 @@ class LlamaModel:
         if self.device.type == "cuda" and int(ws.err.item()) != 0:
             ws.err.zero_()
             raise RuntimeError("fused attention/o_proj hand-off timed out (results invalid)")
+        if self.device.type == "cuda" and ops.tiled_split_fault():
+            raise RuntimeError("split-K GEMM slice wait timed out (results invalid)")
         if self.comm is not None and hasattr(self.comm, "check"):
             self.comm.check()
 

@@ -123,6 +123,14 @@ def lib():
         if fn is not None:
             fn.argtypes = [c_int, c_int, c_int]
             fn.restype = None
+        fn = getattr(L, "p2p_tiled_split_parallel", None)
+        if fn is not None:
+            fn.argtypes = [c_int]
+            fn.restype = None
+        fn = getattr(L, "p2p_tiled_split_fault", None)
+        if fn is not None:
+            fn.argtypes = []
+            fn.restype = c_int
         fn = getattr(L, "p2p_prefill_phased", None)
         if fn is not None:
             fn.argtypes = [c_int]

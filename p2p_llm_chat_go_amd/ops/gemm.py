@@ -151,6 +151,20 @@ def tiled_config(version: int = 2, tile: int = 0, splitk: int = 0):
     _lib.lib().p2p_tiled_gemm_config(int(version), int(tile), int(splitk))
 
 
+def tiled_split_parallel(on: bool = True):
+    """Split-K reduction of the tiled kernel: parallel (every K slice finishes a share of
+    its tile; default where the grid fits one block per CU) or serial (the last arriving
+    slice reduces the whole tile)."""
+    _lib.lib().p2p_tiled_split_parallel(int(bool(on)))
+
+
+def tiled_split_fault() -> int:
+    """Nonzero if a parallel split-K slice gave up waiting for its tile (output invalid);
+    clears the flag.  Synchronises the device."""
+    L = _lib.lib()
+    return int(L.p2p_tiled_split_fault()) if hasattr(L, "p2p_tiled_split_fault") else 0
+
+
 def _code(wt, M, epi, norm, waves):
     if waves:
         return waves

@@ -465,19 +465,24 @@ def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
 
 
 # ------------------------------------------------------------ tiled (prefill) GEMM
-TILED_CFGS = [(2, 0, 0), (2, 1, 1), (2, 2, 1), (2, 3, 1), (2, 3, 4), (2, 1, 3), (2, 4, 1),
-              (2, 4, 3), (2, 5, 2), (1, 0, 0)]
+# (version, tile, splitk[, parallel split-K reduction]); split-K grids of at most one block
+# per CU with splitk | 8 take the parallel reduction unless the 4th field is 0
+TILED_CFGS = [(2, 0, 0), (2, 1, 1), (2, 2, 1), (2, 3, 1), (2, 3, 4), (2, 3, 4, 0), (2, 1, 3),
+              (2, 4, 1), (2, 4, 2), (2, 4, 4), (2, 4, 4, 0), (2, 4, 3), (2, 5, 2), (1, 0, 0)]
 
 
-@pytest.fixture(params=TILED_CFGS, ids=lambda c: "v%d_t%d_s%d" % c)
+@pytest.fixture(params=TILED_CFGS, ids=lambda c: "v%d_t%d_s%d" % c[:3] + ("_serial" if len(c) > 3 else ""))
 def tiled_cfg(request):
-    from p2p_llm_chat_go_amd.ops.gemm import set_tiled_min_m, tiled_config
+    from p2p_llm_chat_go_amd.ops.gemm import set_tiled_min_m, tiled_config, tiled_split_parallel
 
-    tiled_config(*request.param)
+    tiled_config(*request.param[:3])
+    tiled_split_parallel(request.param[3] if len(request.param) > 3 else 1)
     set_tiled_min_m(1)  # small M goes through the tiled kernel too
     yield request.param
     set_tiled_min_m(65)
     tiled_config(2, 0, 0)
+    tiled_split_parallel(1)
+    assert ops.tiled_split_fault() == 0
 
 
 @pytest.mark.parametrize("M", [7, 65, 200, 513])
