@@ -43,7 +43,10 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // one 16-byte la
 constexpr int MAX_RANKS = 8;
 constexpr int MAX_BLOCKS = 64;
 constexpr int NT = 256;
-constexpr size_t FLAG_BYTES = 2ull * MAX_RANKS * MAX_BLOCKS * 4;
+// two flag regions: A = one-shot flags and two-shot phase 1 (src -> owner), B = two-shot
+// phase 2 (owner -> every rank)
+constexpr size_t FLAG_REGION = 2ull * MAX_RANKS * MAX_BLOCKS * 4;
+constexpr size_t FLAG_BYTES = 2 * FLAG_REGION;
 // default spin bound in wall-clock ticks (100 MHz constant clock): 5 s; a healthy call
 // waits microseconds (p2p_car_set_timeout_ms overrides, e.g. for fault-injection tests)
 __device__ long long g_spin_ticks = 500000000ll;
@@ -56,6 +59,23 @@ struct Peers {
 
 __device__ __forceinline__ unsigned* flag_ptr(char* base, int parity, int src, int blk) {
   return reinterpret_cast<unsigned*>(base) + ((size_t)parity * MAX_RANKS + src) * MAX_BLOCKS + blk;
+}
+
+__device__ __forceinline__ unsigned* flag2_ptr(char* base, int parity, int src, int blk) {
+  return flag_ptr(base + FLAG_REGION, parity, src, blk);
+}
+
+// bounded wait until *f == seq (system-scope acquire polls, s_sleep between them)
+__device__ __forceinline__ void wait_flag(unsigned* f, unsigned seq, int* err) {
+  const long long t0 = wall_clock64();
+  const long long bound = g_spin_ticks;
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+    if (wall_clock64() - t0 > bound) {
+      atomicOr(err, 1);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
 }
 
 __device__ __forceinline__ v4u* data_ptr(char* base, size_t max_bytes, int parity, int src) {
@@ -153,6 +173,102 @@ __global__ __launch_bounds__(NT) void car_kernel(Peers peers, int rank, int worl
   }
 }
 
+// Two-shot sum (reduce-scatter + all-gather) for mid-size messages: rank s owns shard s
+// of the vectors.  Per call, block b of rank r:
+//   1. pushes its part of every shard s of `partial` to OWNER s only (slot [parity][r] of
+//      s's buffer, at the shard's offsets) and posts flag A[parity][r][b] on s;
+//   2. as owner of shard r: waits for flag A of every source, sums h + partials in rank
+//      order (the one-shot formula, so both forms are bit-identical), and pushes the
+//      result to every rank (slot [parity][r], shard r's offsets), posting flag B;
+//   3. waits for flag B of every owner and copies the reduced shards into h.
+// Each rank sends 2 (W-1)/W of the message over xGMI instead of the one-shot's (W-1),
+// in two dependent hops instead of one.  Slot reuse follows the one-shot argument: a
+// rank writes parity k&1 in call k+2 only after every peer posted a call-(k+1) flag.
+__global__ __launch_bounds__(NT) void car2_kernel(Peers peers, int rank, int world,
+                                                  size_t max_bytes, const v4u* __restrict__ in,
+                                                  bf16x8* __restrict__ h, int n_vec,
+                                                  unsigned* __restrict__ counters,
+                                                  int* __restrict__ err) {
+  const int blk = blockIdx.x, nblk = gridDim.x;
+  const int ns = (n_vec + world - 1) / world;  // vectors per shard (the last may be short)
+  const int per = (ns + nblk - 1) / nblk;      // this block's part of every shard
+  __shared__ unsigned s_seq;
+  __shared__ int s_failed;
+  if (threadIdx.x == 0) {
+    s_seq = counters[blk] + 1;
+    s_failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const unsigned seq = s_seq;
+  const int parity = seq & 1;
+  auto range = [&](int s, int& a, int& b) {
+    a = min(n_vec, s * ns + blk * per);
+    b = min(min(n_vec, (s + 1) * ns), a + per);
+  };
+  // 1. scatter: my part of shard s -> owner s
+  for (int s = 0; s < world; ++s) {
+    int a, b;
+    range(s, a, b);
+    v4u* dst = data_ptr(peers.base[s], max_bytes, parity, rank);
+    for (int i = a + threadIdx.x; i < b; i += NT) dst[i] = in[i];
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < world)
+    __hip_atomic_store(flag_ptr(peers.base[threadIdx.x], parity, rank, blk), seq,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // 2. reduce my shard, push the result to every rank
+  if (threadIdx.x < world && !s_failed)
+    wait_flag(flag_ptr(peers.base[rank], parity, threadIdx.x, blk), seq, err);
+  __syncthreads();
+  {
+    int a, b;
+    range(rank, a, b);
+    for (int i = a + threadIdx.x; i < b; i += NT) {
+      float acc[8];
+      const bf16x8 hv = h[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = (float)hv[j];
+      for (int p = 0; p < world; ++p) {  // fixed rank order (= the one-shot sum)
+        const v4u raw = __builtin_nontemporal_load(data_ptr(peers.base[rank], max_bytes, parity, p) + i);
+        bf16x8 v;
+        memcpy(&v, &raw, 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+      v4u ov;
+      memcpy(&ov, &o, 16);
+      for (int q = 0; q < world; ++q) data_ptr(peers.base[q], max_bytes, parity, rank)[i] = ov;
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < world)
+    __hip_atomic_store(flag2_ptr(peers.base[threadIdx.x], parity, rank, blk), seq,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // 3. gather every owner's reduced shard into h
+  if (threadIdx.x < world && !s_failed)
+    wait_flag(flag2_ptr(peers.base[rank], parity, threadIdx.x, blk), seq, err);
+  __syncthreads();
+  for (int s = 0; s < world; ++s) {
+    int a, b;
+    range(s, a, b);
+    const v4u* src = data_ptr(peers.base[rank], max_bytes, parity, s);
+    for (int i = a + threadIdx.x; i < b; i += NT) {
+      const v4u raw = __builtin_nontemporal_load(src + i);
+      memcpy(&h[i], &raw, 16);
+    }
+  }
+  if (threadIdx.x == 0) {
+    counters[blk] = seq;
+    if (blk == 0)
+      for (int j = nblk; j < MAX_BLOCKS; ++j) counters[j] = seq;  // keep idle blocks in step
+  }
+}
+
 int launch(int op, void* const* bases, int rank, int world, size_t max_bytes, const void* in,
            void* out, int n_vec, unsigned* counters, int* err, int blocks, void* stream) {
   if (world < 1 || world > MAX_RANKS || rank < 0 || rank >= world || n_vec <= 0) return 1;
@@ -230,6 +346,25 @@ P2P_API int p2p_car_allreduce_add(void* const* bases, int rank, int world, size_
   if (n % 8) return 1;
   return launch(OP_ADD_BF16, bases, rank, world, max_bytes, partial, h, n / 8, counters, err,
                 blocks, stream);
+}
+
+// Two-shot form of p2p_car_allreduce_add (same contract and bit-identical result): for
+// messages where pushing the whole partial to every peer costs more link time than a
+// second hop (see parallel/custom_ar.py for the crossover).
+P2P_API int p2p_car_allreduce_add_2shot(void* const* bases, int rank, int world, size_t max_bytes,
+                                        const void* partial, void* h, int n, unsigned* counters,
+                                        int* err, int blocks, void* stream) {
+  if (n % 8 || world < 1 || world > MAX_RANKS || rank < 0 || rank >= world || n <= 0) return 1;
+  const int n_vec = n / 8;
+  if ((size_t)n_vec * 16 > max_bytes) return 1;
+  Peers peers = {};
+  for (int p = 0; p < world; ++p) peers.base[p] = (char*)bases[p];
+  const int ns = (n_vec + world - 1) / world;
+  if (blocks <= 0) blocks = (ns + NT * 2 - 1) / (NT * 2);
+  blocks = max(1, min(blocks, MAX_BLOCKS));
+  hipLaunchKernelGGL(car2_kernel, dim3(blocks), dim3(NT), 0, (hipStream_t)stream, peers, rank,
+                     world, max_bytes, (const v4u*)partial, (bf16x8*)h, n_vec, counters, err);
+  P2P_CHECK_LAUNCH();
 }
 
 // keys[n] = max over ranks of keys[n] (u64, n even, in place allowed).

@@ -49,6 +49,8 @@ _SIGS = {
     "p2p_car_handle_size": [],
     "p2p_car_allreduce_add": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p, c_int,
                               c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_car_allreduce_add_2shot": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p,
+                                    c_int, c_void_p, c_void_p, c_int, c_void_p],
     "p2p_car_allreduce_max_u64": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p,
                                   c_int, c_void_p, c_void_p, c_int, c_void_p],
     "p2p_car_all_gather": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p,

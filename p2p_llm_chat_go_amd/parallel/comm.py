@@ -25,7 +25,7 @@ _SIGN = -(2 ** 63)
 
 
 class TPComm:
-    def __init__(self, group=None, custom_ar: bool | None = None, car_max_bytes: int = 1 << 21):
+    def __init__(self, group=None, custom_ar: bool | None = None, car_max_bytes: int | None = None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -33,6 +33,10 @@ class TPComm:
         if custom_ar is None:
             custom_ar = os.environ.get("P2P_CUSTOM_AR", "1") == "1"
         self.want_custom_ar = custom_ar
+        # one-/two-shot kernels cover sums up to this size (70B: every row-parallel sum
+        # below the overlapped-RCCL threshold of 256 rows); larger ones use RCCL
+        if car_max_bytes is None:
+            car_max_bytes = int(os.environ.get("P2P_CAR_MAX_BYTES", str(4 << 20)))
         self.car_max_bytes = car_max_bytes
         self.car = None
 

@@ -13,6 +13,12 @@ sampling: a MAX all-reduce of the greedy argmax keys (u64) and an all-gather
 of per-shard top-k candidates.  With those, a TP decode graph holds no RCCL
 call at all (one-shot kernels only).
 
+Mid-size sums (prefill chunks below the overlapped-RCCL row threshold, batched decode)
+take the two-shot form of the same kernel (``allreduce_add_`` picks it from
+``two_shot_min`` bytes at 4+ ranks): reduce-scatter to shard owners, then all-gather of
+the reduced shards -- 2(W-1)/W of the message per rank over xGMI instead of W-1, in two
+hops instead of one, with a bit-identical result.
+
 Handles are exchanged with ``dist.all_gather_object`` over the TP group (any
 backend).  Messages above ``max_bytes`` fall back to the caller's RCCL path.
 Timeouts are loud: ``check()`` raises once a peer failed to arrive within the
@@ -21,6 +27,7 @@ spin bound (``LlamaModel.check_faults`` calls it wherever the host syncs).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -44,6 +51,9 @@ class CustomAllReduce:
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         self.max_bytes = int(max_bytes)
+        # two-shot from this many bytes (and 4+ ranks: at 2 ranks both forms move the same
+        # bytes and the one-shot has one hop less)
+        self.two_shot_min = int(os.environ.get("P2P_CAR_2SHOT_MIN", str(512 << 10)))
         L = self.L = _lib.lib()
         with torch.cuda.device(self.device):
             size = L.p2p_car_buffer_bytes(self.max_bytes)
@@ -106,14 +116,21 @@ class CustomAllReduce:
         """Spin bound of the one-shot kernels (default 5 s); fault-injection tests lower it."""
         _lib.check(_lib.lib().p2p_car_set_timeout_ms(int(ms)), "car_set_timeout_ms")
 
-    def allreduce_add_(self, h: torch.Tensor, partial: torch.Tensor, blocks: int = 0):
-        """h += sum over ranks of partial (bf16, same shape, contiguous)."""
+    def use_two_shot(self, nbytes: int) -> bool:
+        return self.world >= 4 and nbytes >= self.two_shot_min
+
+    def allreduce_add_(self, h: torch.Tensor, partial: torch.Tensor, blocks: int = 0,
+                       two_shot: bool | None = None):
+        """h += sum over ranks of partial (bf16, same shape, contiguous).  two_shot: None =
+        by size (``use_two_shot``); both forms give bit-identical sums."""
         assert self.fits(partial) and h.is_contiguous() and h.numel() == partial.numel()
-        _lib.check(self.L.p2p_car_allreduce_add(self._bases, self.rank, self.world,
-                                                self.max_bytes, partial.data_ptr(), h.data_ptr(),
-                                                partial.numel(), self.counters.data_ptr(),
-                                                self.err.data_ptr(), blocks,
-                                                _lib.stream_ptr(h.device)), "car_allreduce_add")
+        if two_shot is None:
+            two_shot = self.use_two_shot(partial.numel() * 2)
+        fn = self.L.p2p_car_allreduce_add_2shot if two_shot else self.L.p2p_car_allreduce_add
+        _lib.check(fn(self._bases, self.rank, self.world, self.max_bytes, partial.data_ptr(),
+                      h.data_ptr(), partial.numel(), self.counters.data_ptr(),
+                      self.err.data_ptr(), blocks, _lib.stream_ptr(h.device)),
+                   "car_allreduce_add" + ("_2shot" if two_shot else ""))
         return h
 
     def check(self):

@@ -196,3 +196,95 @@ def test_custom_allreduce_two_ranks_one_gpu():
     [p.join(timeout=60) for p in ps]
     for rank, ok, info in res:
         assert ok, (rank, info)
+
+
+def _two_shot_worker(rank, world, port, q):
+    """Two-shot sum (reduce-scatter to shard owners + all-gather) against the one-shot
+    form (bit-identical) and the fp32 reference: uneven shards, alternating forms and
+    sizes with a delayed peer, hipGraph replay."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    car = None
+    try:
+        from p2p_llm_chat_go_amd.parallel.custom_ar import CustomAllReduce
+
+        torch.cuda.set_device(0)
+        car = CustomAllReduce(device="cuda:0", max_bytes=4 << 20)
+        call = 0
+        same, errs = True, []
+        sizes = [8, 4096 + 8, 8 * world * 3 + 8, 300008, 1 << 20, 2 << 20, 24, 1 << 19] * 2
+        outs = []
+        for i, n in enumerate(sizes):
+            call += 1
+            h0 = _data(7 + call, n)
+            p = _data(1000 * call + rank, n).cuda()
+            h1, h2 = h0.cuda(), h0.cuda()
+            if rank == world - 1 and i % 3 == 1:
+                torch.cuda._sleep(2_000_000)  # the slow peer
+            car.allreduce_add_(h1, p, two_shot=False)
+            car.allreduce_add_(h2, p, two_shot=True)
+            outs.append((h1, h2, _expect(h0, world, n, call)))
+        torch.cuda.synchronize()
+        for h1, h2, ref in outs:
+            same = same and torch.equal(h1, h2)
+            errs.append(((h2.cpu().float() - ref.float()).abs().max() /
+                         (ref.float().abs().max() + 1e-6)).item())
+        n = 1 << 18
+        h = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+        p = torch.ones(n, dtype=torch.bfloat16, device="cuda") * (rank + 1)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(4):
+                    car.allreduce_add_(h, p, two_shot=True)
+        torch.cuda.synchronize()
+        h.zero_()
+        torch.cuda.synchronize()
+        dist.barrier()
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        graph_ok = bool((h.float() == 12 * sum(r + 1 for r in range(world))).all().item())
+        # timing (virtual ranks share one GPU: relative only, not xGMI numbers)
+        tim = {}
+        for n in (1 << 17, 1 << 20, 2 << 20):
+            hh = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+            pp = torch.ones_like(hh)
+            for two in (False, True):
+                dist.barrier()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                car.allreduce_add_(hh, pp, two_shot=two)
+                e0.record()
+                for _ in range(10):
+                    car.allreduce_add_(hh, pp, two_shot=two)
+                e1.record()
+                torch.cuda.synchronize()
+                tim["%s_%dKiB" % ("2shot" if two else "1shot", n * 2 >> 10)] = round(
+                    e0.elapsed_time(e1) * 100, 1)
+        car.check()
+        q.put((rank, same and max(errs) < 1e-2 and graph_ok, (same, max(errs), graph_ok, tim)))
+    except Exception:
+        import traceback
+
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        if car is not None:
+            dist.barrier()
+            car.close()
+        dist.destroy_process_group()
+
+
+def test_custom_allreduce_two_shot_four_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 4
+    port = _port()
+    ps = [ctx.Process(target=_two_shot_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in ps]
+    res = [q.get(timeout=300) for _ in range(world)]
+    [p.join(timeout=60) for p in ps]
+    [p.terminate() for p in ps if p.is_alive()]
+    for rank, ok, info in res:
+        print("rank", rank, info)
+        assert ok, (rank, info)
