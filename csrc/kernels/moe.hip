@@ -205,7 +205,129 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict
   }
 }
 
+// ---- expert-parallel all-to-all (DP attention + EP): dispatch, slot grouping, combine ----
+// Slot s = token * K + k goes to rank dest = expert / El.  Its send row is
+//   static capacity C > 0 : dest * C + pos      (graph-capturable, padded)
+//   exact (C == 0)        : off[dest] + pos     (packed; off = exclusive prefix of counts)
+// where pos is drawn with an atomic per destination (row order inside a destination is
+// free: every expert row is computed independently, and the combine sums a token's K
+// returns in k order, so results do not depend on it).
+__global__ __launch_bounds__(256) void a2a_assign_kernel(const int* __restrict__ topk_ids,
+                                                         int n_slots, int El,
+                                                         int* __restrict__ dest_cnt,
+                                                         int* __restrict__ slot_pos) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slots) return;
+  const int dest = topk_ids[s] / El;
+  slot_pos[s] = atomicAdd(&dest_cnt[dest], 1);
+}
+
+__global__ __launch_bounds__(256) void a2a_pack_kernel(const bf16* __restrict__ h, int ldh, int H,
+                                                       const int* __restrict__ topk_ids,
+                                                       const float* __restrict__ topk_w, int K,
+                                                       int El, int W, int C,
+                                                       const int* __restrict__ dest_cnt,
+                                                       const int* __restrict__ slot_pos,
+                                                       bf16* __restrict__ send_x,
+                                                       int* __restrict__ send_meta,
+                                                       int* __restrict__ send_map) {
+  const int s = blockIdx.x;
+  const int e = topk_ids[s];
+  const int dest = e / El;
+  int off = 0;
+  if (C > 0) {
+    off = dest * C;
+  } else {
+    for (int d = 0; d < dest; ++d) off += dest_cnt[d];
+  }
+  const int row = off + slot_pos[s];
+  const bf16x8* src = reinterpret_cast<const bf16x8*>(h + (size_t)(s / K) * ldh);
+  bf16x8* dst = reinterpret_cast<bf16x8*>(send_x + (size_t)row * H);
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) dst[c] = src[c];
+  if (threadIdx.x == 0) {
+    send_meta[2 * row] = e % El;
+    send_meta[2 * row + 1] = __float_as_int(topk_w[s]);
+    send_map[s] = row;
+  }
+}
+
+// received rows -> per-local-expert slot lists (rows whose expert id is < 0 are padding)
+__global__ __launch_bounds__(1024) void a2a_group_kernel(const int* __restrict__ meta, int n,
+                                                         int El, int* __restrict__ cnt,
+                                                         int* __restrict__ rows, int rows_stride) {
+  __shared__ int s_cnt[MAX_E];
+  for (int i = threadIdx.x; i < MAX_E; i += blockDim.x) s_cnt[i] = 0;
+  __syncthreads();
+  for (int r = threadIdx.x; r < n; r += blockDim.x) {
+    const int le = meta[2 * r];
+    if (le < 0 || le >= El) continue;
+    const int pos = atomicAdd(&s_cnt[le], 1);
+    rows[(size_t)le * rows_stride + pos] = r;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < El; i += blockDim.x) cnt[i] = s_cnt[i];
+}
+
+// h[token] += sum_k back[send_map[token * K + k]]  (fp32 sum in k order, one rounding)
+__global__ __launch_bounds__(256) void a2a_combine_kernel(const bf16* __restrict__ back, int H,
+                                                          const int* __restrict__ send_map, int K,
+                                                          bf16* __restrict__ h, int ldh) {
+  const int r = blockIdx.x;
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < K; ++k) {
+      const bf16x8 v = reinterpret_cast<const bf16x8*>(back + (size_t)send_map[r * K + k] * H)[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+    }
+    bf16x8* dst = reinterpret_cast<bf16x8*>(h + (size_t)r * ldh) + c;
+    const bf16x8 hv = *dst;
+    bf16x8 res;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) res[j] = f2bf((float)hv[j] + acc[j]);
+    *dst = res;
+  }
+}
+
 }  // namespace
+
+// Dispatch for the EP all-to-all.  dest_cnt [W] (zeroed by this call), slot_pos [R*K]
+// scratch; send_x [W*C | R*K, H], send_meta [same, 2] int (static mode: pre-filled with
+// -1 by this call so padding rows group nowhere), send_map [R*K].
+P2P_API int p2p_moe_a2a_dispatch(const void* h, int ldh, int R, int H, const int* topk_ids,
+                                 const float* topk_w, int K, int El, int W, int C, int* dest_cnt,
+                                 int* slot_pos, void* send_x, int* send_meta, int* send_map,
+                                 hipStream_t st) {
+  if (R <= 0 || H % 8 || K <= 0 || El <= 0 || W <= 0 || C < 0) return (int)hipErrorInvalidValue;
+  const int n = R * K;
+  hipError_t e = hipMemsetAsync(dest_cnt, 0, sizeof(int) * W, st);
+  if (e != hipSuccess) return (int)e;
+  if (C > 0) {
+    e = hipMemsetAsync(send_meta, 0xFF, sizeof(int) * 2 * (size_t)W * C, st);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(a2a_assign_kernel, dim3((n + 255) / 256), dim3(256), 0, st, topk_ids, n, El,
+                     dest_cnt, slot_pos);
+  hipLaunchKernelGGL(a2a_pack_kernel, dim3(n), dim3(256), 0, st, (const bf16*)h, ldh, H, topk_ids,
+                     topk_w, K, El, W, C, dest_cnt, slot_pos, (bf16*)send_x, send_meta, send_map);
+  return (int)hipGetLastError();
+}
+
+P2P_API int p2p_moe_a2a_group(const int* meta, int n, int El, int* cnt, int* rows, int rows_stride,
+                              hipStream_t st) {
+  if (n <= 0 || El <= 0 || El > MAX_E || rows_stride < n) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(a2a_group_kernel, dim3(1), dim3(1024), 0, st, meta, n, El, cnt, rows,
+                     rows_stride);
+  return (int)hipGetLastError();
+}
+
+P2P_API int p2p_moe_a2a_combine(const void* back, int H, const int* send_map, int R, int K,
+                                void* h, int ldh, hipStream_t st) {
+  if (R <= 0 || H % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(a2a_combine_kernel, dim3(R), dim3(256), 0, st, (const bf16*)back, H, send_map,
+                     K, (bf16*)h, ldh);
+  return (int)hipGetLastError();
+}
 
 P2P_API int p2p_moe_route(const float* logits, int ldl, int R, int E, int K, int e_lo, int e_local,
                           int* topk_ids, float* topk_w, int* cnt, int* rows, int rows_stride,

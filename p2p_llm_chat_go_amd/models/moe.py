@@ -14,9 +14,10 @@ Expert parallelism, two modes:
   sequences; each (token, expert) pair is dispatched to the expert's owner with
   one all-to-all, the owner runs its grouped GEMMs on everything it received,
   and a second all-to-all returns the weighted outputs (SURVEY §2C EP row,
-  BASELINE config 5 "expert all-to-all over xGMI").  Slots per destination are
-  a static capacity (rows x top_k), so ranks must step in lockstep with equal
-  row counts (bench / lockstep serving) and the path is hipGraph-capturable.
+  BASELINE config 5 "expert all-to-all over xGMI").  Dispatch, grouping and combine
+  are kernels; decode uses a static per-destination capacity (rows x top_k, no host
+  sync, hipGraph-capturable), prefill exchanges exact counts and moves only the
+  routed rows.  Ranks step in lockstep with equal row counts (bench / lockstep serving).
 """
 from __future__ import annotations
 
@@ -121,57 +122,108 @@ def moe_forward_tiled(model, lw, ws, R):
         model.comm.allreduce_add_(h, part)
 
 
+class _Grow:
+    """Grow-only device buffers of the EP all-to-all path, one flat allocation per name,
+    handed out as [rows, cols] views.  A grown buffer's predecessor is kept alive: a
+    decode graph captured earlier (another batch bucket) still addresses it."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+        self.retired = []
+
+    def get(self, name, rows, cols=None, dtype=torch.bfloat16):
+        need = max(rows, 1) * (cols or 1)
+        t = self.bufs.get(name)
+        if t is None or t.numel() < need or t.dtype != dtype:
+            if t is not None:
+                self.retired.append(t)
+            t = torch.empty(need, device=self.device, dtype=dtype)
+            self.bufs[name] = t
+        if cols is None:
+            return t[:rows]
+        return t[:rows * cols].view(rows, cols)
+
+
+# static per-destination capacity (graph-capturable, padded) while the padded send stays
+# below this many bytes; larger calls (prefill) exchange exact counts first
+A2A_STATIC_MAX_BYTES = int(os.environ.get("P2P_A2A_STATIC_MAX_BYTES", str(4 << 20)))
+
+
 def moe_forward_a2a(model, lw, ws, R):
-    """DP-attention + EP MoE layer for this rank's R rows (see module doc)."""
+    """DP-attention + EP MoE layer for this rank's R rows (see module doc).
+
+    Kernels (``moe.hip``): routing (``moe_route``), dispatch (``a2a_dispatch``: slot ->
+    owner rank, row packing), slot grouping on the owner (``a2a_group``), the grouped
+    expert GEMMs, and the combine (``a2a_combine``).  Two exchange forms:
+      * static capacity C = R*K rows per destination -- no host sync, hipGraph-capturable
+        (decode), W*C rows on the wire, mostly padding;
+      * exact counts (padded send above ``A2A_STATIC_MAX_BYTES``, not while capturing):
+        rows per destination go to the host, one tiny all-to-all of counts, then the
+        variable-split all-to-all moves only the R*K routed rows (prefill)."""
     cfg, w, comm = model.cfg, model.w, model.comm
     E, K, H = cfg.n_experts, cfg.top_k, cfg.hidden
     W = w.ep_size
     El = E // W
-    C = R * K  # static per-destination capacity
     dev = model.device
     h = ws.h[:R]
-    logits = torch.empty(R, 16, device=dev, dtype=torch.float32)
+    buf = getattr(ws, "a2a", None)
+    if buf is None:
+        buf = ws.a2a = _Grow(dev)
+    n_slots = R * K
+    # routing: logits (RMSNorm folded) -> top-k ids / renormalised weights
+    logits = buf.get("logits", R, 16, torch.float32)
     for r0 in range(0, R, CHUNK):
         rc = min(CHUNK, R - r0)
         ops.skinny_gemm(router_tiled(lw), h[r0:r0 + rc], ops.EPI_F32, norm=True,
                         out=logits[r0:r0 + rc], eps=cfg.eps)
-    p = torch.softmax(logits[:, :E], dim=-1)
-    tw, tid = p.topk(K, dim=-1)
-    tw = tw / tw.sum(-1, keepdim=True)
-    flat = tid.reshape(-1)                                     # [R*K] expert ids
-    dest = torch.div(flat, El, rounding_mode="floor")
-    onehot = torch.nn.functional.one_hot(dest, W)
-    pos = (onehot.cumsum(0) - 1).gather(1, dest[:, None]).squeeze(1)
-    slot = dest * C + pos                                      # unique send slot per pair
-    send_x = torch.zeros(W * C, H, device=dev, dtype=torch.bfloat16)
-    send_x.index_copy_(0, slot, h.repeat_interleave(K, dim=0))
-    meta = torch.full((W * C, 2), -1, device=dev, dtype=torch.int32)
-    meta[:, 1] = 0
-    meta.index_copy_(0, slot, torch.stack([(flat % El).to(torch.int32),
-                                           tw.reshape(-1).float().view(torch.int32)], 1))
-    recv_x = torch.empty_like(send_x)
-    recv_meta = torch.empty_like(meta)
-    comm.all_to_all_(recv_x, send_x)
-    comm.all_to_all_(recv_meta, meta)
-    lexp = recv_meta[:, 0]
-    row_w = recv_meta[:, 1].contiguous().view(torch.float32)
-    # per-local-expert slot lists (invalid slots sort last)
-    key = torch.where(lexp < 0, torch.full_like(lexp, El), lexp).long()
-    order = torch.argsort(key, stable=True).to(torch.int32)
-    counts = torch.bincount(key, minlength=El + 1)[:El]
-    offs = counts.cumsum(0) - counts
-    n = W * C
-    idx = (offs[:, None] + torch.arange(n, device=dev)[None]).clamp(max=n - 1)
-    rows = order[idx].contiguous()                             # [El, n]
+    topk_ids = buf.get("topk_ids", n_slots, None, torch.int32)
+    topk_w = buf.get("topk_w", n_slots, None, torch.float32)
+    dummy_rows = buf.get("route_rows", 1, R, torch.int32)
+    dummy_cnt = buf.get("route_cnt", 1, None, torch.int32)
+    moe_ops.moe_route(logits, E, K, 0, 0, topk_ids, topk_w, dummy_cnt, dummy_rows)
+    capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
+    exact = (not capturing) and W * n_slots * H * 2 > A2A_STATIC_MAX_BYTES
+    C = 0 if exact else n_slots
+    n_send = n_slots if exact else W * C
+    send_x = buf.get("send_x", n_send, H)
+    send_meta = buf.get("send_meta", n_send, 2, torch.int32)
+    send_map = buf.get("send_map", n_slots, None, torch.int32)
+    slot_pos = buf.get("slot_pos", n_slots, None, torch.int32)
+    dest_cnt = buf.get("dest_cnt", W, None, torch.int32)
+    moe_ops.a2a_dispatch(h, topk_ids, topk_w, K, El, W, C, send_x, send_meta, send_map, dest_cnt,
+                         slot_pos)
+    if exact:
+        in_splits = [int(x) for x in dest_cnt.cpu().tolist()]
+        recv_cnt = buf.get("recv_cnt", W, None, torch.int32)
+        comm.all_to_all_(recv_cnt, dest_cnt)
+        out_splits = [int(x) for x in recv_cnt.cpu().tolist()]
+        n = sum(out_splits)
+        recv_x = buf.get("recv_x", n, H)
+        recv_meta = buf.get("recv_meta", n, 2, torch.int32)
+        comm.all_to_all_v_(recv_x, send_x, out_splits, in_splits)
+        comm.all_to_all_v_(recv_meta, send_meta, out_splits, in_splits)
+    else:
+        n = n_send
+        recv_x = buf.get("recv_x", n, H)
+        recv_meta = buf.get("recv_meta", n, 2, torch.int32)
+        comm.all_to_all_(recv_x, send_x)
+        comm.all_to_all_(recv_meta, send_meta)
     Fs = lw.w13.shape[1] * 16 // 2
-    act = torch.empty(n, Fs, device=dev, dtype=torch.bfloat16)
-    o = torch.zeros(n, H, device=dev, dtype=torch.bfloat16)
-    # one grouped launch per projection over every received row (tiled kernel above 64)
-    cnt = counts.to(torch.int32)
-    moe_ops.grouped_gemm(lw.w13, cnt, rows, recv_x, 1, n, ops.EPI_SILU, act, norm=True,
-                         eps=cfg.eps)
-    moe_ops.grouped_gemm(lw.w2, cnt, rows, act, 1, n, ops.EPI_STORE, o, row_w=row_w)
-    back = torch.empty_like(o)
-    comm.all_to_all_(back, o)
-    contrib = back.index_select(0, slot).float().view(R, K, H).sum(1)
-    h.copy_((h.float() + contrib).to(h.dtype))
+    o = buf.get("o", max(n, 1), H)
+    if n > 0:
+        cnt = buf.get("cnt", El, None, torch.int32)
+        rows = buf.get("rows", El, n, torch.int32)
+        moe_ops.a2a_group(recv_meta, n, El, cnt, rows)
+        row_w = recv_meta[:, 1].contiguous().view(torch.float32)
+        act = buf.get("act", n, Fs)
+        # one grouped launch per projection over every received row (tiled kernel above 64)
+        moe_ops.grouped_gemm(lw.w13, cnt, rows, recv_x, 1, n, ops.EPI_SILU, act, norm=True,
+                             eps=cfg.eps)
+        moe_ops.grouped_gemm(lw.w2, cnt, rows, act, 1, n, ops.EPI_STORE, o[:n], row_w=row_w)
+    back = buf.get("back", n_send, H)
+    if exact:
+        comm.all_to_all_v_(back, o[:n], in_splits, out_splits)
+    else:
+        comm.all_to_all_(back, o[:n])
+    moe_ops.a2a_combine(back, send_map, R, K, h)

@@ -91,6 +91,11 @@ _SIGS = {
                       c_void_p, c_void_p, c_int, c_void_p],
     "p2p_moe_router_route": [c_void_p, c_int, c_int, c_int, c_void_p, c_float, c_int, c_int, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_moe_a2a_dispatch": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                             c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p],
+    "p2p_moe_a2a_group": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_moe_a2a_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
     "p2p_moe_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p],
 }

@@ -102,3 +102,66 @@ def moe_combine(o, topk_ids, R, K, e_lo, e_local, out, accumulate=True):
     else:
         out[:R] = s.to(out.dtype)
     return out
+
+
+# ------------------------------------------------------------ expert-parallel all-to-all
+def a2a_dispatch(h, topk_ids, topk_w, K, El, W, C, send_x, send_meta, send_map, dest_cnt,
+                 slot_pos):
+    """Pack every (token, k) slot's row of h for its expert's owner rank (dest = id // El).
+
+    C > 0: static capacity, dest d's rows at [d*C, d*C + count) (padding rows carry expert
+    id -1 in send_meta); C == 0: packed by destination.  Writes send_x [rows, H], send_meta
+    [rows, 2] int32 (local expert id, weight bits), send_map [R*K] (the send row of each
+    slot) and dest_cnt [W] (rows per destination)."""
+    R, H = h.shape
+    n = R * K
+    if h.device.type != "cuda":
+        ids = topk_ids[:n].long()
+        dest = ids // El
+        onehot = torch.nn.functional.one_hot(dest, W)
+        pos = (onehot.cumsum(0) - 1).gather(1, dest[:, None]).squeeze(1)
+        cnt = onehot.sum(0)
+        off = dest * C if C > 0 else (cnt.cumsum(0) - cnt)[dest]
+        row = off + pos
+        if C > 0:
+            send_meta[:W * C].fill_(-1)
+        send_x[row] = h.repeat_interleave(K, dim=0)
+        send_meta[row, 0] = (ids % El).to(torch.int32)
+        send_meta[row, 1] = topk_w[:n].float().view(torch.int32)
+        send_map[:n] = row.to(torch.int32)
+        dest_cnt[:W] = cnt.to(dest_cnt.dtype)
+        return
+    L = _lib.lib()
+    _lib.check(L.p2p_moe_a2a_dispatch(h.data_ptr(), h.stride(0), R, H, topk_ids.data_ptr(),
+                                      topk_w.data_ptr(), K, El, W, C, dest_cnt.data_ptr(),
+                                      slot_pos.data_ptr(), send_x.data_ptr(), send_meta.data_ptr(),
+                                      send_map.data_ptr(), _lib.stream_ptr(h.device)),
+               "moe_a2a_dispatch")
+
+
+def a2a_group(meta, n, El, cnt, rows):
+    """Received rows [n] -> per-local-expert slot lists cnt [El], rows [El, >= n]."""
+    if meta.device.type != "cuda":
+        le = meta[:n, 0].long()
+        cnt.zero_()
+        for r, e in enumerate(le.tolist()):
+            if 0 <= e < El:
+                rows[e, int(cnt[e])] = r
+                cnt[e] += 1
+        return
+    L = _lib.lib()
+    _lib.check(L.p2p_moe_a2a_group(meta.data_ptr(), n, El, cnt.data_ptr(), rows.data_ptr(),
+                                   rows.stride(0), _lib.stream_ptr(meta.device)), "moe_a2a_group")
+
+
+def a2a_combine(back, send_map, R, K, h):
+    """h[r] += sum_k back[send_map[r*K + k]] (fp32 sum in k order, one bf16 rounding)."""
+    H = h.shape[1]
+    if h.device.type != "cuda":
+        contrib = back.index_select(0, send_map[:R * K].long()).float().view(R, K, H).sum(1)
+        h[:R] = (h[:R].float() + contrib).to(h.dtype)
+        return h
+    L = _lib.lib()
+    _lib.check(L.p2p_moe_a2a_combine(back.data_ptr(), H, send_map.data_ptr(), R, K, h.data_ptr(),
+                                     h.stride(0), _lib.stream_ptr(h.device)), "moe_a2a_combine")
+    return h

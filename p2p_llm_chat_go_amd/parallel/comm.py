@@ -111,6 +111,20 @@ class TPComm:
         dist.all_to_all_single(a, b, group=self.group)
         return out
 
+    def all_to_all_v_(self, out: torch.Tensor, inp: torch.Tensor, out_splits: list,
+                      in_splits: list):
+        """Variable-split all-to-all along dim 0 (rows per peer given on the host)."""
+        a, b = out, inp
+        if out.dtype == torch.bfloat16:
+            a, b = out.view(torch.int32), inp.view(torch.int32)
+        if out.device.type == "cuda" and self.backend != "nccl":
+            ah = torch.empty_like(a, device="cpu")
+            dist.all_to_all_single(ah, b.cpu(), out_splits, in_splits, group=self.group)
+            a.copy_(ah)
+            return out
+        dist.all_to_all_single(a, b, out_splits, in_splits, group=self.group)
+        return out
+
     def check(self):
         """Raise if a one-shot collective timed out waiting for a peer."""
         if self.car is not None:

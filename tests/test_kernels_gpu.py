@@ -749,3 +749,54 @@ def test_engine_fp8_weights_decode_matches_dequantized_bf16():
     assert _rel(res[0], res[1]) < 2e-2
     assert len(e8.generate(prompts, max_new_tokens=8)[0].tokens) == 8
     assert e8.weights.nbytes() < ed.weights.nbytes()
+
+
+@pytest.mark.parametrize("R,K,E,W,static", [(1, 2, 8, 8, True), (37, 2, 8, 4, True),
+                                            (300, 2, 8, 8, False), (64, 1, 4, 2, False)])
+def test_moe_a2a_dispatch_group_combine(R, K, E, W, static):
+    """EP all-to-all glue kernels vs their CPU forms: row order inside a destination is
+    free on the GPU (atomics), so rows are compared through send_map / per-expert sets."""
+    from p2p_llm_chat_go_amd.ops import moe as M
+
+    torch.manual_seed(R * 7 + W)
+    H = 256
+    El = E // W
+    h = torch.randn(R, H).to(torch.bfloat16)
+    ids = torch.stack([torch.randperm(E)[:K] for _ in range(R)]).reshape(-1).to(torch.int32)
+    tw = torch.rand(R * K)
+    C = R * K if static else 0
+    n_send = W * C if static else R * K
+    res = {}
+    for dev in ("cpu", DEV):
+        sx = torch.zeros(n_send, H, dtype=torch.bfloat16, device=dev)
+        sm = torch.zeros(n_send, 2, dtype=torch.int32, device=dev)
+        smap = torch.zeros(R * K, dtype=torch.int32, device=dev)
+        dc = torch.zeros(W, dtype=torch.int32, device=dev)
+        sp = torch.zeros(R * K, dtype=torch.int32, device=dev)
+        M.a2a_dispatch(h.to(dev), ids.to(dev), tw.to(dev), K, El, W, C, sx, sm, smap, dc, sp)
+        cnt = torch.zeros(El, dtype=torch.int32, device=dev)
+        rows = torch.zeros(El, n_send, dtype=torch.int32, device=dev)
+        M.a2a_group(sm, n_send, El, cnt, rows)  # every destination's rows, as if received
+        back = (sx.float() * 0.5).to(torch.bfloat16)  # stand-in for the experts' outputs
+        hh = h.clone().to(dev)
+        M.a2a_combine(back, smap, R, K, hh)
+        res[dev] = [t.cpu() for t in (sx, sm, smap, dc, cnt, rows, hh)]
+    (sx0, sm0, map0, dc0, c0, rw0, h0), (sx1, sm1, map1, dc1, c1, rw1, h1) = res["cpu"], res[DEV]
+    assert torch.equal(dc0, dc1) and torch.equal(c0, c1)
+    for s in range(R * K):  # slot s: its row holds token s // K, its expert and weight
+        r0, r1 = int(map0[s]), int(map1[s])
+        assert torch.equal(sx0[r0], sx1[r1]) and torch.equal(sm0[r0], sm1[r1])
+        d = int(ids[s]) // El
+        lo, hi = (d * C, d * C + int(dc1[d])) if static else (
+            int(dc1[:d].sum()), int(dc1[:d + 1].sum()))
+        assert lo <= r1 < hi
+    if static:  # padding rows belong to no expert
+        used = set(int(x) for x in map1)
+        assert all(int(sm1[r, 0]) == -1 for r in range(n_send) if r not in used)
+    for e in range(El):
+        n = int(c1[e])
+        got = sorted(int(sm1[int(x), 0]) for x in rw1[e, :n])
+        assert got == [e] * n
+        assert sorted(sx1[int(x)].float().sum().item() for x in rw1[e, :n]) == sorted(
+            sx0[int(x)].float().sum().item() for x in rw0[e, :n])
+    assert torch.equal(h0, h1)

@@ -25,8 +25,10 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q, moe, a2a=False):
+def _worker(rank, world, port, q, moe, a2a=False, exact=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if exact:  # every EP exchange takes the exact-count form (variable-split all-to-all)
+        os.environ["P2P_A2A_STATIC_MAX_BYTES"] = "0"
     torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -81,11 +83,12 @@ def _sampled(eng, prompts, n=5):
     return out
 
 
-def _run(world, moe=False, a2a=False):
+def _run(world, moe=False, a2a=False, exact=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a, exact))
+          for r in range(world)]
     [p.start() for p in ps]
     res = [q.get(timeout=300) for _ in range(world)]
     [p.join(timeout=60) for p in ps]
@@ -105,8 +108,16 @@ def test_expert_parallel_matches_single(world):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_expert_parallel_all_to_all_dp_attention(world):
-    """EP with token dispatch/return by all-to-all (DP attention, distinct prompts per rank)."""
+    """EP with token dispatch/return by all-to-all (DP attention, distinct prompts per rank),
+    static per-destination capacity."""
     _run(world, moe=True, a2a=True)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_expert_parallel_all_to_all_exact_counts(world):
+    """The exact-count exchange (counts all-to-all, then variable splits: only routed rows
+    travel) gives the same tokens."""
+    _run(world, moe=True, a2a=True, exact=True)
 
 
 def test_u64_max_allreduce_ordering():
