@@ -167,7 +167,6 @@ class Engine:
         for b, p in enumerate(prompts):
             s0 = starts[b] if starts else 0
             rows += [(b, i, p[i]) for i in range(s0, len(p))]
-        bt_d = bt.to(dev, non_blocking=True)
         first = torch.zeros(B, dtype=torch.int32, device=dev)
         all_logits = None
         if return_logits:
@@ -186,16 +185,29 @@ class Engine:
                 if i == len(prompts[b]) - 1:
                     outs.append(j)
                     out_seq.append(b)
-            host = torch.stack([seq, pos, ids, slots, pos + 1])
-            dev_t = host.to(dev, non_blocking=True)
-            seq_d, pos_d, ids_d, slots_d, ctx_d = dev_t[0], dev_t[1], dev_t[2], dev_t[3], dev_t[4]
-            out_rows = torch.tensor(outs or [0], dtype=torch.int32).to(dev, non_blocking=True)
             greedy = all_logits is None and not sampled
-            tiles = tiles_h = qtile = None
+            tiles_h = qtile = None
             if self.flash_prefill_min and R >= self.flash_prefill_min:
                 qtile = ops.flash_tile(self.model.nq, self.model.nkv, R)
                 tiles_h = ops.prefill_tiles(seq.tolist(), pos.tolist(), qtile)
-                tiles = tiles_h.to(dev, non_blocking=True)
+            # every host-built input of the chunk (block tables, row metadata, output rows,
+            # flash tiles, result scatter) in ONE host->device copy: each separate copy of
+            # a pageable tensor is a synchronous staging round trip before the first kernel
+            parts = [bt.reshape(-1), seq, pos, ids, slots, pos + 1,
+                     torch.tensor(outs or [0], dtype=torch.int32),
+                     torch.tensor(out_seq or [0], dtype=torch.int32)]
+            if tiles_h is not None:
+                parts.append(tiles_h.reshape(-1))
+            dev_all = torch.cat(parts).to(dev, non_blocking=True)
+            o = bt.numel()
+            bt_d = dev_all[:o].view(bt.shape)
+            seq_d, pos_d, ids_d, slots_d, ctx_d = (dev_all[o + k * R:o + (k + 1) * R] for k in range(5))
+            o += 5 * R
+            n_o = max(1, len(outs))
+            out_rows = dev_all[o:o + n_o]
+            sel = dev_all[o + n_o:o + 2 * n_o].long()
+            o += 2 * n_o
+            tiles = None if tiles_h is None else dev_all[o:o + tiles_h.numel()].view(tiles_h.shape)
             res = self.model.forward(ws, ids_d, pos_d, slots_d, bt_d, seq_d, ctx_d, R,
                                      max_ctx, out_rows=out_rows, n_out=len(outs), greedy=greedy,
                                      tiles=tiles, tiles_host=tiles_h, qtile=qtile)
@@ -216,7 +228,6 @@ class Engine:
                     toks = sample_tp(self.model, res, params, spos)
             else:
                 toks = self.model.sample_greedy(ws, res)
-            sel = torch.tensor(out_seq, dtype=torch.long).to(dev, non_blocking=True)
             first.index_copy_(0, sel, toks)
             if all_logits is not None:
                 all_logits.index_copy_(0, sel, res)

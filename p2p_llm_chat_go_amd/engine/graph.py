@@ -29,11 +29,12 @@ class DecodeState:
         self.max_pages = max_pages
         self.max_steps = max_steps
         self.max_ctx = max_ctx
-        self.ids = torch.zeros(B, device=dev, dtype=i32)
-        self.pos = torch.zeros(B, device=dev, dtype=i32)
-        self.ctx = torch.ones(B, device=dev, dtype=i32)
-        self.slots = torch.zeros(B, device=dev, dtype=i32)
-        self.bt = torch.zeros(B, max_pages, device=dev, dtype=i32)
+        # ids | pos | ctx | slots | block tables: views of ONE device buffer, so `load`
+        # refreshes a batch's whole state with one host->device copy
+        self.meta = torch.zeros(B * (4 + max_pages), device=dev, dtype=i32)
+        self.ids, self.pos, self.ctx, self.slots = (self.meta[k * B:(k + 1) * B] for k in range(4))
+        self.bt = self.meta[4 * B:].view(B, max_pages)
+        self.ctx.fill_(1)
         self.row_bt = torch.arange(B, device=dev, dtype=i32)
         self.hist = torch.zeros(B, max_steps, device=dev, dtype=i32)
         self.step = torch.zeros(1, device=dev, dtype=i32)
@@ -60,21 +61,20 @@ class DecodeState:
     def load(self, ids, pos, block_tables):
         """ids/pos: int lists (n <= B); block_tables: list of page lists."""
         n = len(ids)
-        assert n <= self.B
-        self.reset_dummy()
-        bt = torch.zeros(self.B, self.max_pages, dtype=torch.int32)
+        B = self.B
+        assert n <= B
+        self.step.zero_()
+        self.ws.keys.zero_()
+        host = torch.zeros(B * (4 + self.max_pages), dtype=torch.int32)
+        bt = host[4 * B:].view(B, self.max_pages)
         for b, pages in enumerate(block_tables):
             bt[b, :len(pages)] = torch.tensor(pages, dtype=torch.int32)
-        p = torch.zeros(self.B, dtype=torch.int32)
+        p = host[B:2 * B]
         p[:n] = torch.tensor(pos, dtype=torch.int32)
-        i = torch.zeros(self.B, dtype=torch.int32)
-        i[:n] = torch.tensor(ids, dtype=torch.int32)
-        slots = bt.gather(1, (p // PAGE).long()[:, None])[:, 0] * PAGE + p % PAGE
-        self.bt.copy_(bt, non_blocking=True)
-        self.pos.copy_(p, non_blocking=True)
-        self.ctx.copy_(p + 1, non_blocking=True)
-        self.ids.copy_(i, non_blocking=True)
-        self.slots.copy_(slots, non_blocking=True)
+        host[:n] = torch.tensor(ids, dtype=torch.int32)
+        host[2 * B:3 * B] = p + 1
+        host[3 * B:4 * B] = bt.gather(1, (p // PAGE).long()[:, None])[:, 0] * PAGE + p % PAGE
+        self.meta.copy_(host, non_blocking=True)  # rows >= n: dummies (page 0, position 0)
 
     def body_logits(self):
         """Forward only (sampling mode): logits of every row in ws.logits."""
