@@ -263,35 +263,39 @@ __global__ __launch_bounds__(512) void flash_prefill2_kernel(
   const size_t page_sz = (size_t)Hkv * PAGE * HD;
   const int krow = kperm(r32);
 
-  bf16x8 kr[2], vr[2];
-  auto fetch = [&](int kt) {
+  // K/V of a page travel global -> registers -> LDS.  Two register sets, so a page's
+  // loads are issued two tiles before it is staged: a fetch has two tiles of MFMA work
+  // (~2 us at 8 waves) to land instead of one, which left the loop waiting on L2/HBM.
+  bf16x8 kA[2], vA[2], kB[2], vB[2];
+  auto fetch = [&](int kt, bf16x8 (&kr)[2], bf16x8 (&vr)[2]) {
     const size_t base = (size_t)btr[kt] * page_sz + head_off;
     const bf16x8* kp = reinterpret_cast<const bf16x8*>(kc + base);
     const bf16x8* vp = reinterpret_cast<const bf16x8*>(vc + base);
+  // K: chunk c = key (c >> 4), dims 8 (c & 15)..+7 (row-major image, b128 stores).
+  // V: chunk c = key (c & 63), dims 8 (c >> 6)..+7 -- the 64 lanes of a wave hold the 64
+  // keys of ONE 8-dim column block, so each of the eight transposed b16 stores writes 128
+  // contiguous bytes of one V^T row (bank-conflict free; with a lane per dim chunk instead
+  // they hit 2 banks, 8-16 way conflicts that cost more than the tile's MFMAs).
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      kr[i] = kp[tid + 512 * i];
-      vr[i] = vp[tid + 512 * i];
+      const int c = tid + 512 * i;
+      kr[i] = kp[c];
+      vr[i] = vp[(c & 63) * (HD / 8) + (c >> 6)];
     }
   };
-  auto stash = [&](int st) {
+  auto stash = [&](int st, const bf16x8 (&kr)[2], const bf16x8 (&vr)[2]) {
     bf16* Ks = lds + st * (KS_ELEMS + VS_ELEMS);
     bf16* Vt = Ks + KS_ELEMS;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int c = tid + 512 * i, key = c >> 4, d0 = (c & 15) * 8;
-      *reinterpret_cast<bf16x8*>(&Ks[key * KLD2 + d0]) = kr[i];
+      const int c = tid + 512 * i;
+      *reinterpret_cast<bf16x8*>(&Ks[(c >> 4) * KLD2 + (c & 15) * 8]) = kr[i];
+      const int key = c & 63, d0 = (c >> 6) * 8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) Vt[(d0 + j) * VLD2 + key] = vr[i][j];
     }
   };
-
-  fetch(0);
-  for (int kt = 0; kt < n_kt; ++kt) {
-    const int st = kt & 1;
-    stash(st);
-    __syncthreads();  // this stage is complete; every wave is past tile kt-1 (WAR on st^1)
-    if (kt + 1 < n_kt) fetch(kt + 1);
+  auto tile = [&](int kt, int st) {
     const bf16* Ks = lds + st * (KS_ELEMS + VS_ELEMS);
     const bf16* Vt = Ks + KS_ELEMS;
 
@@ -351,6 +355,20 @@ __global__ __launch_bounds__(512) void flash_prefill2_kernel(
           o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               *reinterpret_cast<const bf16x8*>(vp + 32 * kh + 16 * s2), pf[kh][s2], o[db], 0, 0, 0);
     }
+  };
+
+  fetch(0, kA, vA);
+  if (n_kt > 1) fetch(1, kB, vB);
+  for (int kt = 0; kt < n_kt; kt += 2) {
+    stash(0, kA, vA);
+    __syncthreads();  // stage 0 complete; every wave is past tile kt-1 (WAR on stage 1)
+    if (kt + 2 < n_kt) fetch(kt + 2, kA, vA);
+    tile(kt, 0);
+    if (kt + 1 >= n_kt) break;
+    stash(1, kB, vB);
+    __syncthreads();
+    if (kt + 3 < n_kt) fetch(kt + 3, kB, vB);
+    tile(kt + 1, 1);
   }
 
   l += __shfl_xor(l, 32, 64);
