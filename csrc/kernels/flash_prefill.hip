@@ -312,6 +312,12 @@ __global__ __launch_bounds__(512) void flash_prefill2_kernel(
             *reinterpret_cast<const bf16x8*>(kp + 16 * s), qf[s], sc[kh], 0, 0, 0);
     }
     // ---- online softmax for this lane's query row (keys of reg rr: 16(rr>>3)+8hh+(rr&7)) ----
+    // m is the running max of the RAW scores; p = exp2(s * c - m * c) is one FMA + exp.
+    // Deferred rescale (cdna_hip_programming.md T13): O and l are rescaled only when some
+    // row's max grew by more than RESCALE_THR (log2 units) -- wave-uniform decision, each
+    // lane with its own factor -- so most tiles skip the 64-register multiply; the
+    // unrescaled p stay <= 2^RESCALE_THR, exact in fp32 and safe in bf16.
+    constexpr float RESCALE_THR = 8.f;
     const int k0 = kt * PAGE;
     const bool diag = k0 + PAGE - 1 > T.pos0;  // some key of the tile may be in the future
     float mx = -INFINITY;
@@ -319,31 +325,35 @@ __global__ __launch_bounds__(512) void flash_prefill2_kernel(
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
-        float v = sc[kh][rr] * scale_log2;
+        float v = sc[kh][rr];
         if (diag) {
           const int key = k0 + 32 * kh + 16 * (rr >> 3) + 8 * hh + (rr & 7);
           v = key <= my_pos ? v : -INFINITY;
+          sc[kh][rr] = v;
         }
-        sc[kh][rr] = v;
         mx = fmaxf(mx, v);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
-    m = mn;
+    if (__any((mx - m) * scale_log2 > RESCALE_THR)) {
+      const float mn = fmaxf(m, mx);
+      const float alpha = exp2f((m - mn) * scale_log2);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    }
+    const float mc = m * scale_log2;
     float ps = 0.f;
     bf16x8 pf[2][2];
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
-        const float p = exp2f(sc[kh][rr] - mn);
+        const float p = exp2f(fmaf(sc[kh][rr], scale_log2, -mc));
         ps += p;
         pf[kh][rr >> 3][rr & 7] = f2bf(p);
       }
-    l = l * alpha + ps;
-#pragma unroll
-    for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    l += ps;
     // ---- O^T += V^T . P^T ----
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
