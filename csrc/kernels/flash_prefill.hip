@@ -319,20 +319,22 @@ __global__ __launch_bounds__(512) void flash_prefill2_kernel(
     // unrescaled p stay <= 2^RESCALE_THR, exact in fp32 and safe in bf16.
     constexpr float RESCALE_THR = 8.f;
     const int k0 = kt * PAGE;
-    const bool diag = k0 + PAGE - 1 > T.pos0;  // some key of the tile may be in the future
+    // some key of the tile may be in the future (workgroup-uniform: a real branch, so the
+    // mask's compares and selects run on diagonal tiles only)
+    if (__builtin_amdgcn_readfirstlane(k0 + PAGE - 1 > T.pos0)) {
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int key = k0 + 32 * kh + 16 * (rr >> 3) + 8 * hh + (rr & 7);
+          if (key > my_pos) sc[kh][rr] = -INFINITY;
+        }
+    }
     float mx = -INFINITY;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        float v = sc[kh][rr];
-        if (diag) {
-          const int key = k0 + 32 * kh + 16 * (rr >> 3) + 8 * hh + (rr & 7);
-          v = key <= my_pos ? v : -INFINITY;
-          sc[kh][rr] = v;
-        }
-        mx = fmaxf(mx, v);
-      }
+      for (int rr = 0; rr < 16; ++rr) mx = fmaxf(mx, sc[kh][rr]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     if (__any((mx - m) * scale_log2 > RESCALE_THR)) {
       const float mn = fmaxf(m, mx);
@@ -349,7 +351,8 @@ __global__ __launch_bounds__(512) void flash_prefill2_kernel(
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
-        const float p = exp2f(fmaf(sc[kh][rr], scale_log2, -mc));
+        // raw v_exp_f32 (arguments <= RESCALE_THR; underflow to 0 is what we want)
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[kh][rr], scale_log2, -mc));
         ps += p;
         pf[kh][rr >> 3][rr & 7] = f2bf(p);
       }
