@@ -75,12 +75,14 @@ __global__ __launch_bounds__(64 * G) void flash_prefill_kernel(
     const size_t base = (size_t)btr[k0 / PAGE] * page_sz + head_off + (size_t)(k0 % PAGE) * HD;
     const bf16x8* kp = reinterpret_cast<const bf16x8*>(kc + base);
     const bf16x8* vp = reinterpret_cast<const bf16x8*>(vc + base);
+    // V chunk c = key (c % KT), dims 8 (c / KT)..+7: 32 consecutive lanes hold the 32
+    // keys of one 8-dim block, so the transposed b16 stores below are bank-conflict free
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * NTH;
       if (c < CH) {
         kr[i] = kp[c];
-        vr[i] = vp[c];
+        vr[i] = vp[(c % KT) * (HD / 8) + c / KT];
       }
     }
   };
@@ -89,8 +91,8 @@ __global__ __launch_bounds__(64 * G) void flash_prefill_kernel(
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * NTH;
       if (c < CH) {
-        const int key = c >> 4, d0 = (c & 15) * 8;
-        *reinterpret_cast<bf16x8*>(&Ks[key * KLD + d0]) = kr[i];
+        *reinterpret_cast<bf16x8*>(&Ks[(c >> 4) * KLD + (c & 15) * 8]) = kr[i];
+        const int key = c % KT, d0 = (c / KT) * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) Vt[(d0 + j) * VLD + key] = vr[i][j];
       }
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(64 * G) void flash_prefill_kernel(
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m - mn <= 0; -inf -> 0
     m = mn;
     bf16x8 pf;
     float ps = 0.f;
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(64 * G) void flash_prefill_kernel(
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = exp2f(s[mt][j] - mn);
+        const float p = __builtin_amdgcn_exp2f(s[mt][j] - mn);
         ps += p;
         pf[4 * mt + j] = f2bf(p);
       }

@@ -127,7 +127,7 @@ FLASH_V2 = os.environ.get("P2P_FLASH_V2", "1") != "0"
 # v2 pays from about this many (query tile, kv head) workgroups; below it the 16-token
 # v1 tiles spread a short prompt over more CUs (profiles/r2_flash_prefill_v2.jsonl:
 # T=512 v1 27 us vs v2 40 us; T=2048 v2 138 us vs v1 236 us)
-FLASH_V2_MIN_BLOCKS = 64  # v2 wins from T=512 at 8 KV heads (profiles/r2_flash_prefill_v2_conflict_free.jsonl)
+FLASH_V2_MIN_BLOCKS = 128  # v1 wins up to T=512 at 8 KV heads, v2 from ~1K (profiles/r2_flash_prefill_v2_conflict_free.jsonl)
 
 
 def flash_tile(n_heads: int, n_kv: int, rows: int | None = None) -> int:
