@@ -32,6 +32,10 @@ CHUNK = 64
 # rows above which a layer routes all rows at once onto the tiled grouped kernel
 # (P2P_MOE_TILED_MIN=100000 keeps the 64-row skinny chunks, for A/B measurements)
 TILED_MIN = int(os.environ.get("P2P_MOE_TILED_MIN", str(CHUNK + 1)))
+# rows up to which the fused single-block router+route kernel is used (decode batches);
+# above, per-row logits workgroups + moe_route (the single block serialised a 43-row
+# prompt chunk: 69 us per layer)
+ROUTER_FUSED_MAX = 8
 
 
 class MoeWorkspace:
@@ -76,9 +80,14 @@ def moe_forward(model, lw, ws, R):
     for r0 in range(0, R, CHUNK):
         rc = min(CHUNK, R - r0)
         h = ws.h[r0:r0 + rc]
-        # router GEMM + softmax/top-k + per-expert slot lists in one kernel
-        moe_ops.moe_router_route(h, lw.router, cfg.n_experts, K, e_lo, e_local, m.topk_ids,
-                                 m.topk_w, m.cnt, m.rows, eps=cfg.eps)
+        if rc <= ROUTER_FUSED_MAX:
+            # router GEMM + softmax/top-k + per-expert slot lists in one (single-block) kernel
+            moe_ops.moe_router_route(h, lw.router, cfg.n_experts, K, e_lo, e_local, m.topk_ids,
+                                     m.topk_w, m.cnt, m.rows, eps=cfg.eps)
+        else:  # prefill chunks: logits one workgroup per row, then the routing kernel
+            moe_ops.moe_router_logits(h, lw.router, cfg.n_experts, m.logits, eps=cfg.eps)
+            moe_ops.moe_route(m.logits[:rc], cfg.n_experts, K, e_lo, e_local, m.topk_ids,
+                              m.topk_w, m.cnt, m.rows)
         moe_ops.grouped_gemm(lw.w13, m.cnt, m.rows, h, K, rc, ops.EPI_SILU, m.act, norm=True,
                              eps=cfg.eps)
         moe_ops.grouped_gemm(lw.w2, m.cnt, m.rows, m.act, 1, rc, ops.EPI_STORE, m.o,

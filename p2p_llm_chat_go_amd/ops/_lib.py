@@ -96,6 +96,8 @@ _SIGS = {
                              c_void_p],
     "p2p_moe_a2a_group": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "p2p_moe_a2a_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
+    "p2p_moe_router_logits": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_float, c_void_p,
+                              c_int, c_void_p],
     "p2p_moe_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p],
 }

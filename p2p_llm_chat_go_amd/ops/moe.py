@@ -55,6 +55,20 @@ def moe_router_route(h, wr, E, K, e_lo, e_local, topk_ids, topk_w, cnt, rows, ep
     return topk_ids, topk_w
 
 
+def moe_router_logits(h, wr, E, logits, eps=1e-5):
+    """logits[:R, :E] = rstd(h) * h @ wr^T (gain folded into wr), one workgroup per row."""
+    R, H = h.shape
+    if h.device.type != "cuda":
+        hf = h.float()
+        logits[:R, :E] = (hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps)) @ wr.float().t()
+        return logits
+    L = _lib.lib()
+    _lib.check(L.p2p_moe_router_logits(h.data_ptr(), h.stride(0), R, H, wr.data_ptr(), E, float(eps),
+                                       logits.data_ptr(), logits.stride(0),
+                                       _lib.stream_ptr(h.device)), "moe_router_logits")
+    return logits
+
+
 def grouped_gemm(wt, cnt, rows, x, x_div, max_rows, epi, out, norm=False, row_w=None, eps=1e-5):
     """Per local expert e: out[slot] = epi(x[slot // x_div] @ W_e^T) for its routed slots.
 

@@ -800,3 +800,19 @@ def test_moe_a2a_dispatch_group_combine(R, K, E, W, static):
         assert sorted(sx1[int(x)].float().sum().item() for x in rw1[e, :n]) == sorted(
             sx0[int(x)].float().sum().item() for x in rw0[e, :n])
     assert torch.equal(h0, h1)
+
+
+@pytest.mark.parametrize("R,E", [(9, 8), (43, 8), (64, 4), (100, 16)])
+def test_moe_router_logits(R, E):
+    """Per-row router logits (prefill chunks) against the fp32 reference."""
+    from p2p_llm_chat_go_amd.ops import moe as M
+
+    torch.manual_seed(R + E)
+    H = 4096
+    h = torch.randn(R, H).to(torch.bfloat16)
+    wr = (torch.randn(E, H) * 0.02).to(torch.bfloat16)
+    ref = torch.zeros(R, 16)
+    M.moe_router_logits(h, wr, E, ref)
+    got = torch.zeros(R, 16, device=DEV)
+    M.moe_router_logits(h.to(DEV), wr.to(DEV), E, got)
+    assert _rel(got.cpu()[:, :E], ref[:, :E]) < 1e-3
