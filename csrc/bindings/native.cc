@@ -4,7 +4,10 @@
 #include <pybind11/functional.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#include <arpa/inet.h>
 #include <sys/socket.h>
+#include <sys/time.h>
+#include <unistd.h>
 
 #include <thread>
 
@@ -374,6 +377,96 @@ PYBIND11_MODULE(_native, m) {
     return py::make_tuple(accepted, refused, reopened, stats);
   }, py::arg("transport") = "tcp", py::arg("peer_streams") = 4, py::arg("proto_streams") = 2048,
      py::arg("attempts") = 8);
+  m.def("quic_version_negotiation", []() {
+    // (server) a long-header first flight of an unknown version gets a Version Negotiation
+    // packet: version 0, connection ids swapped, versions listing 1; a short datagram none.
+    // (client) a VN that does not list v1 fails the dial at once with the server's list;
+    // one that lists v1 is ignored (the dial runs into its timeout instead).
+    // Returns (vn_ok, short_ignored, client_error, ignored_error).
+    PrivateKey kb = PrivateKey::generate(KeyType::Ed25519), ka = PrivateKey::generate(KeyType::Ed25519);
+    bool vn_ok = false, short_ignored = false;
+    std::string cli_err, ign_err;
+    {
+      py::gil_scoped_release nogil;
+      auto srv = QuicTransport::create("127.0.0.1", 0, kb);
+      srv->set_accept([](QuicConnPtr c) { c->start([](StreamPtr) {}); });
+      const int fd = ::socket(AF_INET, SOCK_DGRAM, 0);
+      timeval tv{1, 0};
+      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+      sockaddr_in to{};
+      to.sin_family = AF_INET;
+      to.sin_port = htons((uint16_t)srv->port());
+      inet_pton(AF_INET, "127.0.0.1", &to.sin_addr);
+      auto probe = [&](size_t len) {
+        Bytes pkt(len, 0);
+        pkt[0] = 0xc0;
+        const uint8_t ver[4] = {0x0a, 0x0a, 0x0a, 0x0a};  // a reserved version
+        memcpy(&pkt[1], ver, 4);
+        pkt[5] = 8;
+        for (int i = 0; i < 8; ++i) pkt[6 + i] = (uint8_t)(0xd0 + i);  // DCID
+        pkt[14] = 8;
+        for (int i = 0; i < 8; ++i) pkt[15 + i] = (uint8_t)(0x50 + i);  // SCID
+        ::sendto(fd, pkt.data(), pkt.size(), 0, (const sockaddr*)&to, sizeof(to));
+        uint8_t buf[1500];
+        const ssize_t r = ::recv(fd, buf, sizeof(buf), 0);
+        return Bytes(buf, buf + (r > 0 ? r : 0));
+      };
+      const Bytes shortr = probe(200);
+      short_ignored = shortr.empty();
+      const Bytes v = probe(1200);
+      if (v.size() >= 7 + 8 + 1 + 8 + 4 && (v[0] & 0x80) && v[1] == 0 && v[2] == 0 && v[3] == 0 &&
+          v[4] == 0 && v[5] == 8 && v[6] == 0x50 && v[14] == 8 && v[15] == 0xd0) {
+        for (size_t q = 23; q + 4 <= v.size(); q += 4)
+          vn_ok |= v[q] == 0 && v[q + 1] == 0 && v[q + 2] == 0 && v[q + 3] == 1;
+      }
+      ::close(fd);
+      srv->close();
+      // client side: a fake server answering the first Initial with a VN
+      auto fake = [&](bool list_v1, int timeout_ms) {
+        const int sfd = ::socket(AF_INET, SOCK_DGRAM, 0);
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+        ::bind(sfd, (const sockaddr*)&a, sizeof(a));
+        socklen_t al = sizeof(a);
+        getsockname(sfd, (sockaddr*)&a, &al);
+        setsockopt(sfd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+        std::thread t([&, sfd] {
+          uint8_t buf[1600];
+          sockaddr_in from{};
+          socklen_t fl = sizeof(from);
+          const ssize_t r = ::recvfrom(sfd, buf, sizeof(buf), 0, (sockaddr*)&from, &fl);
+          if (r < 7) return;
+          const size_t dl = buf[5], sl = buf[6 + dl];
+          Bytes vn{0x80, 0, 0, 0, 0, (uint8_t)sl};
+          vn.insert(vn.end(), buf + 7 + dl, buf + 7 + dl + sl);
+          vn.push_back((uint8_t)dl);
+          vn.insert(vn.end(), buf + 6, buf + 6 + dl);
+          const uint8_t other[4] = {0xff, 0x00, 0x00, 0x1d};
+          vn.insert(vn.end(), other, other + 4);
+          if (list_v1) {
+            const uint8_t v1[4] = {0, 0, 0, 1};
+            vn.insert(vn.end(), v1, v1 + 4);
+          }
+          ::sendto(sfd, vn.data(), vn.size(), 0, (const sockaddr*)&from, fl);
+        });
+        auto cli = QuicTransport::create("127.0.0.1", 0, ka);
+        std::string err;
+        try {
+          cli->dial("127.0.0.1", ntohs(a.sin_port), PeerId(), timeout_ms);
+        } catch (const std::exception& e) {
+          err = e.what();
+        }
+        t.join();
+        cli->close();
+        ::close(sfd);
+        return err;
+      };
+      cli_err = fake(false, 5000);
+      ign_err = fake(true, 600);
+    }
+    return py::make_tuple(vn_ok, short_ignored, cli_err, ign_err);
+  });
   m.def("quic_protocol_violation", [](const std::string& kind) {
     // a client sends a frame past the server's advertised limits; returns the client's
     // view of the close (the server must answer with the RFC 9000 error code)

@@ -706,6 +706,27 @@ void QuicConn::on_datagram(const uint8_t* d, size_t n) {
         if (p + sl > n) break;
         const Bytes scid(d + p, d + p + sl);
         p += sl;
+        if (ver == 0) {
+          // Version Negotiation (RFC 9000 §6.2): only before the handshake made progress;
+          // one that lists the version we sent is discarded, otherwise the attempt fails
+          if (client_ && !established_ && sp_[HANDSHAKE].recvd.empty()) {
+            bool has_v1 = false;
+            std::string list;
+            for (size_t q = p; q + 4 <= n; q += 4) {
+              const uint32_t v = ((uint32_t)d[q] << 24) | ((uint32_t)d[q + 1] << 16) |
+                                 ((uint32_t)d[q + 2] << 8) | d[q + 3];
+              has_v1 |= v == 1;
+              char buf[16];
+              snprintf(buf, sizeof(buf), "%s0x%08x", list.empty() ? "" : ",", v);
+              list += buf;
+            }
+            if (!has_v1) {  // abandon silently (no CONNECTION_CLOSE: RFC 9000 §6.2)
+              error_ = "quic: version negotiation: server supports only " + list;
+              close_locked(0, false, ev, false);
+            }
+          }
+          break;
+        }
         if (ver != 1) break;
         const int type = (b0 >> 4) & 3;
         if (type == 0) {
@@ -1543,16 +1564,50 @@ QuicConnPtr QuicTransport::dial(const std::string& host, int port, const PeerId&
   return c;
 }
 
+// RFC 9000 §6 / §17.2.1: a long-header packet of a version this endpoint does not speak,
+// in a datagram large enough to be a client's first flight, is answered with a Version
+// Negotiation packet (version 0) listing the supported versions, with the connection ids
+// echoed back swapped.  (Never in response to a Version Negotiation packet.)
+void QuicTransport::send_version_negotiation(const uint8_t* d, size_t n, const sockaddr_in& to) {
+  if (n < 7) return;
+  const size_t dl = d[5];
+  if (6 + dl + 1 > n || dl > 20) return;
+  const size_t sl = d[6 + dl];
+  if (7 + dl + sl > n || sl > 20) return;
+  Bytes vn;
+  vn.push_back((uint8_t)(0x80 | (rand_cid()[0] & 0x7f)));
+  for (int i = 0; i < 4; ++i) vn.push_back(0);                  // version 0 = VN
+  vn.push_back((uint8_t)sl);
+  vn.insert(vn.end(), d + 7 + dl, d + 7 + dl + sl);             // DCID = client's SCID
+  vn.push_back((uint8_t)dl);
+  vn.insert(vn.end(), d + 6, d + 6 + dl);                       // SCID = client's DCID
+  const uint32_t versions[2] = {0x00000001u, 0x1a2a3a4au};      // v1 + a reserved (greasing) one
+  for (uint32_t v : versions)
+    for (int i = 3; i >= 0; --i) vn.push_back((uint8_t)(v >> (8 * i)));
+  ::sendto(fd_, vn.data(), vn.size(), 0, (const sockaddr*)&to, sizeof(to));
+  vn_sent_++;
+}
+
 void QuicTransport::dispatch(const uint8_t* d, size_t n, const sockaddr_in& from) {
   if (n < 1 + QuicConn::kCidLen) return;
   Bytes dcid;
   bool initial = false;
   if (d[0] & 0x80) {
     if (n < 6) return;
+    const uint32_t ver = ((uint32_t)d[1] << 24) | ((uint32_t)d[2] << 16) | ((uint32_t)d[3] << 8) | d[4];
     const size_t dl = d[5];
     if (6 + dl > n || dl > 20) return;
     dcid.assign(d + 6, d + 6 + dl);
-    initial = ((d[0] >> 4) & 3) == 0;
+    if (ver != 1 && ver != 0) {  // unknown version: no connection may have it
+      bool listening;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        listening = (bool)accept_;
+      }
+      if (listening && n >= kMaxDatagram) send_version_negotiation(d, n, from);
+      return;
+    }
+    initial = ver == 1 && ((d[0] >> 4) & 3) == 0;
   } else {
     dcid.assign(d + 1, d + 1 + QuicConn::kCidLen);
   }

@@ -288,12 +288,14 @@ class QuicTransport : public std::enable_shared_from_this<QuicTransport> {
   void close();
   // Test hook: drop this fraction of received datagrams (loss-recovery tests).
   void set_drop_rate(double r) { drop_rate_ = r; }
+  long version_negotiations_sent() const { return vn_sent_; }
 
  private:
   friend class QuicConn;
   QuicTransport(const PrivateKey& key) : key_(key) {}
   void loop();
   void dispatch(const uint8_t* d, size_t n, const sockaddr_in& from);
+  void send_version_negotiation(const uint8_t* d, size_t n, const sockaddr_in& to);
   void forget(const QuicConn* c);
   void register_cid(const Bytes& cid, const QuicConnPtr& c);
 
@@ -308,6 +310,7 @@ class QuicTransport : public std::enable_shared_from_this<QuicTransport> {
   std::atomic<bool> closed_{false};
   std::atomic<int> busy_{0};
   double drop_rate_ = 0;
+  std::atomic<long> vn_sent_{0};
 };
 
 }  // namespace p2p

@@ -192,3 +192,14 @@ def test_relay_reservation_voucher(N):
     signed by the relay's own key verifies."""
     good, wrong_peer, wrong_exp, foreign, tampered = N.relay_voucher_check()
     assert good and not wrong_peer and not wrong_exp and not foreign and not tampered
+
+
+def test_quic_version_negotiation(N):
+    """RFC 9000 §6: an unknown-version first flight gets a Version Negotiation packet
+    (version 0, ids swapped, v1 listed; nothing for a short datagram); a client that is
+    offered no common version fails at once with the server's list, and ignores a VN
+    listing the version it sent."""
+    vn_ok, short_ignored, cli_err, ign_err = N.quic_version_negotiation()
+    assert vn_ok and short_ignored
+    assert "version negotiation" in cli_err and "0xff00001d" in cli_err
+    assert "version negotiation" not in ign_err and "timeout" in ign_err
