@@ -56,6 +56,12 @@ class Workspace:
         self.moe = None  # lazily sized by models.moe
         # fused attention + o_proj hand-off counters (re-armed by the kernel) + fault flag
         self.sync = torch.zeros(2, device=dev, dtype=torch.int32)
+        # head-split attention + o_proj (ops.attn_oproj_heads): fp32 partial slab + tickets
+        self.heads_slab = self.heads_tickets = None
+        if dev.type == "cuda" and tp_size == 1 and cfg.hidden % ops.attention.HEADS_COLS == 0:
+            rows = min(max_rows, ops.attention.HEADS_MAX_ROWS)
+            self.heads_slab, self.heads_tickets = ops.attn_oproj_heads_workspace(
+                rows, nkv, cfg.hidden, dev)
         self.row_ids = torch.arange(max_rows, device=dev, dtype=torch.int32)  # identity row_bt
         self.err = torch.zeros(1, device=dev, dtype=torch.int32)
 
@@ -75,7 +81,16 @@ class LlamaModel:
         # decode: attention and o_proj in one launch (ops.attn_oproj).  Opt-in: measured on
         # MI355X it is 16.5 us vs 14.0 us for the two kernels at 8B / batch 1
         # (profiles/r1_fused_attn_oproj_vs_separate.jsonl), so the two-kernel path stays default.
-        self.fuse_attn_oproj = os.environ.get("P2P_FUSED_ATTN_OPROJ", "0") == "1"
+        # "heads": the head-split fused kernel (ops.attn_oproj_heads) -- every workgroup
+        # computes one kv head's attention while its o_proj slice streams in, no hand-off,
+        # the last head of each column block sums the partials -- for decode batches of
+        # <= P2P_HEADS_MAX_ROWS rows at contexts <= 256.  Also measured slower (16.9 vs
+        # 14.5 us at batch 1, profiles/r2_attn_oproj_heads_negative.jsonl: the 8-way fan-in
+        # tail ~4 us); "1": the hand-off kernel above; "0" (default): two kernels.
+        mode = os.environ.get("P2P_FUSED_ATTN_OPROJ", "0")
+        self.fuse_attn_oproj = mode == "1"
+        self.fuse_heads = mode == "heads"
+        self.heads_max_rows = int(os.environ.get("P2P_HEADS_MAX_ROWS", "4"))
         # TP prefill: row-parallel GEMMs of >= this many rows overlap their all-reduce
         # (chunked, separate communication stream); decode-size sums use the one-shot AR
         self.overlap_min_rows = int(os.environ.get("P2P_TP_OVERLAP_MIN_ROWS", "256"))
@@ -154,11 +169,19 @@ class LlamaModel:
         fused = (self.fuse_attn_oproj and tiles is None and self.tp == 1
                  and self.device.type == "cuda" and isinstance(self.w.layers[0].o, torch.Tensor)
                  and ops.attn_oproj_ok(R, self.nq, self.nkv, max_ctx, cfg.hidden))
+        heads = (not fused and self.fuse_heads and tiles is None and ws.heads_slab is not None
+                 and R <= self.heads_max_rows and isinstance(self.w.layers[0].o, torch.Tensor)
+                 and ops.attn_oproj_heads_ok(R, self.nq, self.nkv, max_ctx, cfg.hidden))
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)
             ops.qkv_rope_gemm(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc,
                               vc, eps=cfg.eps)
-            if fused:
+            if heads:
+                ops.attn_oproj_heads(q, kc, vc, block_tables,
+                                     row_bt[:R] if row_bt is not None else None, ctx_lens[:R],
+                                     self.nq, self.nkv, max_ctx, lw.o, h, ws.heads_slab,
+                                     ws.heads_tickets)
+            elif fused:
                 rb = row_bt[:R] if row_bt is not None else ws.row_ids[:R]
                 ops.attn_oproj(q, kc, vc, block_tables, rb, ctx_lens[:R], self.nq,
                                self.nkv, max_ctx, lw.o, h, attn, ws.sync, ws.err)

@@ -9,7 +9,8 @@ from .gemm import (EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, Fp8Weight, argmax_fi
                    quantize_fp8,
                    lm_head_argmax, new_argmax_keys, qkv_rope_gemm, rope_row_perm, skinny_gemm, tile_weight,
                    tiled_shape, tiled_split_fault, tiled_split_parallel, untile_weight)
-from .attention import (PAGE, HEAD_DIM, attn_oproj, attn_oproj_ok, attn_workspace,
+from .attention import (PAGE, HEAD_DIM, attn_oproj, attn_oproj_ok, attn_oproj_heads,
+                        attn_oproj_heads_ok, attn_oproj_heads_workspace, attn_workspace,
                         flash_prefill, flash_tile, paged_attention, prefill_tiles, rope_cache)
 from .elementwise import advance, argmax, gather_rows, l3_prefetch
 from .sampling import sample, sample_candidates, topk_candidates
@@ -19,7 +20,8 @@ __all__ = [
     "EPI_F32", "EPI_RESID", "EPI_SILU", "EPI_STORE", "fold_norm", "skinny_gemm", "tile_weight",
     "tiled_shape", "untile_weight", "argmax_finalize", "lm_head_argmax", "new_argmax_keys", "qkv_rope_gemm",
     "rope_row_perm", "PAGE", "HEAD_DIM", "attn_workspace", "paged_attention", "flash_prefill", "flash_tile", "prefill_tiles",
-    "attn_oproj", "attn_oproj_ok", "tiled_split_fault", "tiled_split_parallel", "l3_prefetch",
+    "attn_oproj", "attn_oproj_ok", "attn_oproj_heads", "attn_oproj_heads_ok",
+    "attn_oproj_heads_workspace", "tiled_split_fault", "tiled_split_parallel", "l3_prefetch",
     "rope_cache", "sample", "sample_candidates", "topk_candidates", "advance", "argmax", "gather_rows", "kernels_available", "kernel_lib",
     "kernel_lib_path",
 ]

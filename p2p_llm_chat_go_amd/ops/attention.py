@@ -119,6 +119,54 @@ def attn_oproj(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_k
     return h
 
 
+HEADS_MAX_ROWS = 16  # kernel limit (one MFMA M-tile); the engine's default is lower
+HEADS_COLS = 128     # output columns per workgroup
+
+
+def attn_oproj_heads_ok(R: int, n_heads: int, n_kv: int, max_ctx: int, N: int) -> bool:
+    """Shapes the head-split fused attention + o_proj kernel handles."""
+    return (R <= HEADS_MAX_ROWS and max_ctx <= FUSED_MAX_CTX and n_heads % n_kv == 0
+            and n_heads // n_kv in (1, 2, 4) and N % HEADS_COLS == 0)
+
+
+def attn_oproj_heads_workspace(R: int, n_kv: int, N: int, device) -> tuple:
+    """(fp32 partial slab [n_kv * R * N], u32 tickets [N / 128] zeroed once)."""
+    slab = torch.zeros(n_kv * R * N, device=device, dtype=torch.float32)
+    tickets = torch.zeros(N // HEADS_COLS, device=device, dtype=torch.int32)
+    return slab, tickets
+
+
+def attn_oproj_heads(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_kv, max_ctx,
+                     wo, h, slab, tickets, attn=None, scale=None):
+    """h += attention(q) @ Wo^T in ONE launch without a cross-workgroup hand-off
+    (decode, R <= 16 rows, ctx <= 256): workgroup (column block, kv head) streams its
+    o_proj slice while it computes that head's attention, stores a partial o_proj, and
+    the last head of each column block sums the partials + residual
+    (csrc/kernels/attn_oproj_heads.hip).  row_bt None = identity; attn (optional):
+    [R, n_heads*128] copy of the attention output."""
+    from .gemm import EPI_RESID, skinny_gemm, tiled_shape
+
+    R = q.shape[0]
+    if scale is None:
+        scale = 1.0 / math.sqrt(HEAD_DIM)
+    N, K = tiled_shape(wo)
+    if q.device.type != "cuda":
+        a = attn if attn is not None else torch.empty(R, n_heads * HEAD_DIM, dtype=q.dtype)
+        paged_attention(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_kv,
+                        max_ctx, out=a, scale=scale)
+        return skinny_gemm(wo, a, EPI_RESID, out=h)
+    if slab.numel() < n_kv * R * N or tickets.numel() < N // HEADS_COLS:
+        raise ValueError("attn_oproj_heads: workspace too small")
+    L = _lib.lib()
+    _lib.check(L.p2p_attn_oproj_heads(
+        q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+        block_tables.stride(0), _lib.ptr(row_bt), ctx_lens.data_ptr(), R, n_heads, n_kv, HEAD_DIM,
+        float(scale), int(max_ctx), wo.data_ptr(), N, h.data_ptr(), h.stride(0), slab.data_ptr(),
+        tickets.data_ptr(), _lib.ptr(attn), attn.stride(0) if attn is not None else 0,
+        _lib.stream_ptr(q.device)), "attn_oproj_heads")
+    return h
+
+
 QTILE = 16
 # v2 flash prefill (256 query rows per workgroup, 32x32x16 MFMA); P2P_FLASH_V2=0 selects v1
 FLASH_V2 = os.environ.get("P2P_FLASH_V2", "1") != "0"

@@ -248,6 +248,63 @@ def test_attn_oproj_fused(R, Hkv, G, ctxs):
         assert _rel(h.cpu(), ref) < 1e-2, i
 
 
+@pytest.mark.parametrize("R,Hkv,G,ctxs", [(1, 8, 4, [100]), (1, 8, 4, [1]), (1, 8, 4, [256]),
+                                          (3, 2, 2, [1, 17, 256]), (2, 4, 1, [64, 65]),
+                                          (16, 1, 4, list(range(5, 245, 15)))])
+def test_attn_oproj_heads(R, Hkv, G, ctxs):
+    """Head-split fused decode attention + o_proj (no hand-off; the last kv head of each
+    column block sums the partials) == paged_attention followed by the o_proj+residual
+    GEMM; back-to-back launches and graph replays exercise the ticket re-arming, and
+    repeated runs must be bit-identical (the partials are summed in head order)."""
+    torch.manual_seed(R * 100 + Hkv * 10 + G + 7)
+    Hq = Hkv * G
+    K = Hq * 128
+    N = 256 if K < 4096 else 4096
+    npg = 4
+    P = 1 + R * npg
+    k, v = _make_cache(P, Hkv, seed=R + G + 3)
+    bt = (torch.randperm(P - 1)[:R * npg] + 1).view(R, npg).to(torch.int32)
+    q = torch.randn(R, Hq * 128).to(torch.bfloat16)
+    ctx = torch.tensor(ctxs, dtype=torch.int32)
+    row_bt = torch.arange(R, dtype=torch.int32)
+    Wo = (torch.randn(N, K) * 0.02).to(torch.bfloat16)
+    h0 = torch.randn(R, N).to(torch.bfloat16)
+    a_ref = A.paged_attention_ref(q, k, v, bt, row_bt, ctx, Hq, Hkv, 1 / math.sqrt(128),
+                                  torch.empty(R, Hq * 128, dtype=torch.float32))
+    ref = h0.float() + a_ref.to(torch.bfloat16).float() @ Wo.float().t()
+    assert ops.attn_oproj_heads_ok(R, Hq, Hkv, 256, N)
+    d = {n: t.to(DEV) for n, t in dict(q=q, k=k, v=v, bt=bt, ctx=ctx, rb=row_bt).items()}
+    wt = ops.tile_weight(Wo).to(DEV)
+    attn = torch.zeros(R, Hq * 128, dtype=torch.bfloat16, device=DEV)
+    slab, tickets = ops.attn_oproj_heads_workspace(R, Hkv, N, DEV)
+    outs = []
+    for i in range(3):
+        h = h0.to(DEV)
+        ops.attn_oproj_heads(d["q"], d["k"], d["v"], d["bt"], d["rb"] if i else None, d["ctx"],
+                             Hq, Hkv, 256, wt, h, slab, tickets, attn=attn)
+        torch.cuda.synchronize()
+        assert tickets.abs().sum().item() == 0
+        assert _rel(attn.cpu(), a_ref) < 1e-2
+        assert _rel(h.cpu(), ref) < 1e-2
+        outs.append(h.cpu())
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    h = h0.to(DEV)
+    hs = h.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            ops.attn_oproj_heads(d["q"], d["k"], d["v"], d["bt"], d["rb"], d["ctx"], Hq, Hkv,
+                                 256, wt, h, slab, tickets)
+    torch.cuda.synchronize()
+    for i in range(4):
+        h.copy_(hs)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(h.cpu(), outs[0]), i
+
+
 # ------------------------------------------------------- flash prefill (MFMA)
 @pytest.mark.parametrize("v2", [True, False])
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
