@@ -226,6 +226,12 @@ std::tuple<bool, uint64_t, long, uint64_t, uint64_t> quic_echo(const std::string
 
 }  // namespace
 
+static p2p::Bytes hexb(const std::string& h) {
+  p2p::Bytes b;
+  for (size_t i = 0; i + 1 < h.size(); i += 2) b.push_back((uint8_t)std::stoi(h.substr(i, 2), nullptr, 16));
+  return b;
+}
+
 PYBIND11_MODULE(_native, m) {
   m.doc() = "native chat plane (libp2p subset, HTTP, directory, relay) + engine runtime";
   py::register_exception<NetError>(m, "NetError");
@@ -466,6 +472,118 @@ PYBIND11_MODULE(_native, m) {
       ign_err = fake(true, 600);
     }
     return py::make_tuple(vn_ok, short_ignored, cli_err, ign_err);
+  });
+  m.def("quic_retry", []() {
+    // (a) the RFC 9001 Appendix A.4 Retry integrity tag;
+    // (b) a server requiring address validation answers the first Initial with a Retry and
+    //     completes the handshake with the client echoing the token (both ends check the
+    //     original/retry connection-id transport parameters);
+    // (c) an Initial with a forged token is dropped;
+    // (d) against a fake server: a Retry with a bad tag is ignored, a valid one makes the
+    //     client resend its first flight to the Retry's SCID carrying the token.
+    // Returns (vector_ok, handshake_ok, retries_sent, forged_rejected, bad_tag_ignored,
+    //          resend_ok).
+    const Bytes odcid = hexb("8394c8f03e515708");
+    const Bytes rp = hexb("ff000000010008f067a5502a4262b5746f6b656e");
+    const bool vector_ok = quic_retry_tag(odcid, rp.data(), rp.size()) ==
+                           hexb("04a265ba2eff4d829058fb3f0f2496ba");
+    bool handshake_ok = false, bad_tag_ignored = false, resend_ok = false;
+    long retries = 0, rejected = 0;
+    {
+      py::gil_scoped_release nogil;
+      PrivateKey kb = PrivateKey::generate(KeyType::Ed25519), ka = PrivateKey::generate(KeyType::Ed25519);
+      auto srv = QuicTransport::create("127.0.0.1", 0, kb);
+      srv->set_require_retry(true);
+      srv->set_accept([](QuicConnPtr c) { c->start([](StreamPtr) {}); });
+      auto cli = QuicTransport::create("127.0.0.1", 0, ka);
+      try {
+        auto c = cli->dial("127.0.0.1", srv->port(), PeerId::from_public_key(kb.public_key()), 5000);
+        handshake_ok = c->established();
+        c->close();
+      } catch (const std::exception&) {
+      }
+      retries = srv->retries_sent();
+      // (c) forged token
+      const int fd = ::socket(AF_INET, SOCK_DGRAM, 0);
+      sockaddr_in to{};
+      to.sin_family = AF_INET;
+      to.sin_port = htons((uint16_t)srv->port());
+      inet_pton(AF_INET, "127.0.0.1", &to.sin_addr);
+      Bytes pkt(1200, 0);
+      pkt[0] = 0xc3;
+      pkt[4] = 1;
+      pkt[5] = 8;
+      for (int i = 0; i < 8; ++i) pkt[6 + i] = (uint8_t)(0xa0 + i);
+      pkt[14] = 8;
+      for (int i = 0; i < 8; ++i) pkt[15 + i] = (uint8_t)(0xb0 + i);
+      pkt[23] = 41;  // token length (1-byte varint), bytes of garbage follow
+      for (int i = 0; i < 41; ++i) pkt[24 + i] = (uint8_t)(i * 7);
+      ::sendto(fd, pkt.data(), pkt.size(), 0, (const sockaddr*)&to, sizeof(to));
+      ::close(fd);
+      for (int i = 0; i < 100 && srv->tokens_rejected() == 0; ++i)
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      rejected = srv->tokens_rejected();
+      cli->close();
+      srv->close();
+      // (d) fake server
+      auto fake = [&](bool good_tag) {
+        const int sfd = ::socket(AF_INET, SOCK_DGRAM, 0);
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+        ::bind(sfd, (const sockaddr*)&a, sizeof(a));
+        socklen_t al = sizeof(a);
+        getsockname(sfd, (sockaddr*)&a, &al);
+        timeval tv{1, 0};
+        setsockopt(sfd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+        const Bytes rscid = hexb("5a5a5a5a5a5a5a5a"), token = hexb("746f6b656e2d31");
+        bool resent = false, second = false;
+        std::thread t([&, sfd] {
+          uint8_t buf[1600];
+          sockaddr_in from{};
+          socklen_t fl = sizeof(from);
+          const ssize_t r = ::recvfrom(sfd, buf, sizeof(buf), 0, (sockaddr*)&from, &fl);
+          if (r < 7) return;
+          const size_t dl = buf[5], sl = buf[6 + dl];
+          const Bytes cdcid(buf + 6, buf + 6 + dl);
+          Bytes rt{0xf0, 0, 0, 0, 1, (uint8_t)sl};
+          rt.insert(rt.end(), buf + 7 + dl, buf + 7 + dl + sl);
+          rt.push_back((uint8_t)rscid.size());
+          rt.insert(rt.end(), rscid.begin(), rscid.end());
+          rt.insert(rt.end(), token.begin(), token.end());
+          Bytes tag = quic_retry_tag(cdcid, rt.data(), rt.size());
+          if (!good_tag) tag[3] ^= 1;
+          rt.insert(rt.end(), tag.begin(), tag.end());
+          ::sendto(sfd, rt.data(), rt.size(), 0, (const sockaddr*)&from, fl);
+          // the next Initial: (good tag) DCID = rscid + our token; (bad tag) unchanged
+          for (int k = 0; k < 4; ++k) {
+            const ssize_t r2 = ::recvfrom(sfd, buf, sizeof(buf), 0, (sockaddr*)&from, &fl);
+            if (r2 < 7) break;
+            const size_t dl2 = buf[5];
+            const Bytes d2(buf + 6, buf + 6 + dl2);
+            const size_t sl2 = buf[6 + dl2];
+            size_t q = 7 + dl2 + sl2;
+            const size_t tl = buf[q++];  // tokens here are < 64 bytes: 1-byte varint
+            const Bytes tk(buf + q, buf + q + tl);
+            second = true;
+            resent = good_tag ? (d2 == rscid && tk == token) : (d2 == cdcid && tk.empty());
+            break;
+          }
+        });
+        auto cl = QuicTransport::create("127.0.0.1", 0, ka);
+        try {
+          cl->dial("127.0.0.1", ntohs(a.sin_port), PeerId(), 1500);
+        } catch (const std::exception&) {
+        }
+        t.join();
+        cl->close();
+        ::close(sfd);
+        return second && resent;
+      };
+      bad_tag_ignored = fake(false);
+      resend_ok = fake(true);
+    }
+    return py::make_tuple(vector_ok, handshake_ok, retries, rejected, bad_tag_ignored, resend_ok);
   });
   m.def("quic_protocol_violation", [](const std::string& kind) {
     // a client sends a frame past the server's advertised limits; returns the client's

@@ -189,6 +189,20 @@ Bytes from_hex(const std::string& h) {
   return b;
 }
 
+// RFC 9001 §5.8: AES-128-GCM with a fixed key and nonce, empty plaintext, the Retry
+// pseudo-packet (ODCID length + ODCID + the Retry packet up to its tag) as AAD
+Bytes retry_tag(const Bytes& odcid, const uint8_t* retry, size_t len) {
+  static const uint8_t kKey[16] = {0xbe, 0x0c, 0x69, 0x0b, 0x9f, 0x66, 0x57, 0x5a,
+                                   0x1d, 0x76, 0x6b, 0x54, 0xe3, 0x68, 0xc8, 0x4e};
+  static const uint8_t kNonce[12] = {0x46, 0x15, 0x99, 0xd3, 0x5d, 0x63,
+                                     0x2b, 0xf2, 0x23, 0x98, 0x25, 0xbb};
+  Bytes pseudo;
+  pseudo.push_back((uint8_t)odcid.size());
+  pseudo.insert(pseudo.end(), odcid.begin(), odcid.end());
+  pseudo.insert(pseudo.end(), retry, retry + len);
+  return aead_seal(kKey, kNonce, 0, pseudo.data(), pseudo.size(), nullptr, 0);
+}
+
 Bytes rand_cid() {
   Bytes b(QuicConn::kCidLen);
   random_bytes(b.data(), b.size());
@@ -400,6 +414,7 @@ Bytes QuicConn::transport_params() const {
   param(0x09, 0);                            // initial_max_streams_uni
   param_bytes(0x0c, Bytes());                // disable_active_migration
   param_bytes(0x0f, scid_);                  // initial_source_connection_id
+  if (!client_ && !retry_scid_.empty()) param_bytes(0x10, retry_scid_);  // retry_source_cid
   return b;
 }
 
@@ -413,6 +428,10 @@ void QuicConn::parse_transport_params(const uint8_t* p, size_t n) {
     auto num = [&] { return get_varint(v, len, &q); };
     switch (id) {
       case 0x00: peer_odcid_.assign(v, v + len); break;
+      case 0x10:
+        peer_has_retry_scid_ = true;
+        peer_retry_scid_.assign(v, v + len);
+        break;
       case 0x01: peer_idle_ms_ = num(); break;
       case 0x04: peer_max_data_ = num(); break;
       case 0x05: peer_sd_local_ = num(); break;
@@ -436,13 +455,15 @@ void QuicConn::tls_keylog(const char* line) {
   else if (label == "SERVER_TRAFFIC_SECRET_0") sec_[1][1] = secret;
 }
 
-void QuicConn::begin(const Bytes& dcid, const Bytes& scid, const Bytes& odcid) {
+void QuicConn::begin(const Bytes& dcid, const Bytes& scid, const Bytes& odcid,
+                     const Bytes& key_cid, const Bytes& retry_scid) {
   std::lock_guard<std::mutex> lk(mu_);
   dcid_ = dcid;
   scid_ = scid;
   odcid_ = odcid;
+  retry_scid_ = retry_scid;
   QuicKeys c, s;
-  quic_initial_keys(odcid, &c, &s);
+  quic_initial_keys(key_cid.empty() ? odcid : key_cid, &c, &s);
   sp_[INITIAL].tx = client_ ? c : s;
   sp_[INITIAL].rx = client_ ? s : c;
   ERR_clear_error();
@@ -653,6 +674,9 @@ void QuicConn::on_handshake_complete(Events& ev) {
   X509_free(pc);
   if (!peer_tp_) return fail("peer sent no transport parameters", 0x08, ev);
   if (client_ && peer_odcid_ != odcid_) return fail("original_destination_connection_id mismatch", 0x08, ev);
+  if (client_ && (retry_seen_ != peer_has_retry_scid_ ||
+                  (retry_seen_ && peer_retry_scid_ != retry_scid_)))
+    return fail("retry_source_connection_id mismatch", 0x08, ev);
   if (!client_) {
     sp_[APP].queued.push_back(Bytes{0x1e});  // HANDSHAKE_DONE
     confirmed_ = true;
@@ -729,6 +753,18 @@ void QuicConn::on_datagram(const uint8_t* d, size_t n) {
         }
         if (ver != 1) break;
         const int type = (b0 >> 4) & 3;
+        if (type == 3) {
+          // Retry (RFC 9000 §17.2.5): at most one, only before any server Initial, with a
+          // valid integrity tag (RFC 9001 §5.8) and a SCID that differs from the DCID we
+          // sent; anything else is discarded.  A Retry fills its datagram.
+          if (client_ && !retry_seen_ && !dcid_switched_ && sp_[INITIAL].recvd.empty() &&
+              n - p >= 16 && scid != dcid_) {
+            const Bytes tag = retry_tag(odcid_, d + off, n - 16 - off);
+            if (CRYPTO_memcmp(tag.data(), d + n - 16, 16) == 0)
+              on_retry(scid, Bytes(d + p, d + n - 16));
+          }
+          break;
+        }
         if (type == 0) {
           const uint64_t tl = get_varint(d, n, &p);
           p += tl;
@@ -753,6 +789,30 @@ void QuicConn::on_datagram(const uint8_t* d, size_t n) {
     flush();
   }
   run(ev);
+}
+
+// Client, mutex held: switch to the server's new connection id, re-derive the Initial
+// keys from it, and resend the first flight (CRYPTO frames) in new Initials carrying the
+// token; packet numbers continue, loss recovery restarts (RFC 9002 §6.3).
+void QuicConn::on_retry(const Bytes& scid, const Bytes& token) {
+  retry_seen_ = true;
+  retry_scid_ = scid;
+  retry_token_ = token;
+  dcid_ = scid;
+  QuicKeys c, s;
+  quic_initial_keys(scid, &c, &s);
+  Space& S = sp_[INITIAL];
+  S.tx = c;
+  S.rx = s;
+  S.undecryptable.clear();
+  std::deque<Bytes> again;
+  for (auto& kv : S.sent) {
+    for (auto& f : kv.second.frames) again.push_back(f);
+    bytes_in_flight_ -= std::min<uint64_t>(bytes_in_flight_, kv.second.bytes);
+  }
+  S.sent.clear();
+  for (auto it = again.rbegin(); it != again.rend(); ++it) S.queued.push_front(*it);
+  pto_count_ = 0;
 }
 
 void QuicConn::handle_packet(Bytes pkt, size_t pn_off, int space, bool long_hdr, Events& ev) {
@@ -1147,7 +1207,10 @@ void QuicConn::send_packet(int space, const Bytes& payload_in, bool elicit,
     hdr.insert(hdr.end(), dcid_.begin(), dcid_.end());
     hdr.push_back((uint8_t)scid_.size());
     hdr.insert(hdr.end(), scid_.begin(), scid_.end());
-    if (space == INITIAL) hdr.push_back(0);  // token length
+    if (space == INITIAL) {  // token (a client echoes the Retry's; empty otherwise)
+      put_varint(hdr, retry_token_.size());
+      hdr.insert(hdr.end(), retry_token_.begin(), retry_token_.end());
+    }
     if (space == INITIAL && elicit) {        // RFC 9000 §14.1: 1200-byte datagrams
       const size_t total = hdr.size() + 2 + 4 + payload.size() + 16;
       if (total < kMaxDatagram) payload.resize(payload.size() + (kMaxDatagram - total), 0);
@@ -1503,6 +1566,10 @@ std::shared_ptr<QuicTransport> QuicTransport::create(const std::string& host, in
   getsockname(t->fd_, (sockaddr*)&a, &al);
   t->port_ = ntohs(a.sin_port);
   t->host_ = host;
+  t->token_key_.resize(32);
+  random_bytes(t->token_key_.data(), t->token_key_.size());
+  const char* rr = getenv("P2P_QUIC_RETRY");
+  t->require_retry_ = rr && rr[0] == '1';
   auto self = t;
   t->th_ = std::thread([self] { self->loop(); });
   return t;
@@ -1588,6 +1655,67 @@ void QuicTransport::send_version_negotiation(const uint8_t* d, size_t n, const s
   vn_sent_++;
 }
 
+// Retry tokens: expiry (ms since epoch, 8 bytes BE) | odcid len | odcid | 16-byte MAC
+// (HMAC-SHA256 under the transport's random key over the client's address + the body).
+// The token is bound to the address and to the Retry SCID (= the DCID the client must
+// use next), and valid for 10 s.
+Bytes QuicTransport::token_mac(const sockaddr_in& peer, const uint8_t* body, size_t n) const {
+  Bytes m(body, body + n);
+  const uint8_t* ip = reinterpret_cast<const uint8_t*>(&peer.sin_addr);
+  m.insert(m.end(), ip, ip + 4);
+  m.push_back((uint8_t)(ntohs(peer.sin_port) >> 8));
+  m.push_back((uint8_t)ntohs(peer.sin_port));
+  Bytes h = hmac256(token_key_, m);
+  h.resize(16);
+  return h;
+}
+
+static uint64_t wall_ms() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+void QuicTransport::send_retry(const Bytes& odcid, const Bytes& client_scid, const sockaddr_in& to) {
+  const Bytes rscid = rand_cid();
+  Bytes body;
+  const uint64_t exp = wall_ms() + 10000;
+  for (int i = 7; i >= 0; --i) body.push_back((uint8_t)(exp >> (8 * i)));
+  body.push_back((uint8_t)odcid.size());
+  body.insert(body.end(), odcid.begin(), odcid.end());
+  Bytes bound = body;  // the MAC also covers the SCID the client will address
+  bound.insert(bound.end(), rscid.begin(), rscid.end());
+  const Bytes mac = token_mac(to, bound.data(), bound.size());
+  Bytes pkt;
+  pkt.push_back((uint8_t)(0xf0 | (rscid[0] & 0x0f)));  // long header, type 3 (Retry)
+  pkt.insert(pkt.end(), {0, 0, 0, 1});
+  pkt.push_back((uint8_t)client_scid.size());
+  pkt.insert(pkt.end(), client_scid.begin(), client_scid.end());
+  pkt.push_back((uint8_t)rscid.size());
+  pkt.insert(pkt.end(), rscid.begin(), rscid.end());
+  pkt.insert(pkt.end(), body.begin(), body.end());
+  pkt.insert(pkt.end(), mac.begin(), mac.end());
+  const Bytes tag = retry_tag(odcid, pkt.data(), pkt.size());
+  pkt.insert(pkt.end(), tag.begin(), tag.end());
+  ::sendto(fd_, pkt.data(), pkt.size(), 0, (const sockaddr*)&to, sizeof(to));
+  retries_sent_++;
+}
+
+bool QuicTransport::check_token(const Bytes& token, const Bytes& dcid, const sockaddr_in& from,
+                                Bytes* odcid) const {
+  if (token.size() < 8 + 1 + 16) return false;
+  const size_t ol = token[8];
+  if (ol > 20 || token.size() != 8 + 1 + ol + 16) return false;
+  Bytes bound(token.begin(), token.end() - 16);
+  bound.insert(bound.end(), dcid.begin(), dcid.end());
+  const Bytes mac = token_mac(from, bound.data(), bound.size());
+  if (CRYPTO_memcmp(mac.data(), token.data() + token.size() - 16, 16) != 0) return false;
+  uint64_t exp = 0;
+  for (int i = 0; i < 8; ++i) exp = (exp << 8) | token[i];
+  if (wall_ms() > exp) return false;
+  odcid->assign(token.begin() + 9, token.begin() + 9 + ol);
+  return true;
+}
+
 void QuicTransport::dispatch(const uint8_t* d, size_t n, const sockaddr_in& from) {
   if (n < 1 + QuicConn::kCidLen) return;
   Bytes dcid;
@@ -1626,14 +1754,30 @@ void QuicTransport::dispatch(const uint8_t* d, size_t n, const sockaddr_in& from
     if (!initial || !listening || n < kMaxDatagram || dcid.size() < 8) return;
     // fresh client Initial: new server-side connection
     const size_t sl = d[6 + dcid.size()];
-    if (7 + dcid.size() + sl > n) return;
+    if (7 + dcid.size() + sl > n || sl > 20) return;
     const Bytes peer_scid(d + 7 + dcid.size(), d + 7 + dcid.size() + sl);
+    size_t tp = 7 + dcid.size() + sl;
+    const uint64_t tl = get_varint(d, n, &tp);
+    if (tp > n || tl > n - tp) return;
+    const Bytes token(d + tp, d + tp + tl);
+    Bytes odcid = dcid, retry_scid;
+    if (require_retry_) {
+      if (token.empty()) {
+        send_retry(dcid, peer_scid, from);
+        return;
+      }
+      if (!check_token(token, dcid, from, &odcid)) {  // forged, expired or another path's
+        tokens_rejected_++;
+        return;
+      }
+      retry_scid = dcid;  // the client now addresses the Retry's SCID
+    }
     c = std::make_shared<QuicConn>(shared_from_this(), false, from, key_);
     const Bytes scid = rand_cid();
     register_cid(scid, c);
     register_cid(dcid, c);
     try {
-      c->begin(peer_scid, scid, dcid);
+      c->begin(peer_scid, scid, odcid, dcid, retry_scid);
     } catch (...) {
       forget(c.get());
       return;
@@ -1707,5 +1851,9 @@ void QuicTransport::close() {
 }
 
 void quic_put_varint(Bytes& b, uint64_t v) { put_varint(b, v); }
+
+Bytes quic_retry_tag(const Bytes& odcid, const uint8_t* retry, size_t len) {
+  return retry_tag(odcid, retry, len);
+}
 
 }  // namespace p2p

@@ -163,7 +163,11 @@ class QuicConn : public MuxSession, public std::enable_shared_from_this<QuicConn
   };
 
   // -- called by the transport thread / dialer
-  void begin(const Bytes& dcid, const Bytes& scid, const Bytes& odcid);
+  // key_cid: the client DCID the Initial keys derive from (after a Retry: the Retry's
+  // SCID; default odcid); retry_scid: server side, the SCID of the Retry it sent
+  void begin(const Bytes& dcid, const Bytes& scid, const Bytes& odcid,
+             const Bytes& key_cid = Bytes(), const Bytes& retry_scid = Bytes());
+  void on_retry(const Bytes& scid, const Bytes& token);
   void on_datagram(const uint8_t* d, size_t n);
   void tick(std::chrono::steady_clock::time_point now);
   bool wait_established(int timeout_ms);
@@ -200,6 +204,11 @@ class QuicConn : public MuxSession, public std::enable_shared_from_this<QuicConn
   const PrivateKey& key_;
   Bytes dcid_, scid_, odcid_;
   bool dcid_switched_ = false;
+  // Retry (RFC 9000 §8.1.2 / §17.2.5): client -- the token echoed in every later Initial
+  // and the Retry's SCID (checked against the server's retry_source_connection_id);
+  // server -- the SCID of the Retry it sent (its transport parameter 0x10)
+  bool retry_seen_ = false;
+  Bytes retry_token_, retry_scid_;
   mutable std::mutex mu_;
   std::condition_variable cv_;
   Space sp_[3];
@@ -216,6 +225,8 @@ class QuicConn : public MuxSession, public std::enable_shared_from_this<QuicConn
   // transport parameters
   bool peer_tp_ = false;
   Bytes peer_odcid_;
+  bool peer_has_retry_scid_ = false;
+  Bytes peer_retry_scid_;
   uint64_t peer_max_data_ = 0, peer_sd_local_ = 0, peer_sd_remote_ = 0, peer_max_bidi_ = 0;
   uint64_t peer_idle_ms_ = 0;
   // state
@@ -289,6 +300,11 @@ class QuicTransport : public std::enable_shared_from_this<QuicTransport> {
   // Test hook: drop this fraction of received datagrams (loss-recovery tests).
   void set_drop_rate(double r) { drop_rate_ = r; }
   long version_negotiations_sent() const { return vn_sent_; }
+  // Address validation (RFC 9000 §8.1.2): answer every token-less client Initial with a
+  // Retry and accept only Initials echoing a valid token (env P2P_QUIC_RETRY=1 at create).
+  void set_require_retry(bool on) { require_retry_ = on; }
+  long retries_sent() const { return retries_sent_; }
+  long tokens_rejected() const { return tokens_rejected_; }
 
  private:
   friend class QuicConn;
@@ -296,6 +312,10 @@ class QuicTransport : public std::enable_shared_from_this<QuicTransport> {
   void loop();
   void dispatch(const uint8_t* d, size_t n, const sockaddr_in& from);
   void send_version_negotiation(const uint8_t* d, size_t n, const sockaddr_in& to);
+  void send_retry(const Bytes& odcid, const Bytes& client_scid, const sockaddr_in& to);
+  bool check_token(const Bytes& token, const Bytes& dcid, const sockaddr_in& from,
+                   Bytes* odcid) const;
+  Bytes token_mac(const sockaddr_in& peer, const uint8_t* body, size_t n) const;
   void forget(const QuicConn* c);
   void register_cid(const Bytes& cid, const QuicConnPtr& c);
 
@@ -311,6 +331,12 @@ class QuicTransport : public std::enable_shared_from_this<QuicTransport> {
   std::atomic<int> busy_{0};
   double drop_rate_ = 0;
   std::atomic<long> vn_sent_{0};
+  std::atomic<bool> require_retry_{false};
+  Bytes token_key_;  // random per transport: Retry tokens are only valid at this server
+  std::atomic<long> retries_sent_{0}, tokens_rejected_{0};
 };
+// RFC 9001 §5.8 Retry integrity tag over the Retry pseudo-packet (odcid + the Retry
+// packet without its tag); exposed for the RFC 9001 Appendix A.4 vector test.
+Bytes quic_retry_tag(const Bytes& odcid, const uint8_t* retry, size_t len);
 
 }  // namespace p2p

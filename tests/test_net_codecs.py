@@ -203,3 +203,16 @@ def test_quic_version_negotiation(N):
     assert vn_ok and short_ignored
     assert "version negotiation" in cli_err and "0xff00001d" in cli_err
     assert "version negotiation" not in ign_err and "timeout" in ign_err
+
+
+def test_quic_retry(N):
+    """RFC 9000 §8.1.2 address validation: the RFC 9001 A.4 integrity-tag vector; a server
+    requiring Retry completes the handshake with a token-echoing client (one Retry sent,
+    retry_source_connection_id checked); a forged token is dropped; a client ignores a
+    Retry with a bad tag and answers a valid one by resending its first flight to the
+    Retry's SCID with the token."""
+    vector_ok, handshake_ok, retries, rejected, bad_tag_ignored, resend_ok = N.quic_retry()
+    assert vector_ok
+    assert handshake_ok and retries >= 1
+    assert rejected >= 1
+    assert bad_tag_ignored and resend_ok
