@@ -1,6 +1,6 @@
 """Mid-M (prompt-sized, 16 < M <= 64) projection GEMMs at llama3.1-8B shapes: every
 launch family the autotuner can pick (skinny MT=2/4 with NG 1/2, split-K tiled
-LDS-DMA), best time per family, over all 32 layers' weights (cold, graph-replayed).  Run on the GPU: python bench/midm_bench.py [M ...]"""
+LDS-DMA, whole-K midm LDS-DMA), best time per family, over all 32 layers' weights (cold, graph-replayed).  Run on the GPU: python bench/midm_bench.py [M ...]"""
 import json
 import os
 import sys
@@ -18,6 +18,8 @@ from p2p_llm_chat_go_amd.ops import gemm as G  # noqa: E402
 def family(code):
     if code & G.TILED_FLAG:
         return "tiled"
+    if code & G.MIDM_FLAG:
+        return "midm"
     return "skinny_ng2" if (code >> 16) & 0xff else "skinny"
 
 
@@ -49,7 +51,7 @@ def main():
         for name, wts, epi, fn in jobs:
             N, K = G.tiled_shape(wts[0])
             best = {}
-            for code in _configs(K, M, G.tiled_ok(N, K, epi)):
+            for code in _configs(K, M, G.tiled_ok(N, K, epi), midm=True):
                 t = _graph_time(lambda: [fn(wt, code) for wt in wts]) * 1000 / len(wts)
                 f = family(code)
                 if f not in best or t < best[f][0]:

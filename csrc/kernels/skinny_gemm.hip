@@ -33,6 +33,7 @@
 //               (ordered(value) << 32 | ~index) per row and block (ties -> lowest id).
 // Split-K across the waves of a block (WAVES), reduced through LDS.
 #include "gemm_epilogue.h"
+#include "midm_gemm.h"
 
 #include <type_traits>
 
@@ -410,6 +411,8 @@ int launch_e(int mt, int waves, const void* Wt, const void* X, int ldx, int M, i
 
 }  // namespace
 
+constexpr int MIDM_FLAG = 1 << 25;  // launch-code bit (ops.gemm.MIDM_FLAG)
+
 // Picks the split-K factor: enough waves to keep ~8+ MB of weight loads in flight,
 // but every wave resident in the first dispatch round (256 CUs x 4 SIMDs x
 // g_resident waves/SIMD) and streaming >= 8 k-steps.
@@ -439,6 +442,30 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
     if ((N % 32) != 0) return (int)hipErrorInvalidValue;
     groups = N / 32;
     up_off = groups;
+  }
+  // bit 25: the mid-M LDS-DMA kernel (midm_gemm.h; bf16 dense weights, K % 128 == 0)
+  if ((waves & MIDM_FLAG) && !ea.wscale && !ea.moe_cnt && K % 128 == 0) {
+    switch (epi) {
+      case EPI_STORE:
+        return norm ? midm::launch<EPI_STORE, true>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream)
+                    : midm::launch<EPI_STORE, false>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      case EPI_RESID:
+        if (norm) return (int)hipErrorInvalidValue;
+        return midm::launch<EPI_RESID, false>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      case EPI_SILU:
+        if (!norm) return (int)hipErrorInvalidValue;
+        return midm::launch<EPI_SILU, true>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      case EPI_F32:
+        return norm ? midm::launch<EPI_F32, true>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream)
+                    : midm::launch<EPI_F32, false>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      case EPI_QKV_ROPE:
+        if (!norm) return (int)hipErrorInvalidValue;
+        return midm::launch<EPI_QKV_ROPE, true>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+      case EPI_ARGMAX:
+        if (!norm) return (int)hipErrorInvalidValue;
+        return midm::launch<EPI_ARGMAX, true>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, stream);
+    }
+    return (int)hipErrorInvalidValue;
   }
   // waves: low 8 bits = split-K waves (0 = heuristic), bits 8..15 = pipeline depth U
   // (0 = default), bits 16..23 = column groups per block (M > 16 only; 0 = 1)

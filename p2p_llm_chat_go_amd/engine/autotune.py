@@ -40,10 +40,13 @@ def _graph_time(fn, reps=3):
     return best
 
 
-def _configs(K, M=1, tiled=False):
+def _configs(K, M=1, tiled=False, midm=False):
     """Launch codes: waves | U << 8 | NG << 16 (NG = column groups per block, M > 16);
-    G.TILED_FLAG = the split-K LDS-DMA tiled kernel (M > 16, tileable shapes)."""
+    G.TILED_FLAG = the split-K LDS-DMA tiled kernel (M > 16, tileable shapes);
+    G.MIDM_FLAG = the whole-K LDS-DMA kernel (M > 1, bf16 weights, K % 128 == 0)."""
     out = [G.TILED_FLAG] if (tiled and M > 16) else []
+    if midm and M > 1 and K % 128 == 0:
+        out.append(G.MIDM_FLAG)
     for ng in ((1,) if M <= 16 else (1, 2)):
         for u in ((4, 8) if M <= 16 else (2, 4)):
             for w in (1, 2, 4, 8):
@@ -55,6 +58,8 @@ def _configs(K, M=1, tiled=False):
 def describe(code: int) -> str:
     if code & G.TILED_FLAG:
         return "tiled"
+    if code & G.MIDM_FLAG:
+        return "midm"
     ng = (code >> 16) & 0xff
     return "w%d/U%d%s" % (code & 0xff, (code >> 8) & 0xff, "/NG%d" % ng if ng > 1 else "")
 
@@ -95,7 +100,8 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
         for name, wts, epi, fn in jobs:
             N, K = G.tiled_shape(wts[0])
             times = {}
-            for code in _configs(K, M, G.tiled_ok(N, K, epi) and not G._is_f8(wts[0])):
+            bf = not G._is_f8(wts[0])
+            for code in _configs(K, M, G.tiled_ok(N, K, epi) and bf, midm=bf):
                 times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
             best = min(times, key=times.get)
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)

@@ -131,7 +131,8 @@ class Engine:
     def warmup(self, batch_sizes=(1,), ctx=256, autotune=True):
         if autotune and not getattr(self, "tuning", None):
             # decode buckets + the prefill tile (prompt chunks run at M <= 64 rows per call)
-            self.autotune(tuple(bucket(b, BATCH_BUCKETS) for b in batch_sizes) + (64,))
+            # decode buckets + prompt chunks of 33-48 rows (chat-length prompts) and 49-64
+            self.autotune(tuple(bucket(b, BATCH_BUCKETS) for b in batch_sizes) + (48, 64))
         for b in batch_sizes:
             self.decode_graph(b, ctx)
 

@@ -97,7 +97,9 @@ def _wptr(wt):
 
 
 def m_tile(M: int) -> int:
-    return 1 if M <= 16 else (2 if M <= 32 else 4)
+    """Autotune bucket of M: 16-row MFMA tiles (1..4).  The skinny kernel runs 3 tiles as
+    4; the midm / tiled kernels use the exact count, so 33-48 rows tune separately."""
+    return min(4, (max(M, 1) + 15) // 16)
 
 
 def tune_key(wt, M, epi, norm):
@@ -132,6 +134,10 @@ def use_tiled(M, N, K, epi) -> bool:
 # launch-code bit: run this (shape, M tile) on the tiled LDS-DMA kernel (autotuned for
 # 16 < M <= 64, where the split-K tiled kernel can beat the skinny one)
 TILED_FLAG = 1 << 24
+# launch-code bit: the mid-M LDS-DMA kernel (csrc/kernels/midm_gemm.h: one column group
+# per workgroup over the whole K, activations + weights streamed through an LDS ring);
+# bf16 dense weights, K % 128 == 0, M <= 64 (autotuned against skinny / tiled)
+MIDM_FLAG = 1 << 25
 
 
 def _want_tiled(wt, M, N, K, epi, norm, waves) -> bool:

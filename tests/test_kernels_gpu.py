@@ -95,11 +95,24 @@ def _ng_code(w, u):
 @pytest.mark.parametrize("w,u", [(1, 2), (2, 4), (4, 2), (4, 4)])
 def test_skinny_two_groups_per_block(M, w, u):
     """NG=2 launch codes (two column groups share the A fragments) on every epilogue."""
+    _every_epilogue(M, _ng_code(w, u), M + 10 * w + u)
+
+
+@pytest.mark.parametrize("M", [2, 17, 44, 64])
+@pytest.mark.parametrize("K", [1024, 1536])
+def test_midm_gemm_every_epilogue(M, K):
+    """The mid-M LDS-DMA kernel (launch-code bit ops.gemm.MIDM_FLAG: one column group per
+    workgroup, whole K, 4-wave k-split) on every epilogue vs fp32 references."""
+    from p2p_llm_chat_go_amd.ops.gemm import MIDM_FLAG
+
+    _every_epilogue(M, MIDM_FLAG, 1000 + M, K=K)
+
+
+def _every_epilogue(M, code, seed, K=1024):
     from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
 
-    torch.manual_seed(M + 10 * w + u)
-    code = _ng_code(w, u)
-    K, N = 1024, 512
+    torch.manual_seed(seed)
+    N = 512
     W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
     x = torch.randn(M, K).to(torch.bfloat16)
     Wt = ops.tile_weight(W).to(DEV)
