@@ -244,10 +244,174 @@ __global__ __launch_bounds__(HD * CG) void attn_combine_kernel(const float* __re
   }
 }
 
+// ---- single-chunk decode attention on MFMA (contexts <= 256 keys: chat decode) ----
+// The 16-wave kernel above spends its time in a serial per-lane P.V loop over LDS and a
+// 16-way cross-wave merge; here 4 waves x 64 keys (= one KV page per wave, so one
+// block-table load per wave) run both products on v_mfma_f32_16x16x32_bf16 with the
+// query heads on the MFMA's N axis (G <= 16, padded with zero rows):
+//   S^T[key][head] = K . Q^T   (A = 16 keys x 32 dims straight from the page, 16 B per
+//                               lane; B = q fragments, loaded once)
+//   O[head][dim]  += P . V     (A = P: the S^T accumulator registers after the softmax ARE
+//                               the A fragment -- lane (head, key group) -- with the 32
+//                               keys of a k-step taken as two 16-key blocks; B = V^T
+//                               fragments read from the wave's V rows in LDS with the
+//                               same key permutation)
+// and the 4 wave partials merge once through LDS.
+constexpr int MW = 4;            // waves
+constexpr int MKPW = 64;         // keys per wave = one page
+constexpr int MVS = HD + 8;      // V row stride (bf16) in LDS: conflict-free 16-B writes
+
+template <int G>
+__global__ __launch_bounds__(MW * 64) void paged_attn_mfma_kernel(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const int* __restrict__ bt, int bt_stride, const int* __restrict__ row_bt,
+    const int* __restrict__ ctx_lens, int Hkv, float scale, bf16* __restrict__ out, int ldo) {
+  static_assert(G >= 1 && G <= 16, "query heads on the MFMA N axis");
+  __shared__ __attribute__((aligned(16))) bf16 vs[MW][MKPW][MVS];
+  __shared__ float so[MW][G][HD];
+  __shared__ float sm[MW][G], sl[MW][G];
+  const int h = blockIdx.x, r = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kk = lane & 15, qd = lane >> 4;
+  const int ctx = ctx_lens[r];
+  const int rb = row_bt ? row_bt[r] : r;
+  const int page = bt[(size_t)rb * bt_stride + min(w, bt_stride - 1)];  // wave-uniform
+  const size_t pbase = ((size_t)page * Hkv + h) * PAGE * HD;
+
+  // loads: K and V rows of this wave's 64 keys (block b = keys 16b.., lane row kk, dims
+  // 32s + 8qd..), q fragments of the G heads (rows kk >= G are zero)
+  bf16x8 kr[4][4], vr[4][4], qf[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const bf16x8* kp = reinterpret_cast<const bf16x8*>(kc + pbase + (size_t)(16 * b + kk) * HD + 8 * qd);
+    const bf16x8* vp = reinterpret_cast<const bf16x8*>(vc + pbase + (size_t)(16 * b + kk) * HD + 8 * qd);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) kr[b][s2] = kp[4 * s2];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) vr[b][s2] = vp[4 * s2];
+  }
+  {
+    const bf16x8* qp = reinterpret_cast<const bf16x8*>(q + (size_t)r * ldq +
+                                                       (size_t)(h * G + min(kk, G - 1)) * HD + 8 * qd);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) qf[s2] = kk < G ? qp[4 * s2] : zero_bf16x8();
+  }
+  const int n_valid = min(max(ctx - w * MKPW, 0), MKPW);  // wave-uniform
+
+  // V rows -> LDS (this wave's region only: a wave barrier orders them for its reads)
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+      *reinterpret_cast<bf16x8*>(&vs[w][16 * b + kk][32 * s2 + 8 * qd]) = vr[b][s2];
+
+  float mg = -INFINITY, lg = 0.f;  // per head kk (every lane of column kk agrees)
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int c = 0; c < HD / 16; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (n_valid > 0) {
+    // S^T blocks: lane holds keys 16b + 4qd + j (j < 4) of head kk
+    f32x4 st[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      st[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        st[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[b][s2], qf[s2], st[b], 0, 0, 0);
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = 16 * b + 4 * qd + j < n_valid;
+        st[b][j] = ok ? st[b][j] * scale : -INFINITY;
+        m = fmaxf(m, st[b][j]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = __expf(st[b][j] - m);  // -inf -> 0
+        st[b][j] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    mg = m;
+    lg = l;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's V rows are in LDS
+    __builtin_amdgcn_wave_barrier();
+    // P.V: k-step t covers key blocks 2t (A slots 0-3) and 2t+1 (slots 4-7)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 pa;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pa[j] = f2bf(st[2 * t][j]);
+        pa[4 + j] = f2bf(st[2 * t + 1][j]);
+      }
+#pragma unroll
+      for (int c = 0; c < HD / 16; ++c) {
+        bf16x8 vb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          vb[j] = vs[w][32 * t + 4 * qd + j][16 * c + kk];
+          vb[4 + j] = vs[w][32 * t + 16 + 4 * qd + j][16 * c + kk];
+        }
+        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[c], 0, 0, 0);
+      }
+    }
+  }
+  // O accumulators: lane holds O[head 4qd + j][dim 16c + kk]
+#pragma unroll
+  for (int c = 0; c < HD / 16; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int hd = 4 * qd + j;
+      if (hd < G) so[w][hd][16 * c + kk] = o[c][j];
+    }
+  if (qd == 0 && kk < G) {
+    sm[w][kk] = mg;
+    sl[w][kk] = lg;
+  }
+  __syncthreads();
+  for (int i = tid; i < G * HD; i += MW * 64) {
+    const int hd = i / HD, d = i % HD;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < MW; ++ww) M = fmaxf(M, sm[ww][hd]);
+    float num = 0.f, den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < MW; ++ww) {
+        const float e = __expf(sm[ww][hd] - M);
+        num = fmaf(e, so[ww][hd][d], num);
+        den = fmaf(e, sl[ww][hd], den);
+      }
+    }
+    out[(size_t)r * ldo + (size_t)(h * G + hd) * HD + d] = f2bf(den > 0.f ? num / den : 0.f);
+  }
+}
+
+// Opt-in (p2p_paged_attention_mfma(1)): measured on MI355X it is 7.7-7.9 us per launch
+// at 44-256 keys vs 6.3-8.1 us for the 16-wave kernel (profiles/r2_decode_attn_mfma.jsonl):
+// both are bound by the block-table -> K/V load chain, not by the arithmetic.
+static int g_attn_mfma = 0;
+
 template <int G>
 int launch_attn(const void* q, int ldq, const void* kc, const void* vc, const int* bt,
                 int bt_stride, const int* row_bt, const int* ctx, int R, int Hkv, float scale,
                 int n_chunks, void* out, int ldo, float* part_o, float* part_ml, hipStream_t st) {
+  if (n_chunks == 1 && g_attn_mfma) {
+    hipLaunchKernelGGL((paged_attn_mfma_kernel<G>), dim3(Hkv, R), dim3(MW * 64), 0, st,
+                       (const bf16*)q, ldq, (const bf16*)kc, (const bf16*)vc, bt, bt_stride, row_bt,
+                       ctx, Hkv, scale, (bf16*)out, ldo);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL((paged_attn_kernel<G>), dim3(n_chunks, Hkv, R), dim3(WAVES * 64), 0, st,
                      (const bf16*)q, ldq, (const bf16*)kc, (const bf16*)vc, bt, bt_stride, row_bt,
                      ctx, Hkv, scale, n_chunks, (bf16*)out, ldo, part_o, part_ml);
@@ -259,6 +423,9 @@ int launch_attn(const void* q, int ldq, const void* kc, const void* vc, const in
 }
 
 }  // namespace
+
+// 1: contexts <= 256 keys run the 4-wave MFMA kernel; 0 (default): the 16-wave kernel.
+P2P_API void p2p_paged_attention_mfma(int on) { g_attn_mfma = on; }
 
 // row_bt null = identity (decode batches: row r is sequence r), one dependent load less
 // on the kernel's critical path (row_bt -> page -> K/V becomes page -> K/V).

@@ -63,6 +63,7 @@ _SIGS = {
                              c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int,
                              c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "p2p_attn_oproj_heads_tune": [c_int],
+    "p2p_paged_attention_mfma": [c_int],
     "p2p_l3_prefetch": [c_void_p, ctypes.c_size_t, c_int, c_void_p, c_void_p],
     "p2p_gather_rows": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
     "p2p_rope_cache": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

@@ -167,8 +167,21 @@ def _make_cache(P, Hkv, seed=0):
 
 
 @pytest.mark.parametrize("G", [1, 4, 8])
-@pytest.mark.parametrize("ctxs", [[1], [63, 64, 65], [300, 7], [1000, 257, 1]])
-def test_paged_attention(G, ctxs):
+@pytest.mark.parametrize("ctxs", [[1], [63, 64, 65], [256, 200, 129, 17], [300, 7], [1000, 257, 1]])
+@pytest.mark.parametrize("mfma", [False, True])
+def test_paged_attention(G, ctxs, mfma):
+    """Contexts <= 256: the 16-wave kernel or (mfma) the 4-wave MFMA kernel; longer
+    contexts the split-K kernel + combine."""
+    from p2p_llm_chat_go_amd.ops import _lib
+
+    _lib.lib().p2p_paged_attention_mfma(int(mfma))
+    try:
+        _paged_attention_case(G, ctxs)
+    finally:
+        _lib.lib().p2p_paged_attention_mfma(0)
+
+
+def _paged_attention_case(G, ctxs):
     Hkv = 2
     Hq = Hkv * G
     B = len(ctxs)
