@@ -25,7 +25,9 @@ def main():
     variants = [("v2_auto", (2, 0, 0)), ("v2_256x256_phased", (2, 1, 1)),
                 ("v2_256x256_2stage", (2, 1, 1, 0)),
                 ("v2_128x256", (2, 2, 1)), ("v2_128x128", (2, 3, 1)),
-                ("v2_128x128_s2", (2, 3, 2)), ("v2_128x128_s4", (2, 3, 4))]
+                ("v2_128x128_s2", (2, 3, 2)), ("v2_128x128_s4", (2, 3, 4)),
+                ("v2_320x128", (2, 6, 1)), ("v2_320x128_s2", (2, 6, 2)), ("v2_192x128", (2, 7, 1)),
+                ("v2_192x128_s2", (2, 7, 2))]
     L = __import__("p2p_llm_chat_go_amd.ops._lib", fromlist=["lib"]).lib()
     for M in a.M:
         x = torch.randn(M, H, device="cuda").to(torch.bfloat16)

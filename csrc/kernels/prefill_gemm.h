@@ -798,14 +798,22 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
     case 3: return launch<128, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 4: return launch<64, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 5: return launch<64, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 6: return launch<320, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 7: return launch<192, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
   }
   return (int)hipErrorInvalidValue;
 }
 
 // Largest tile that still gives about one block per CU; N must divide.  M <= 64
 // uses the 64-row tiles (no MFMA work or DMA on padding rows beyond one tile).
+// 129-192 and 257-320 rows (batched chat prompts: 8 peers x ~36-44 tokens) take ONE
+// m-tile of 192 / 320 rows: at these M the tiles are bound by the per-CU LDS-DMA fill
+// rate, so the bytes staged per useful output decide, and 128-row tiles would stream
+// every weight column 2-3 times (25 % padding) while 256x256 pads up to 44 %.
 int pick_tile(int M, int N) {
   if (M <= 64) return N % 128 == 0 ? 4 : 0;
+  if (N % 128 == 0 && ((M > 128 && M <= 192) || (M > 256 && M <= 320)))
+    return M <= 192 ? 7 : 6;
   const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};
   int best = 0;
   for (auto& c : cand) {
@@ -831,7 +839,7 @@ static int prefill_dispatch(const void* Wt, const void* X, int ldx, int M, int K
   using namespace pgemm;
   if (M <= 0 || K % BK) return (int)hipErrorInvalidValue;
   int tile = g_prefill_tile ? g_prefill_tile : pick_tile(M, N);
-  const int bn = (tile == 3 || tile == 4) ? 128 : 256;
+  const int bn = (tile == 3 || tile == 4 || tile == 6 || tile == 7) ? 128 : 256;
   if (!tile || N % bn) return (int)hipErrorInvalidValue;
   const int up_off = (epi == EPI_SILU) ? N / 32 : 0;
   switch (epi) {

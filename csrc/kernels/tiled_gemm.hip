@@ -203,8 +203,8 @@ int launch_tiled(const void* Wt, const void* X, int ldx, int M, int K, int n_til
 // (SiLU: (N/2) % 64 == 0).  Returns hipErrorInvalidValue if the shape does not tile.
 static int g_tiled_version = 2;  // 2 = LDS-DMA 8-wave kernel (prefill_gemm.h), 1 = register-staged
 
-// Benchmarks / A-B tests: version 1|2, tile 0 (heuristic) or 1..5 (256x256, 128x256, 128x128,
-// 64x128, 64x256),
+// Benchmarks / A-B tests: version 1|2, tile 0 (heuristic) or 1..7 (256x256, 128x256, 128x128,
+// 64x128, 64x256, 320x128, 192x128),
 // splitk 0 (heuristic), 1 (off) or a forced K-slice count.
 // 256x256 prefill tiles: 1 = phased pipeline (default), 0 = the 2-stage kernel (A/B).
 P2P_API void p2p_prefill_phased(int on) { pgemm::g_phased = on ? 1 : 0; }
@@ -229,7 +229,7 @@ P2P_API int p2p_tiled_split_fault() {
 
 P2P_API void p2p_tiled_gemm_config(int version, int tile, int splitk) {
   if (version == 1 || version == 2) g_tiled_version = version;
-  g_prefill_tile = (tile >= 0 && tile <= 5) ? tile : 0;
+  g_prefill_tile = (tile >= 0 && tile <= 7) ? tile : 0;
   pgemm::g_splitk = splitk >= 0 ? splitk : 0;
 }
 

@@ -551,7 +551,8 @@ def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
 # (version, tile, splitk[, parallel split-K reduction]); split-K grids of at most one block
 # per CU with splitk | 8 take the parallel reduction unless the 4th field is 0
 TILED_CFGS = [(2, 0, 0), (2, 1, 1), (2, 2, 1), (2, 3, 1), (2, 3, 4), (2, 3, 4, 0), (2, 1, 3),
-              (2, 4, 1), (2, 4, 2), (2, 4, 4), (2, 4, 4, 0), (2, 4, 3), (2, 5, 2), (1, 0, 0)]
+              (2, 4, 1), (2, 4, 2), (2, 4, 4), (2, 4, 4, 0), (2, 4, 3), (2, 5, 2), (2, 6, 1),
+              (2, 6, 4), (2, 7, 1), (2, 7, 2), (1, 0, 0)]
 
 
 @pytest.fixture(params=TILED_CFGS, ids=lambda c: "v%d_t%d_s%d" % c[:3] + ("_serial" if len(c) > 3 else ""))
@@ -568,7 +569,7 @@ def tiled_cfg(request):
     assert ops.tiled_split_fault() == 0
 
 
-@pytest.mark.parametrize("M", [7, 65, 200, 513])
+@pytest.mark.parametrize("M", [7, 65, 150, 200, 300, 513])
 @pytest.mark.parametrize("epi", ["store", "store_norm", "resid", "silu", "f32"])
 def test_tiled_gemm(M, epi, tiled_cfg):
     torch.manual_seed(M)
