@@ -20,6 +20,12 @@ from kernel_bench import graph_time  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, nargs="*", default=[36, 64, 288, 512, 2048, 8192])
+    ap.add_argument("--deep", action="store_true",
+                    help="A/B the deep LDS pipeline: each variant with shallow stages (deep=0) "
+                         "and with the default rule (deep=1)")
+    ap.add_argument("--deep-modes", type=int, nargs="*", default=[0, 1])
+    ap.add_argument("--only", nargs="*", default=None, help="variant names to run")
+    ap.add_argument("--no-hipblaslt", action="store_true")
     a = ap.parse_args()
     H, F = LLAMA31_8B.hidden, LLAMA31_8B.ffn
     variants = [("v2_auto", (2, 0, 0)), ("v2_256x256_phased", (2, 1, 1)),
@@ -47,8 +53,16 @@ def main():
                       ("v2_64x128_s2", (2, 4, 2)), ("v2_64x128_s4", (2, 4, 4)),
                       ("v2_64x128_s8", (2, 4, 8)), ("v2_64x256", (2, 5, 1)),
                       ("v2_64x256_s2", (2, 5, 2)), ("v2_128x128_s4", (2, 3, 4))]
-            for vname, cfg in vs:
+            if a.deep:
+                vs = [(v + "_deep%d" % d, c, d) for v, c in vs if c is not None
+                      for d in a.deep_modes]
+            else:
+                vs = [(v, c, 1) for v, c in vs]
+            if a.only:
+                vs = [v for v in vs if v[0].rsplit("_deep", 1)[0] in a.only]
+            for vname, cfg, deep in vs:
                 set_tiled_min_m(65 if cfg is None else 1)
+                L.p2p_prefill_deep(deep)
                 if cfg is not None:
                     tiled_config(*cfg[:3])
                     L.p2p_prefill_phased(cfg[3] if len(cfg) > 3 else 1)
@@ -58,6 +72,10 @@ def main():
                                   "TBps": round(N * K * 2 / (t * 1e-6) / 1e12, 2)}), flush=True)
             set_tiled_min_m(65)
             tiled_config(2, 0, 0)
+            L.p2p_prefill_deep(1)
+            if a.no_hipblaslt:
+                del W
+                continue
             Wb = torch.randn(K, N, device="cuda").to(torch.bfloat16)
             xin = x if K == H else xf
             t = graph_time(lambda i: torch.matmul(xin, Wb), n_inner=10)

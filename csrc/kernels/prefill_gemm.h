@@ -66,6 +66,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 // Waits until at most `pending` x L of this thread's LDS-DMA loads are in flight.
 template <int L, int STAGES>
 __device__ __forceinline__ void wait_tiles(int pending) {
+  if constexpr (STAGES >= 6) {
+    if (pending >= 4) { wait_vmcnt<4 * L>(); return; }
+  }
+  if constexpr (STAGES >= 5) {
+    if (pending >= 3) { wait_vmcnt<3 * L>(); return; }
+  }
   if constexpr (STAGES >= 4) {
     if (pending >= 2) { wait_vmcnt<2 * L>(); return; }
   }
@@ -713,51 +719,103 @@ static int cu_count() {
 
 // LDS stages per tile shape.  Measured on MI355X (bench/prefill_gemm_bench.py): the
 // 64-row tiles are latency-bound streams and want 3-4 stages in flight; the 128/256-row
-// tiles are MFMA-bound and lose more to 1-block/CU occupancy than they gain from depth.
+// tiles are MFMA-bound at large M, where two blocks share a CU and hide each other's
+// loads, and lose more to 1-block/CU occupancy than they gain from depth.
 template <int BM, int BN>
 constexpr int stages_for() {
   if constexpr (BM >= 128) return 2;
   return BN <= 128 ? 4 : 3;
 }
 
-template <int BM, int BN, int EPI, bool NORM>
-int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off, void* out,
-           int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
-  constexpr int STAGES = stages_for<BM, BN>();
-  const int m_tiles = (M + BM - 1) / BM;
-  const int n_tiles = N / BN;
+// Deep variant for grids of at most one block per CU (mid-M prompts, split-K tiles): one
+// resident block per CU is bound by its own bytes in flight (Little's law: one 128x128
+// stage is 32 KiB, a k-tile's MFMAs take ~0.05 us, an L2/MALL round trip ~1.5 us), so the
+// block keeps as many stages in flight as 160 KiB of LDS holds.
+// The 64-row tiles already run 3-4 stages and measured 4-9 % slower with 4-6
+// (profiles/r2_prefill_gemm_deep_stages.jsonl): deep applies from 128 rows.
+template <int BM, int BN>
+constexpr int deep_stages_for() {
+  if constexpr (BM < 128) return stages_for<BM, BN>();
+  constexpr int stage_bytes = (BM + BN) * BK * 2;
+  constexpr int most = (160 * 1024) / stage_bytes;
+  return most > 6 ? 6 : (most < 2 ? 2 : most);
+}
+
+// 0 = shallow stages only, 1 = deep variant when the grid is <= one block per CU (default),
+// 2 = deep variant always (A/B).
+static int g_deep = 1;
+
+template <int BM, int BN, int EPI, bool NORM, int STAGES>
+int launch_stages(const void* Wt, const void* X, int ldx, int M, int K, int m_tiles, int n_tiles,
+                  int up_off, void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st,
+                  int splitk, char* ws, int par) {
   const int tiles = m_tiles * n_tiles;
-  const int nk = K / BK;
-  // too few tiles to fill 256 CUs: split K so every CU gets work (>= 4 k-tiles per slice)
-  // (measured on MI355X at 8B shapes: ~400 blocks, >= 16 k-tiles per slice)
-  int splitk = g_splitk ? g_splitk : std::min(8, std::max(1, std::min(400 / tiles, nk / 16)));
-  splitk = std::max(1, std::min(splitk, nk / 4));
-  if (splitk > 1 && (size_t)tiles * sizeof(unsigned) < kCounterBytes / 2) {
+  if (splitk > 1) {
     constexpr int FM = BM / 32, FN = BN / 64;
     const size_t slab = (size_t)tiles * splitk * FM * FN * NT * sizeof(f32x4);
-    const size_t ssb = (size_t)tiles * splitk * BM * sizeof(float);
-    char* ws = nullptr;
-    if (split_ws(slab + ssb, st, &ws) && slab + ssb < 0x7FFFFFFF) {
-      // counters live at the END of the workspace at a fixed offset from the end so a
-      // grown workspace keeps them zeroed; see split_ws.  Layout of that region (u32):
-      // [0, n/2) arrival tickets, [n/2, n-1) generations, [n-1] the fault word.
-      unsigned* ctr = (unsigned*)(ws + g_split_ws.bytes - kCounterBytes);
-      constexpr size_t nw = kCounterBytes / sizeof(unsigned);
-      const int cus = cu_count();
-      const int par = g_split_parallel && (8 % splitk) == 0 && cus > 0 && tiles * splitk <= cus;
-      SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), ctr, ctr + nw / 2,
-                   (int*)(ctr + nw - 1), par};
-      hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, true, STAGES>),
-                         dim3(tiles * splitk), dim3(NT), 0, st, (const bf16x8*)Wt,
-                         (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, sp);
-      return (int)hipGetLastError();
-    }
+    // counters live at the END of the workspace at a fixed offset from the end so a
+    // grown workspace keeps them zeroed; see split_ws.  Layout of that region (u32):
+    // [0, n/2) arrival tickets, [n/2, n-1) generations, [n-1] the fault word.
+    unsigned* ctr = (unsigned*)(ws + g_split_ws.bytes - kCounterBytes);
+    constexpr size_t nw = kCounterBytes / sizeof(unsigned);
+    SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), ctr, ctr + nw / 2,
+                 (int*)(ctr + nw - 1), par};
+    hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, true, STAGES>),
+                       dim3(tiles * splitk), dim3(NT), 0, st, (const bf16x8*)Wt,
+                       (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, sp);
+    return (int)hipGetLastError();
   }
   SplitArgs none{1, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, false, STAGES>), dim3(tiles), dim3(NT), 0,
                      st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off,
                      out, ldo, eps, ea, none);
   return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int EPI, bool NORM>
+int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, int up_off, void* out,
+           int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
+  constexpr int SHALLOW = stages_for<BM, BN>();
+  constexpr int DEEP = deep_stages_for<BM, BN>();
+  const int m_tiles = (M + BM - 1) / BM;
+  const int n_tiles = N / BN;
+  const int tiles = m_tiles * n_tiles;
+  const int nk = K / BK;
+  const int cus = cu_count();
+  const bool deep_auto = DEEP > SHALLOW && g_deep == 1 && cus > 0 && tiles <= cus;
+  // too few tiles to fill 256 CUs: split K so every CU gets work (>= 4 k-tiles per slice)
+  // (measured on MI355X at 8B shapes: ~400 blocks, >= 16 k-tiles per slice); the deep
+  // variant keeps the grid at one block per CU instead (power-of-two slices <= CUs/tiles)
+  int splitk;
+  if (g_splitk) {
+    splitk = g_splitk;
+  } else if (deep_auto) {
+    const int cap = std::min(8, std::max(1, std::min(cus / tiles, nk / 16)));
+    splitk = 1;
+    while (splitk * 2 <= cap) splitk *= 2;
+  } else {
+    splitk = std::min(8, std::max(1, std::min(400 / tiles, nk / 16)));
+  }
+  splitk = std::max(1, std::min(splitk, nk / 4));
+  char* ws = nullptr;
+  int par = 0;
+  if (splitk > 1 && (size_t)tiles * sizeof(unsigned) < kCounterBytes / 2) {
+    constexpr int FM = BM / 32, FN = BN / 64;
+    const size_t slab = (size_t)tiles * splitk * FM * FN * NT * sizeof(f32x4);
+    const size_t ssb = (size_t)tiles * splitk * BM * sizeof(float);
+    if (!(split_ws(slab + ssb, st, &ws) && slab + ssb < 0x7FFFFFFF)) splitk = 1;
+    par = g_split_parallel && (8 % splitk) == 0 && cus > 0 && tiles * splitk <= cus;
+  } else {
+    splitk = 1;
+  }
+  const bool deep = DEEP > SHALLOW && (g_deep == 2 || (g_deep == 1 && cus > 0 && tiles * splitk <= cus));
+  if constexpr (DEEP > SHALLOW) {
+    if (deep)
+      return launch_stages<BM, BN, EPI, NORM, DEEP>(Wt, X, ldx, M, K, m_tiles, n_tiles, up_off, out,
+                                                    ldo, eps, ea, st, splitk, ws, par);
+  }
+  return launch_stages<BM, BN, EPI, NORM, SHALLOW>(Wt, X, ldx, M, K, m_tiles, n_tiles, up_off, out,
+                                                   ldo, eps, ea, st, splitk, ws, par);
 }
 
 template <int BM, int BN, int EPI, bool NORM>

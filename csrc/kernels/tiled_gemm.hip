@@ -209,6 +209,10 @@ static int g_tiled_version = 2;  // 2 = LDS-DMA 8-wave kernel (prefill_gemm.h), 
 // 256x256 prefill tiles: 1 = phased pipeline (default), 0 = the 2-stage kernel (A/B).
 P2P_API void p2p_prefill_phased(int on) { pgemm::g_phased = on ? 1 : 0; }
 
+// Deep LDS pipeline (A/B): 0 = shallow stages only, 1 = deep variant for grids of at most
+// one block per CU (default), 2 = deep variant always.
+P2P_API void p2p_prefill_deep(int mode) { pgemm::g_deep = (mode >= 0 && mode <= 2) ? mode : 1; }
+
 // Split-K reduction mode (A/B): 1 = parallel (every slice reduces a share, default where
 // residency allows), 0 = serial (the last arriving slice reduces the whole tile).
 P2P_API void p2p_tiled_split_parallel(int on) { pgemm::g_split_parallel = on ? 1 : 0; }

@@ -145,10 +145,11 @@ def lib():
         if fn is not None:
             fn.argtypes = []
             fn.restype = c_int
-        fn = getattr(L, "p2p_prefill_phased", None)
-        if fn is not None:
-            fn.argtypes = [c_int]
-            fn.restype = None
+        for name in ("p2p_prefill_phased", "p2p_prefill_deep"):
+            fn = getattr(L, name, None)
+            if fn is not None:
+                fn.argtypes = [c_int]
+                fn.restype = None
         fn = getattr(L, "p2p_skinny_gemm_tune", None)
         if fn is not None:
             fn.argtypes = [c_int, c_int]

@@ -600,6 +600,48 @@ def test_tiled_gemm(M, epi, tiled_cfg):
     assert _rel(out.cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("deep", [0, 2])
+@pytest.mark.parametrize("splitk", [1, 4])
+@pytest.mark.parametrize("tile", [2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("epi", ["store_norm", "silu", "resid"])
+def test_tiled_gemm_deep_stages(epi, tile, splitk, deep):
+    """Shallow (deep=0) and deep LDS pipelines (deep=2: as many stages as 160 KiB holds)
+    of every tile shape against the fp32 reference."""
+    from p2p_llm_chat_go_amd.ops import _lib
+    from p2p_llm_chat_go_amd.ops.gemm import set_tiled_min_m, tiled_config
+
+    L = _lib.lib()
+    torch.manual_seed(tile * 10 + splitk)
+    M, K, N = 300, 1024, 768
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    Wt = ops.tile_weight(W).to(DEV)
+    acc = x.float() @ W.float().t()
+    tiled_config(2, tile, splitk)
+    set_tiled_min_m(1)
+    L.p2p_prefill_deep(deep)
+    try:
+        if epi == "resid":
+            h = torch.randn(M, N).to(torch.bfloat16)
+            hd = h.to(DEV)
+            ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_RESID, out=hd)
+            assert _rel(hd.cpu(), h.float() + acc) < 1e-2
+        else:
+            acc = acc * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+            if epi == "silu":
+                out = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_SILU, norm=True)
+                ref = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
+            else:
+                out = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_STORE, norm=True)
+                ref = acc
+            assert _rel(out.cpu(), ref) < 1e-2
+    finally:
+        L.p2p_prefill_deep(1)
+        set_tiled_min_m(65)
+        tiled_config(2, 0, 0)
+    assert ops.tiled_split_fault() == 0
+
+
 @pytest.mark.parametrize("M", [150, 300])
 def test_tiled_qkv_rope_and_argmax(M, tiled_cfg):
     from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table

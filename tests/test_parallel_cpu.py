@@ -170,7 +170,7 @@ def test_tp_peer_death_raises_cpu():
     port = _port()
     ps = [ctx.Process(target=_dying_worker, args=(r, 2, port, q)) for r in range(2)]
     [p.start() for p in ps]
-    rank, ok, info = q.get(timeout=300)
+    rank, ok, info = q.get(timeout=600)  # spawned ranks import torch: slow under a loaded pytest -n
     [p.join(timeout=60) for p in ps]
     [p.terminate() for p in ps if p.is_alive()]
     assert rank == 0 and ok, info
