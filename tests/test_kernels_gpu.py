@@ -602,7 +602,7 @@ def test_tiled_gemm(M, epi, tiled_cfg):
 
 @pytest.mark.parametrize("deep", [0, 2])
 @pytest.mark.parametrize("splitk", [1, 4])
-@pytest.mark.parametrize("tile", [2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("epi", ["store_norm", "silu", "resid"])
 def test_tiled_gemm_deep_stages(epi, tile, splitk, deep):
     """Shallow (deep=0) and deep LDS pipelines (deep=2: as many stages as 160 KiB holds)
