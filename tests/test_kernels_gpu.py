@@ -642,6 +642,41 @@ def test_tiled_gemm_deep_stages(epi, tile, splitk, deep):
     assert ops.tiled_split_fault() == 0
 
 
+@pytest.mark.parametrize("cfg", [(2, 1, 1), (2, 1, 0), (2, 2, 1), (2, 3, 1), (2, 3, 2)])
+@pytest.mark.parametrize("epi", ["store_norm", "silu", "resid"])
+def test_tiled_gemm_grouped_order(epi, cfg):
+    """More than GROUP_M (8) m-tiles: the grouped tile order (8-m-tile bands) must still
+    cover every output tile exactly once (phased 256x256, 2-stage, 128-row tiles)."""
+    from p2p_llm_chat_go_amd.ops.gemm import set_tiled_min_m, tiled_config
+
+    torch.manual_seed(7)
+    M, K, N = 2100, 512, 1536
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    Wt = ops.tile_weight(W).to(DEV)
+    acc = x.float() @ W.float().t()
+    tiled_config(*cfg)
+    set_tiled_min_m(1)
+    try:
+        if epi == "resid":
+            h = torch.randn(M, N).to(torch.bfloat16)
+            hd = h.to(DEV)
+            ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_RESID, out=hd)
+            assert _rel(hd.cpu(), h.float() + acc) < 1e-2
+        else:
+            acc = acc * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+            if epi == "silu":
+                out = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_SILU, norm=True)
+                ref = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
+            else:
+                out = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_STORE, norm=True)
+                ref = acc
+            assert _rel(out.cpu(), ref) < 1e-2
+    finally:
+        set_tiled_min_m(65)
+        tiled_config(2, 0, 0)
+
+
 @pytest.mark.parametrize("M", [150, 300])
 def test_tiled_qkv_rope_and_argmax(M, tiled_cfg):
     from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
