@@ -38,6 +38,7 @@ struct EpiArgs {
   const float* wscale;  // FP8 weights: per-output-channel scale [N] (null = bf16 weights)
   int u;   // requested pipeline depth (0 = default)
   int ng;  // requested column groups per block (skinny GEMM, M > 16; 0/1 = one)
+  const float* rstd_in;  // prefill GEMM NORM: per-row rstd precomputed (null = in-loop sums)
 };
 
 __device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) {

@@ -135,6 +135,10 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
     Wt += (size_t)e * ea.w_stride;
     mrows = ea.moe_rows + (size_t)e * ea.rows_stride;
   }
+  // rows' RMSNorm rstd precomputed by row_rstd_kernel (ea.rstd_in): the host launches the
+  // NORM = false instantiation, so no sums of squares ride in the k loop (they cost
+  // 12-22 % of the GEMM, profiles/r2_norm_cost.jsonl); applied in the epilogue
+  const bool pre = !NORM && !MOE && ea.rstd_in != nullptr;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;
   const int S = K >> 5;
@@ -317,6 +321,7 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
     }
   };
   auto rstd_of = [&](float t) { return rsqrtf(t / (float)K + eps); };
+  auto rstd_pre = [&](int rl) { return pre ? ea.rstd_in[min(m0 + rl, M - 1)] : 1.f; };
 
   if constexpr (SPLIT) {
     f32x4* my = sp.slab + ((size_t)tile * splitk + split) * (FM * FN) * NT;
@@ -380,8 +385,8 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
         }
       }
       epilogue(vw >> 2, vw & 3, acc, [&](int i, int jj) {
-        if constexpr (!NORM) return 1.f;
         const int rl = (vw >> 2) * (BM / 2) + 16 * i + 4 * q + jj;
+        if constexpr (!NORM) return rstd_pre(rl);
         float t = 0.f;
         for (int s2 = 0; s2 < splitk; ++s2)
           t += __hip_atomic_load(&sp.ss_slab[((size_t)tile * splitk + s2) * BM + rl],
@@ -439,8 +444,9 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   }
 
   epilogue(wm, wn, acc, [&](int i, int jj) {
-    if constexpr (!NORM) return 1.f;
-    return rstd_of(ss_row[wm * (BM / 2) + 16 * i + 4 * q + jj]);
+    const int rl = wm * (BM / 2) + 16 * i + 4 * q + jj;
+    if constexpr (!NORM) return rstd_pre(rl);
+    return rstd_of(ss_row[rl]);
   });
 }
 
@@ -467,6 +473,7 @@ __global__ __launch_bounds__(NT) void prefill_gemm8_kernel(const bf16x8* __restr
   constexpr int BM = 256, BN = 256, FM = 8, FN = 4;
   constexpr int AB = 32, BB = 32, STAGE = (AB + BB) * 64;
   __shared__ __attribute__((aligned(16))) bf16x8 lds[2 * STAGE];
+  const bool pre = !NORM && ea.rstd_in != nullptr;  // rows' rstd precomputed (see above)
 
   const int nb = m_tiles * n_tiles;
   const int b = xcd_remap(blockIdx.x, nb);
@@ -655,7 +662,7 @@ __global__ __launch_bounds__(NT) void prefill_gemm8_kernel(const bf16x8* __restr
       const int rl = wm * (BM / 2) + 16 * i + 4 * q + jj;
       const int m = m0 + rl;
       const bool valid = m < M;
-      float scale = 1.f;
+      float scale = pre ? ea.rstd_in[min(m, M - 1)] : 1.f;
       if constexpr (NORM) scale = rsqrtf(ss_row[rl] / (float)K + eps);
       if constexpr (EPI == EPI_SILU) {
 #pragma unroll
@@ -903,6 +910,59 @@ int pick_tile(int M, int N) {
   return best;
 }
 
+// Per-row RMSNorm statistics for the prefill GEMMs (one wave per row, every 16-byte load
+// of the row issued before the first use): rstd[m] = rsqrt(mean_k X[m,k]^2 + eps).  Run
+// once per normed projection instead of inside every n-tile's k loop.
+__global__ __launch_bounds__(256) void row_rstd_kernel(const bf16* __restrict__ X, int ldx, int M,
+                                                       int K, float eps, float* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const bf16x8* p = reinterpret_cast<const bf16x8*>(X + (size_t)row * ldx);
+  const int nv = K / 8;
+  float s = 0.f;
+  for (int c0 = 0; c0 < nv; c0 += 64 * 16) {
+    bf16x8 v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = c0 + 64 * j + lane;
+      v[j] = c < nv ? p[c] : zero_bf16x8();
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = (float)v[j][e];
+        s = fmaf(f, f, s);
+      }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[row] = rsqrtf(s / (float)K + eps);
+}
+
+// rstd workspace: grow-only like the split-K workspace (a captured graph keeps its address);
+// never grown while capturing (the GEMM then keeps the in-loop sums)
+static SplitWs g_rstd_ws;
+static int g_pre_rstd = 1;  // 0: always in-loop sums (A/B)
+static const float* pre_rstd(const void* X, int ldx, int M, int K, float eps, hipStream_t st) {
+  if (!g_pre_rstd || M < 128 || (ldx % 8) || (K % 8) || ((uintptr_t)X % 16)) return nullptr;
+  const size_t bytes = (size_t)M * sizeof(float);
+  if (g_rstd_ws.bytes < bytes) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
+    void* buf = nullptr;
+    const size_t want = std::max(bytes, 2 * g_rstd_ws.bytes);
+    if (hipMalloc(&buf, want) != hipSuccess) return nullptr;
+    g_rstd_ws.buf = buf;  // the old buffer stays allocated (see split_ws)
+    g_rstd_ws.bytes = want;
+  }
+  float* out = (float*)g_rstd_ws.buf;
+  hipLaunchKernelGGL(row_rstd_kernel, dim3((M + 3) / 4), dim3(256), 0, st, (const bf16*)X, ldx, M,
+                     K, eps, out);
+  return hipGetLastError() == hipSuccess ? out : nullptr;
+}
+
 }  // namespace pgemm
 
 static int g_prefill_tile = 0;  // 0 = heuristic (benchmarks can force 1..3)
@@ -918,6 +978,20 @@ static int prefill_dispatch(const void* Wt, const void* X, int ldx, int M, int K
   const int bn = (tile == 3 || tile == 4 || tile == 6 || tile == 7) ? 128 : 256;
   if (!tile || N % bn) return (int)hipErrorInvalidValue;
   const int up_off = (epi == EPI_SILU) ? N / 32 : 0;
+  // normed projections from 128 rows: rstd by row_rstd_kernel, GEMM without in-loop sums
+  if (norm && !ea.moe_cnt) {
+    if (const float* r = pre_rstd(X, ldx, M, K, eps, st)) {
+      EpiArgs e2 = ea;
+      e2.rstd_in = r;
+      switch (epi) {
+        case EPI_STORE: return launch_tile<EPI_STORE, false>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, e2, st);
+        case EPI_SILU: return launch_tile<EPI_SILU, false>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, e2, st);
+        case EPI_F32: return launch_tile<EPI_F32, false>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, e2, st);
+        case EPI_QKV_ROPE: return launch_tile<EPI_QKV_ROPE, false>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, e2, st);
+        case EPI_ARGMAX: return launch_tile<EPI_ARGMAX, false>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, e2, st);
+      }
+    }
+  }
   switch (epi) {
     case EPI_STORE:
       return norm ? launch_tile<EPI_STORE, true>(tile, Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st)

@@ -367,9 +367,10 @@ int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups,
     }
     return (int)hipErrorInvalidValue;
   }
-  if constexpr (MT > 1) {
-    // two column groups per block (shared A fragments); only where the split-K
-    // reduction buffer still fits the 64 KiB static LDS window
+  if constexpr (MT > 1 || U == 4) {
+    // two column groups per block (shared A fragments at MT > 1; at MT = 1, twice the
+    // weight bytes in flight per wave); only where the split-K reduction buffer still
+    // fits the 64 KiB static LDS window (MT = 1: the 4-deep batch, 8 would spill)
     constexpr int NW2 = 2 * ((EPI == EPI_SILU) ? 2 : 1);
     constexpr size_t lds2 = (size_t)(WAVES - 1) * NW2 * MT * 4 * 64 * 4;
     if constexpr (lds2 <= 56 * 1024) {

@@ -211,6 +211,9 @@ P2P_API void p2p_prefill_phased(int on) { pgemm::g_phased = on ? 1 : 0; }
 
 // Deep LDS pipeline (A/B): 0 = shallow stages only, 1 = deep variant for grids of at most
 // one block per CU (default), 2 = deep variant always.
+// Precomputed per-row rstd for normed prefill GEMMs (A/B): 1 = on (default), 0 = in-loop sums.
+P2P_API void p2p_prefill_pre_rstd(int on) { pgemm::g_pre_rstd = on ? 1 : 0; }
+
 P2P_API void p2p_prefill_deep(int mode) { pgemm::g_deep = (mode >= 0 && mode <= 2) ? mode : 1; }
 
 // Split-K reduction mode (A/B): 1 = parallel (every slice reduces a share, default where

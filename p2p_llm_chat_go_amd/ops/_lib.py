@@ -145,7 +145,7 @@ def lib():
         if fn is not None:
             fn.argtypes = []
             fn.restype = c_int
-        for name in ("p2p_prefill_phased", "p2p_prefill_deep"):
+        for name in ("p2p_prefill_phased", "p2p_prefill_deep", "p2p_prefill_pre_rstd"):
             fn = getattr(L, name, None)
             if fn is not None:
                 fn.argtypes = [c_int]

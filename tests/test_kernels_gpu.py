@@ -91,7 +91,7 @@ def _ng_code(w, u):
     return w | (u << 8) | (2 << 16)
 
 
-@pytest.mark.parametrize("M", [20, 40, 64])
+@pytest.mark.parametrize("M", [1, 7, 20, 40, 64])
 @pytest.mark.parametrize("w,u", [(1, 2), (2, 4), (4, 2), (4, 4)])
 def test_skinny_two_groups_per_block(M, w, u):
     """NG=2 launch codes (two column groups share the A fragments) on every epilogue."""
@@ -675,6 +675,38 @@ def test_tiled_gemm_grouped_order(epi, cfg):
     finally:
         set_tiled_min_m(65)
         tiled_config(2, 0, 0)
+
+
+@pytest.mark.parametrize("pre", [0, 1])
+@pytest.mark.parametrize("cfg", [(2, 1, 1), (2, 3, 1), (2, 3, 4), (2, 6, 1), (2, 7, 2)])
+def test_tiled_norm_precomputed_vs_inloop(cfg, pre):
+    """Normed prefill GEMMs with the rows' rstd from row_rstd_kernel (pre=1, the default
+    from 128 rows) and with the in-loop sums of squares (pre=0) on phased, split-K
+    (parallel) and one-m-tile shapes."""
+    from p2p_llm_chat_go_amd.ops import _lib
+    from p2p_llm_chat_go_amd.ops.gemm import set_tiled_min_m, tiled_config
+
+    L = _lib.lib()
+    torch.manual_seed(11)
+    M, K, N = 300, 1024, 768
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    x = (torch.randn(M, K) * torch.linspace(0.2, 3.0, M)[:, None]).to(torch.bfloat16)
+    Wt = ops.tile_weight(W).to(DEV)
+    acc = (x.float() @ W.float().t()) * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    tiled_config(*cfg)
+    set_tiled_min_m(1)
+    L.p2p_prefill_pre_rstd(pre)
+    try:
+        out = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_STORE, norm=True)
+        assert _rel(out.cpu(), acc) < 1e-2
+        act = ops.skinny_gemm(Wt, x.to(DEV), ops.EPI_SILU, norm=True)
+        ref = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
+        assert _rel(act.cpu(), ref) < 1e-2
+    finally:
+        L.p2p_prefill_pre_rstd(1)
+        set_tiled_min_m(65)
+        tiled_config(2, 0, 0)
+    assert ops.tiled_split_fault() == 0
 
 
 @pytest.mark.parametrize("M", [150, 300])

@@ -132,16 +132,20 @@ def test_u64_max_allreduce_ordering():
 def _dying_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
-    # a bounded collective timeout: a survivor blocked on a dead peer's socket still raises
-    dist.init_process_group("gloo", rank=rank, world_size=world,
-                            timeout=datetime.timedelta(seconds=60))
-    from p2p_llm_chat_go_amd.engine import Engine
-    from p2p_llm_chat_go_amd.parallel.comm import TPComm
+    try:
+        # a bounded collective timeout: a survivor blocked on a dead peer's socket still raises
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=60))
+        from p2p_llm_chat_go_amd.engine import Engine
+        from p2p_llm_chat_go_amd.parallel.comm import TPComm
 
-    comm = TPComm()
-    eng = Engine(TP_CFG, device="cpu", kv_pages=32, comm=comm, tp_rank=rank, tp_size=world)
-    prompts = [[1, 2, 3, 4, 5]]
-    eng.generate(prompts, 4, stop_on_eos=False)
+        comm = TPComm()
+        eng = Engine(TP_CFG, device="cpu", kv_pages=32, comm=comm, tp_rank=rank, tp_size=world)
+        prompts = [[1, 2, 3, 4, 5]]
+        eng.generate(prompts, 4, stop_on_eos=False)
+    except Exception as e:  # rendezvous lost (e.g. the port was taken meanwhile): retry
+        q.put((rank, None, "setup: %s" % e))
+        os._exit(0)
     if rank == 1:  # die mid-decode: after a few collectives of the next reply
         calls = [0]
         orig = comm.allreduce_add_
@@ -166,12 +170,15 @@ def _dying_worker(rank, world, port, q):
 def test_tp_peer_death_raises_cpu():
     """A TP rank dying mid-decode makes the survivor raise (no silent tokens)."""
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    ps = [ctx.Process(target=_dying_worker, args=(r, 2, port, q)) for r in range(2)]
-    [p.start() for p in ps]
-    rank, ok, info = q.get(timeout=600)  # spawned ranks import torch: slow under a loaded pytest -n
-    [p.join(timeout=60) for p in ps]
-    [p.terminate() for p in ps if p.is_alive()]
+    for attempt in range(3):  # a fresh port per attempt if the rendezvous itself failed
+        q = ctx.Queue()
+        port = _port()
+        ps = [ctx.Process(target=_dying_worker, args=(r, 2, port, q)) for r in range(2)]
+        [p.start() for p in ps]
+        rank, ok, info = q.get(timeout=600)  # spawned ranks import torch: slow under pytest -n
+        [p.join(timeout=90) for p in ps]
+        [p.terminate() for p in ps if p.is_alive()]
+        if ok is not None:
+            break
     assert rank == 0 and ok, info
     assert ps[1].exitcode == 3
