@@ -129,6 +129,15 @@ def test_u64_max_allreduce_ordering():
     assert int(flipped.max()) == int(flipped[0, 1])  # the "negative" int64 is the larger u64
 
 
+def _put_exit(q, item, code=0):
+    # os._exit skips the queue's feeder-thread flush: drain it first, or the result can be
+    # lost on a loaded machine and the parent waits for nothing
+    q.put(item)
+    q.close()
+    q.join_thread()
+    os._exit(code)
+
+
 def _dying_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
@@ -144,8 +153,7 @@ def _dying_worker(rank, world, port, q):
         prompts = [[1, 2, 3, 4, 5]]
         eng.generate(prompts, 4, stop_on_eos=False)
     except Exception as e:  # rendezvous lost (e.g. the port was taken meanwhile): retry
-        q.put((rank, None, "setup: %s" % e))
-        os._exit(0)
+        _put_exit(q, (rank, None, "setup: %s" % e))
     if rank == 1:  # die mid-decode: after a few collectives of the next reply
         calls = [0]
         orig = comm.allreduce_add_
@@ -161,10 +169,10 @@ def _dying_worker(rank, world, port, q):
     t0 = time.time()
     try:
         eng.generate(prompts, 16, stop_on_eos=False)
-        q.put((rank, False, "tokens returned with a dead peer"))
+        item = (rank, False, "tokens returned with a dead peer")
     except Exception as e:
-        q.put((rank, True, "%s after %.1fs" % (type(e).__name__, time.time() - t0)))
-    os._exit(0)
+        item = (rank, True, "%s after %.1fs" % (type(e).__name__, time.time() - t0))
+    _put_exit(q, item)
 
 
 def test_tp_peer_death_raises_cpu():
