@@ -138,7 +138,7 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
   // rows' RMSNorm rstd precomputed by row_rstd_kernel (ea.rstd_in): the host launches the
   // NORM = false instantiation, so no sums of squares ride in the k loop (they cost
   // 12-22 % of the GEMM, profiles/r2_norm_cost.jsonl); applied in the epilogue
-  const bool pre = !NORM && !MOE && ea.rstd_in != nullptr;
+  const bool pre = !NORM && ea.rstd_in != nullptr;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;
   const int S = K >> 5;
@@ -321,7 +321,12 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
     }
   };
   auto rstd_of = [&](float t) { return rsqrtf(t / (float)K + eps); };
-  auto rstd_pre = [&](int rl) { return pre ? ea.rstd_in[min(m0 + rl, M - 1)] : 1.f; };
+  auto rstd_pre = [&](int rl) {
+    if (!pre) return 1.f;
+    int m = min(m0 + rl, M - 1);
+    if constexpr (MOE) m = mrows[m] / ea.x_div;  // the slot's token row of X
+    return ea.rstd_in[m];
+  };
 
   if constexpr (SPLIT) {
     f32x4* my = sp.slab + ((size_t)tile * splitk + split) * (FM * FN) * NT;

@@ -320,6 +320,19 @@ P2P_API int p2p_grouped_gemm_tiled(const void* Wt, long long w_stride, int n_exp
   ea.row_w = row_w;
   ea.w_stride = w_stride;
   ea.n_experts = n_experts;
+  // normed (w13): the token rows' rstd once (X has max_rows rows), then the NORM = false
+  // kernel with the rstd applied per slot in the epilogue (prefill_gemm.h, pre_rstd)
+  if (norm && (epi == EPI_SILU || epi == EPI_STORE)) {
+    if (const float* r = pre_rstd(X, ldx, max_rows, K, eps, stream)) {
+      if (epi == EPI_SILU && N % 256) return (int)hipErrorInvalidValue;
+      ea.rstd_in = r;
+      return epi == EPI_SILU
+                 ? launch_moe<128, 128, EPI_SILU, false>(Wt, X, ldx, max_rows, K, N, N / 32, out,
+                                                         ldo, eps, ea, stream)
+                 : launch_moe<128, 128, EPI_STORE, false>(Wt, X, ldx, max_rows, K, N, 0, out, ldo,
+                                                          eps, ea, stream);
+    }
+  }
   if (epi == EPI_SILU) {
     if (!norm || N % 256) return (int)hipErrorInvalidValue;
     return launch_moe<128, 128, EPI_SILU, true>(Wt, X, ldx, max_rows, K, N, N / 32, out, ldo, eps,

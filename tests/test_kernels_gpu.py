@@ -526,7 +526,8 @@ def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
                        for _ in range(e_local)])
     w2 = torch.stack([ops.tile_weight((torch.randn(H, F) * 0.05).to(torch.bfloat16))
                       for _ in range(e_local)])
-    h = torch.randn(R, H).to(torch.bfloat16)
+    # rows of very different norms: a slot -> token-row mix-up in the RMSNorm shows
+    h = (torch.randn(R, H) * torch.linspace(0.2, 3.0, R)[:, None]).to(torch.bfloat16)
     outs = {}
     for dev in ("cpu", DEV):
         ids = torch.zeros(R * K, dtype=torch.int32, device=dev)

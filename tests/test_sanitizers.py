@@ -137,7 +137,7 @@ def test_daemons_clean_under_sanitizer(sanbin, tmp_path):
                               range(16)))
         assert sts == [200] * 16
         assert http("POST", f + "/send", {"to_username": "E", "content": "back"})[0] == 200
-        assert len(_wait_inbox(f, 16)) == 16
+        assert len(_wait_inbox(f, 16, timeout=60)) == 16  # TSan: 5-15x slower, PTO backoff
         assert _wait_inbox(e, 1)[0]["content"] == "back"
     finally:
         sp.close()
