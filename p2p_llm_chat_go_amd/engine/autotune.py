@@ -47,8 +47,10 @@ def _configs(K, M=1, tiled=False, midm=False):
     out = [G.TILED_FLAG] if (tiled and M > 16) else []
     if midm and M > 1 and K % 128 == 0:
         out.append(G.MIDM_FLAG)
-    for ng in (1, 2):
-        for u in (((4, 8) if ng == 1 else (4,)) if M <= 16 else (2, 4)):
+    # NG=2 at M <= 16 (twice the weight bytes in flight per wave) is supported by the kernel
+    # but was never faster at the 8B decode shapes (two bench runs, w1-w8): not tuned
+    for ng in ((1,) if M <= 16 else (1, 2)):
+        for u in ((4, 8) if M <= 16 else (2, 4)):
             for w in (1, 2, 4, 8):
                 if (K // 32) // w >= 8 and not (ng > 1 and w == 8):
                     out.append(w | (u << 8) | ((ng if ng > 1 else 0) << 16))
