@@ -222,7 +222,9 @@ def run(a):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            # weight-only fp8 runs are labelled as such (bf16 activations / MFMA inputs,
+            # e4m3 weights): never readable as the bf16 headline
+            "dtype": "bf16" if a.weights == "bf16" else "fp8-weights/bf16-compute",
             "data": "synthetic chat prompts (reference co-pilot template, llama3.1 chat format, "
                     "median-length sample message); random-init weights",
             "config": {"model": cfg.name, "global_batch": (world // group_size) * a.peers,

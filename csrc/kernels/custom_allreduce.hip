@@ -35,6 +35,7 @@
 #include <cstring>
 
 #include "common.h"
+#include "fused_ar.h"
 
 namespace {
 
@@ -329,10 +330,21 @@ P2P_API int p2p_car_close_handle(void* p) { return (int)hipIpcCloseMemHandle(p);
 P2P_API int p2p_car_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
 
 // Spin bound of every later call on the current device (ms > 0).
+static long long g_host_spin_ticks = 500000000ll;  // = g_spin_ticks, for the fused epilogue
+
 P2P_API int p2p_car_set_timeout_ms(int ms) {
   if (ms <= 0) return 1;
   const long long ticks = (long long)ms * 100000ll;  // 100 MHz constant clock
+  g_host_spin_ticks = ticks;
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_spin_ticks), &ticks, sizeof(ticks));
+}
+
+P2P_API long long p2p_car_spin_ticks() { return g_host_spin_ticks; }
+
+// Bytes of one rank's fused-epilogue all-reduce buffer (fused_ar.h) for partials of up to
+// max_bytes; allocate / export / map it with p2p_car_alloc / _get_handle / _open_handle.
+P2P_API size_t p2p_far_buffer_bytes(size_t max_bytes) {
+  return FAR_FLAG_BYTES + 2ull * FAR_MAX_RANKS * max_bytes;
 }
 
 // h[n] += sum over the group's ranks of partial[n] (bf16, n % 8 == 0,

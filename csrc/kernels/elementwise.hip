@@ -24,12 +24,21 @@ __device__ __forceinline__ int reduce_keys(unsigned long long* keys, int m) {
 }
 
 // out[t, :] = src[idx[t], :]  (H bf16 per row, 16-B vectors)
+// An index outside [0, n_src) -- e.g. a token id decoded from the argmax keys of a step
+// whose collective timed out -- yields a zero row instead of a wild read (the fault word
+// already makes the host raise; this keeps the device from faulting first).
 __global__ __launch_bounds__(256) void gather_rows_kernel(const bf16* __restrict__ src,
                                                           const int* __restrict__ idx, int H,
-                                                          bf16* __restrict__ out, int ldo) {
+                                                          int n_src, bf16* __restrict__ out,
+                                                          int ldo) {
   const int t = blockIdx.x;
-  const bf16x8* s = reinterpret_cast<const bf16x8*>(src + (size_t)idx[t] * H);
+  const int r = idx[t];
   bf16x8* o = reinterpret_cast<bf16x8*>(out + (size_t)t * ldo);
+  if (r < 0 || r >= n_src) {
+    for (int i = threadIdx.x; i < H / 8; i += 256) o[i] = zero_bf16x8();
+    return;
+  }
+  const bf16x8* s = reinterpret_cast<const bf16x8*>(src + (size_t)r * H);
   for (int i = threadIdx.x; i < H / 8; i += 256) o[i] = s[i];
 }
 
@@ -148,11 +157,11 @@ P2P_API int p2p_argmax_finalize(unsigned long long* keys, int* ids, int M, hipSt
   return (int)hipGetLastError();
 }
 
-P2P_API int p2p_gather_rows(const void* src, const int* idx, int T, int H, void* out, int ldo,
-                            hipStream_t st) {
-  if (H % 8 != 0 || T <= 0) return (int)hipErrorInvalidValue;
+P2P_API int p2p_gather_rows(const void* src, const int* idx, int T, int H, int n_src, void* out,
+                            int ldo, hipStream_t st) {
+  if (H % 8 != 0 || T <= 0 || n_src <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(T), dim3(256), 0, st, (const bf16*)src, idx, H,
-                     (bf16*)out, ldo);
+                     n_src, (bf16*)out, ldo);
   return (int)hipGetLastError();
 }
 

@@ -2,11 +2,14 @@
 // fp32 accumulator element (row m, column 16*g + r) after the K reduction.
 #pragma once
 #include "common.h"
+#include "fused_ar.h"
 
 namespace {
 
+// EPI_AR: TP row-parallel projection with the all-reduce + residual add fused into the
+// epilogue (skinny kernel only; fused_ar.h)
 enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_F32 = 3, EPI_QKV_ROPE = 4,
-             EPI_ARGMAX = 5 };
+             EPI_ARGMAX = 5, EPI_AR = 6 };
 
 constexpr int PAGE = 64;
 constexpr int HD = 128;
@@ -39,6 +42,7 @@ struct EpiArgs {
   int u;   // requested pipeline depth (0 = default)
   int ng;  // requested column groups per block (skinny GEMM, M > 16; 0/1 = one)
   const float* rstd_in;  // prefill GEMM NORM: per-row rstd precomputed (null = in-loop sums)
+  FusedArArgs far;       // EPI_AR: the group's fused all-reduce buffers
 };
 
 __device__ __forceinline__ unsigned long long argmax_key(float v, unsigned idx) {

@@ -280,6 +280,20 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   }
 
   // ---- epilogue (wave 0) ----
+  if constexpr (EPI == EPI_AR) {  // TP row-parallel: push, wait, sum + residual (fused_ar.h)
+    static_assert(NG == 1 && !MOE, "fused all-reduce: one column group per block");
+    float v[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float s = rstd[mt][j];
+        if constexpr (F8) s *= ea.wscale[(size_t)g0 * 16 + r];
+        v[mt][j] = acc[0][mt][j] * s;
+      }
+    far::epilogue<MT>(v, M, g0, lane, reinterpret_cast<bf16*>(out), ldo, ea.far);
+    return;
+  }
 #pragma unroll
   for (int c = 0; c < NG; ++c) {
     const int g = g0 + c;
@@ -373,7 +387,7 @@ int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups,
     // fits the 64 KiB static LDS window (MT = 1: the 4-deep batch, 8 would spill)
     constexpr int NW2 = 2 * ((EPI == EPI_SILU) ? 2 : 1);
     constexpr size_t lds2 = (size_t)(WAVES - 1) * NW2 * MT * 4 * 64 * 4;
-    if constexpr (lds2 <= 56 * 1024) {
+    if constexpr (lds2 <= 56 * 1024 && EPI != EPI_AR) {
       if (ea.ng == 2 && groups % 2 == 0) {
         hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, false, 2>),
                            dim3(groups / 2), dim3(WAVES * 64), 0, st, (const bf16x8*)Wt,
@@ -497,6 +511,10 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
     case EPI_ARGMAX:
       if (!norm) return (int)hipErrorInvalidValue;
       return launch_e<EPI_ARGMAX, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream);
+    case EPI_AR:
+      if (norm || ea.moe_cnt) return (int)hipErrorInvalidValue;
+      ea2.ng = 0;  // one column group per block: block b owns the same columns on every rank
+      return launch_e<EPI_AR, false>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea2, stream);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -551,6 +569,33 @@ P2P_API int p2p_skinny_gemm_qkv_rope(const void* Wt, const void* X, int ldx, int
   ea.Hkv = Hkv;
   const int N = (Hq + 2 * Hkv) * HD;
   return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_QKV_ROPE, 1, nullptr, 0, eps, waves, ea, stream);
+}
+
+// TP row-parallel projection with the all-reduce fused into the epilogue (fused_ar.h):
+//   h[m, :N] += sum over the group's ranks of (X @ W^T)[m, :N]   (bf16 partials, rank order)
+// bases: every rank's fused buffer (p2p_far_buffer_bytes(max_bytes), own at [rank]);
+// counters: device u32 [FAR_MAX_BLOCKS] (zeroed, private); err: device int.  Every rank
+// of the group must make the same sequence of calls with the same N and M.  The tiled /
+// mid-M launch-code bits are ignored (skinny kernel only; M <= 64).
+P2P_API int p2p_skinny_gemm_ar(const void* Wt, const void* X, int ldx, int M, int K, int N,
+                               void* h, int ldh, void* const* bases, int rank, int world,
+                               size_t max_bytes, unsigned* counters, int* err, int waves,
+                               const float* wscale, hipStream_t stream) {
+  if (world < 1 || world > FAR_MAX_RANKS || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
+  if (N % 16 || N / 16 > FAR_MAX_BLOCKS || ldh % 8 || ldh < N || M < 1 || M > 64 || max_bytes % 16)
+    return (int)hipErrorInvalidValue;
+  if (((size_t)(M - 1) * ldh + N) * 2 > max_bytes) return (int)hipErrorInvalidValue;
+  EpiArgs ea = {};
+  ea.wscale = wscale;
+  for (int p = 0; p < world; ++p) ea.far.base[p] = (char*)bases[p];
+  ea.far.rank = rank;
+  ea.far.world = world;
+  ea.far.max_bytes = max_bytes;
+  ea.far.counters = counters;
+  ea.far.err = err;
+  ea.far.spin_ticks = p2p_car_spin_ticks();
+  waves &= ~(MIDM_FLAG | (1 << 24));  // skinny only
+  return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_AR, 0, h, ldh, 0.f, waves, ea, stream);
 }
 
 // tiled_gemm.hip: the grouped mode of the LDS-tiled MFMA kernel (rows > 64)

@@ -108,6 +108,11 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
             best = min(times, key=times.get)
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)
             G.set_tune(G.tune_key(wts[0], M, epi, norm), best)
+            if epi == G.EPI_RESID:
+                # TP row-parallel projections run the same shape with other epilogues
+                # (partial store / fused all-reduce); the weight stream is the same
+                for e2 in (G.EPI_STORE, G.EPI_AR):
+                    G.set_tune(G.tune_key(wts[0], M, e2, False), best)
             result[(name, M)] = (describe(best), times[best] * 1000 / len(wts))
             if verbose:
                 print("autotune %-9s M=%-2d %s  %.2f us" % (

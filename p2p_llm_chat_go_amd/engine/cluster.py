@@ -137,13 +137,21 @@ def build_rank_engine(spec: dict, rank: int, device: str):
     from ..models.weights import EngineWeights
     from ..parallel.comm import TPComm
 
-    cfg = get_config(spec["model"])
     tp, ep = spec.get("tp", 1), spec.get("ep", 1)
     par = dict(tp_rank=rank, tp_size=tp) if tp > 1 else {}
     if ep > 1:
-        par = dict(ep_rank=rank, ep_size=ep, ep_mode="allreduce")
+        par = dict(ep_rank=rank, ep_size=ep, ep_mode=spec.get("ep_mode", "allreduce"))
     weights = None
-    if spec.get("sd_seed") is not None:  # sharding-invariant random init (tests, parity)
+    ckpt = spec.get("checkpoint")
+    if ckpt:  # HF checkpoint: every rank reads only its own shard of each tensor
+        from ..models.weights import LazySafetensors, config_from_hf
+
+        cfg = config_from_hf(ckpt)
+        weights = EngineWeights.from_state_dict(LazySafetensors(ckpt), cfg, device, **{
+            k: v for k, v in par.items() if k != "ep_mode"})
+    else:
+        cfg = get_config(spec["model"])
+    if not ckpt and spec.get("sd_seed") is not None:  # sharding-invariant random init (tests)
         from ..models.reference import random_state_dict
 
         sd = random_state_dict(cfg, seed=int(spec["sd_seed"]))
@@ -207,7 +215,8 @@ def _leader_main(spec, replica, eng, parent_conn, follower_conns):
 
     group = spec.get("tp", 1) * spec.get("ep", 1)
     front = LockstepEngine(eng, follower_conns) if group > 1 else eng
-    server = EngineServer(front, get_tokenizer(eng.cfg, spec.get("tokenizer")),
+    server = EngineServer(front, get_tokenizer(eng.cfg, spec.get("tokenizer")
+                                               or spec.get("checkpoint")),
                           model_name=spec.get("model_name", "llama3.1"),
                           default_max_tokens=spec.get("max_tokens", 128))
     send_lock = threading.Lock()
@@ -286,7 +295,7 @@ class ClusterServer:
                  max_batch: int = 16, max_tokens: int = 128, model_name: str = "llama3.1",
                  weights: str | None = None, tokenizer: str | None = None, sd_seed=None,
                  kv_pages=None, warmup: bool = True, start_timeout: float = 1800.0,
-                 first_gpu: int = 0):
+                 first_gpu: int = 0, checkpoint: str | None = None, ep_mode: str = "allreduce"):
         import multiprocessing as mp
 
         group = tp * ep
@@ -296,7 +305,8 @@ class ClusterServer:
         self.group = group
         spec = dict(model=model, tp=tp, ep=ep, max_batch=max_batch, max_tokens=max_tokens,
                     model_name=model_name, weights=weights, tokenizer=tokenizer, sd_seed=sd_seed,
-                    kv_pages=kv_pages, warmup=warmup, world=gpus)
+                    kv_pages=kv_pages, warmup=warmup, world=gpus, checkpoint=checkpoint or None,
+                    ep_mode=ep_mode)
         ctx = mp.get_context("spawn")
         self._replicas = []
         self._rid = itertools.count(1)
@@ -485,4 +495,6 @@ def from_env(device: str | None = None):
                          tokenizer=os.environ.get("TOKENIZER_PATH") or None,
                          sd_seed=int(seed) if seed else None,
                          warmup=os.environ.get("ENGINE_WARMUP", "1") != "0",
-                         first_gpu=int(os.environ.get("ENGINE_FIRST_GPU", "0")))
+                         first_gpu=int(os.environ.get("ENGINE_FIRST_GPU", "0")),
+                         checkpoint=os.environ.get("ENGINE_CHECKPOINT") or None,
+                         ep_mode=os.environ.get("ENGINE_EP_MODE", "allreduce"))

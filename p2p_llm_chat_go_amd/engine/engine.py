@@ -126,7 +126,26 @@ class Engine:
 
         if self.device.type == "cuda" and os.environ.get("P2P_AUTOTUNE", "1") != "0":
             self.tuning = autotune_model(self.model, batch_sizes, verbose=verbose)
+            self._share_tuning()
         return getattr(self, "tuning", {})
+
+    def _share_tuning(self):
+        """TP/EP: every rank adopts the group leader's launch codes.  The ranks must agree
+        on which kernel runs a row-parallel projection (the fused all-reduce epilogue
+        exists on the skinny kernel only), and a group steps at its slowest rank anyway."""
+        comm = self.model.comm
+        if comm is None or getattr(comm, "world", 1) <= 1:
+            return
+        import torch.distributed as dist
+
+        from ..ops import gemm as G
+
+        src = 0 if comm.group is None else dist.get_global_rank(comm.group, 0)
+        box = [dict(G._TUNE), self.tuning]
+        dist.broadcast_object_list(box, src=src, group=comm.group)
+        G._TUNE.clear()
+        G._TUNE.update(box[0])
+        self.tuning = box[1]
 
     def warmup(self, batch_sizes=(1,), ctx=256, autotune=True):
         if autotune and not getattr(self, "tuning", None):

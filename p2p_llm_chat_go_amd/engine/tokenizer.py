@@ -6,8 +6,12 @@
 * ``SyntheticTokenizer`` is the offline default (no tokenizer files on the
   box): a deterministic word-level tokenizer whose token counts track BPE on
   English chat text (one token per word / punctuation mark), which is all the
-  benchmark depends on.  Ids are stable hashes into the model vocabulary;
-  decoding returns words it has seen and ``<id>`` placeholders otherwise.
+  benchmark depends on.  Ids are stable hashes into the model vocabulary.
+  Decoding is a pure function of the id, identical in every process (DP replicas,
+  TP ranks, the node): ids of a fixed built-in vocabulary (common chat words, the
+  co-pilot template, the sample messages) decode to their word, every other id to a
+  deterministic pronounceable pseudo-word -- never to whatever this process happened
+  to encode before.
 
 ``suggest_prompt`` reproduces the reference co-pilot template verbatim
 (`web/streamlit_app.py:93`) and ``chat_ids`` wraps it the way Ollama's
@@ -63,8 +67,25 @@ def _render_messages(tok, messages: list, special) -> list:
     return ids
 
 
+# Built-in vocabulary of the synthetic tokenizer: decoding these words is exact.
+_COMMON = (
+    "a about after again all also am an and any are around as at back be been before being "
+    "best better but by call can could day did do does done don't down each even every find "
+    "first for from get give go going good got great had has have he hear hello help her here "
+    "hey hi him his hope how i if in into is it it's just know last let like look lot love make "
+    "many maybe me meet more morning most much my need new next nice night no not now of off "
+    "ok okay on one only or other our out over please plan really right said same see send she "
+    "should so some soon sorry sounds still sure take talk team tell than thank thanks that "
+    "the their them then there these they thing think this time to today tomorrow too two up "
+    "us very want was way we week well were what when where which while who why will with "
+    "work would yeah yes yet you your happy glad free later tonight weekend lunch dinner "
+    "coffee meeting project call message reply friend great awesome cool definitely absolutely "
+    "let's see you soon")
+
+
 class SyntheticTokenizer:
     _pat = re.compile(r"\s*\w+|\s*[^\w\s]|\s+")
+    _tables: dict = {}  # (lo, hi) -> {id: piece}, shared by every instance of a vocab range
 
     def __init__(self, vocab: int = 128256, n_special: int = 256, bos_id=None, eos_ids=None,
                  llama3: bool | None = None):
@@ -74,13 +95,42 @@ class SyntheticTokenizer:
         self.lo = 3
         self.bos_id = bos_id if bos_id is not None else (128000 if self.llama3 else 1)
         self.eos_ids = tuple(eos_ids) if eos_ids else ((128009, 128001) if self.llama3 else (2,))
-        self._seen = {}
 
     def _id(self, piece: str) -> int:
         h = zlib.crc32(piece.encode("utf-8"))
-        i = self.lo + h % (self.hi - self.lo)
-        self._seen.setdefault(i, piece)
-        return i
+        return self.lo + h % (self.hi - self.lo)
+
+    def _table(self) -> dict:
+        key = (self.lo, self.hi)
+        t = SyntheticTokenizer._tables.get(key)
+        if t is None:
+            corpus = [_COMMON, SUGGEST_TEMPLATE, "user assistant system"] + list(SAMPLE_MESSAGES)
+            pieces = set()
+            for text in corpus:
+                for m in self._pat.finditer(text):
+                    w = m.group(0)
+                    for v in (w.strip(), w.strip().capitalize()):
+                        pieces.update((v, " " + v, "\n" + v, "\n\n" + v))
+                    pieces.add(w)
+            pieces.update(("\n\n", "\n", " "))
+            t = {}
+            for w in sorted(p for p in pieces if p):  # sorted: collisions resolve the same way
+                t.setdefault(self._id(w), w)
+            SyntheticTokenizer._tables[key] = t
+        return t
+
+    @staticmethod
+    def _pseudo(i: int) -> str:
+        """Deterministic pronounceable word for an id outside the built-in vocabulary."""
+        cons, vows = "bdfgklmnprstvz", "aeiou"
+        out = []
+        n = int(i)
+        while True:
+            out.append(cons[n % len(cons)] + vows[(n // len(cons)) % len(vows)])
+            n //= len(cons) * len(vows)
+            if n == 0:
+                break
+        return " " + "".join(out)
 
     def encode(self, text: str, bos: bool = False) -> list:
         ids = [self.bos_id] if bos else []
@@ -90,11 +140,13 @@ class SyntheticTokenizer:
     def decode(self, ids) -> str:
         out = []
         inv = {v: k for k, v in LLAMA3_SPECIAL.items()} if self.llama3 else {}
+        table = self._table()
         for i in ids:
             i = int(i)
             if i in inv or i == self.bos_id or i in self.eos_ids:
                 continue
-            out.append(self._seen.get(i, " <%d>" % i))
+            w = table.get(i)
+            out.append(w if w is not None else self._pseudo(i))
         return "".join(out).strip()
 
     def chat_ids(self, user_text: str) -> list:

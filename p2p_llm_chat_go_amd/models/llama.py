@@ -13,8 +13,10 @@ context length.  Per layer (TP=1, dense):
 
 i.e. 5 launches per layer, every RMSNorm / RoPE / KV write / residual add /
 SwiGLU fused into a GEMM; the LM head fuses greedy argmax (64-bit atomicMax
-keys) so no logits round trip on the greedy path.  With TP>1 the row-parallel outputs (o_proj, down) go to a scratch
-buffer and ``comm.allreduce_add_(h, partial)`` sums them into the residual.
+keys) so no logits round trip on the greedy path.  With TP>1 the row-parallel outputs
+(o_proj, down) are summed across ranks in the GEMM epilogue itself at decode sizes
+(``ops.skinny_gemm_ar``, one launch); larger chunks go to a scratch buffer and
+``comm.allreduce_add_(h, partial)`` sums them into the residual.
 MoE layers (Mixtral) route through ``models.moe``.
 
 Every buffer lives in a preallocated ``Workspace`` so the decode step can be
@@ -95,6 +97,10 @@ class LlamaModel:
         # (chunked, separate communication stream); decode-size sums use the one-shot AR
         self.overlap_min_rows = int(os.environ.get("P2P_TP_OVERLAP_MIN_ROWS", "256"))
         self.overlap_chunks = int(os.environ.get("P2P_TP_OVERLAP_CHUNKS", "4"))
+        # TP row-parallel projections of <= 64 rows (decode, short prompt chunks) on the
+        # skinny kernel sum across ranks in their own epilogue (ops.skinny_gemm_ar): 5
+        # launches per layer instead of 7.  P2P_TP_FUSED_AR=0: partial store + one-shot kernel
+        self.fused_ar = os.environ.get("P2P_TP_FUSED_AR", "1") == "1"
         self._comm_stream = None
         # TP sampling reference path: gather the full logits row instead of per-shard top-128
         # candidates (same draw; tests compare the two on the same sharded numerics)
@@ -108,6 +114,12 @@ class LlamaModel:
         """h += x @ W (row-parallel across TP ranks)."""
         if self.tp == 1:
             ops.skinny_gemm(wt, x, ops.EPI_RESID, out=h)
+            return
+        car = getattr(self.comm, "car", None)
+        if (self.fused_ar and car is not None and h.device.type == "cuda"
+                and ops.skinny_ar_ok(wt, R) and car.fused_ok(R, h.shape[1], h.stride(0))):
+            # decode-size sums: the all-reduce + residual run in the GEMM's own epilogue
+            ops.skinny_gemm_ar(wt, x, h, car)
             return
         part = ws.partial[:R]
         if R >= self.overlap_min_rows and h.device.type == "cuda":

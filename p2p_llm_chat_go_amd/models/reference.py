@@ -12,14 +12,19 @@ from .config import ModelConfig, rope_table
 
 
 def random_state_dict(cfg: ModelConfig, seed: int = 0, std: float = 0.02,
-                      dtype=torch.bfloat16, device="cpu") -> dict:
-    g = torch.Generator(device="cpu").manual_seed(seed)
+                      dtype=torch.bfloat16, device="cpu", on_device: bool = False) -> dict:
+    """HF-named random checkpoint.  on_device=True draws with a generator on ``device``
+    (full-width models in multi-process GPU tests: every process of one device gets the
+    same tensors without a multi-GiB CPU draw); False draws on the CPU (the default, so
+    CPU and GPU tests see identical weights for a seed)."""
+    gdev = torch.device(device) if on_device else torch.device("cpu")
+    g = torch.Generator(device=gdev).manual_seed(seed)
 
     def rnd(*shape, s=std):
-        return (torch.randn(*shape, generator=g) * s).to(dtype).to(device)
+        return (torch.randn(*shape, generator=g, device=gdev) * s).to(dtype).to(device)
 
     def gain(n):
-        return (1.0 + 0.1 * torch.randn(n, generator=g)).to(dtype).to(device)
+        return (1.0 + 0.1 * torch.randn(n, generator=g, device=gdev)).to(dtype).to(device)
 
     H, D = cfg.hidden, cfg.head_dim
     sd = {"model.embed_tokens.weight": rnd(cfg.vocab, H, s=1.0), "model.norm.weight": gain(H)}

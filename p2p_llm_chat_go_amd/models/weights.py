@@ -190,6 +190,37 @@ class EngineWeights:
         return cls(cfg, embed, head, layers, tp_rank, tp_size, ep_rank, ep_size)
 
 
+class LazySafetensors:
+    """Read-on-access view of an HF checkpoint directory's ``*.safetensors`` shards (no
+    pickle).  ``EngineWeights.from_state_dict`` takes one tensor at a time and keeps only
+    its rank's slice, so a TP rank never holds the whole checkpoint in host memory (a 70B
+    checkpoint is ~140 GB; eight ranks each loading it whole would be ~1.1 TB)."""
+
+    def __init__(self, path: str):
+        from safetensors import safe_open
+
+        self.path = path
+        files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+        if not files:
+            raise FileNotFoundError("no .safetensors files under %s" % path)
+        self._where = {}
+        self._handles = {}
+        for f in files:
+            h = safe_open(f, framework="pt", device="cpu")
+            self._handles[f] = h
+            for k in h.keys():
+                self._where[k] = f
+
+    def __contains__(self, name):
+        return name in self._where
+
+    def keys(self):
+        return self._where.keys()
+
+    def __getitem__(self, name):
+        return self._handles[self._where[name]].get_tensor(name)
+
+
 def load_safetensors_dir(path: str, device="cpu") -> dict:
     """Read every ``*.safetensors`` shard of an HF checkpoint directory (no pickle)."""
     from safetensors.torch import load_file

@@ -5,7 +5,8 @@ a missing library raises).  CPU tensors run the PyTorch reference of the same
 math -- that is the CPU tiny-llama plumbing config and the numerics oracle,
 never a fallback for GPU tensors.
 """
-from .gemm import (EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, Fp8Weight, argmax_finalize, fold_norm,
+from .gemm import (EPI_AR, EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, Fp8Weight, skinny_ar_ok,
+                   skinny_gemm_ar, argmax_finalize, fold_norm,
                    quantize_fp8,
                    lm_head_argmax, new_argmax_keys, qkv_rope_gemm, rope_row_perm, skinny_gemm, tile_weight,
                    tiled_shape, tiled_split_fault, tiled_split_parallel, untile_weight)
@@ -17,7 +18,7 @@ from .sampling import sample, sample_candidates, topk_candidates
 from ._lib import available as kernels_available, lib as kernel_lib, lib_path as kernel_lib_path
 
 __all__ = [
-    "EPI_F32", "EPI_RESID", "EPI_SILU", "EPI_STORE", "fold_norm", "skinny_gemm", "tile_weight",
+    "EPI_AR", "skinny_ar_ok", "skinny_gemm_ar", "EPI_F32", "EPI_RESID", "EPI_SILU", "EPI_STORE", "fold_norm", "skinny_gemm", "tile_weight",
     "tiled_shape", "untile_weight", "argmax_finalize", "lm_head_argmax", "new_argmax_keys", "qkv_rope_gemm",
     "rope_row_perm", "PAGE", "HEAD_DIM", "attn_workspace", "paged_attention", "flash_prefill", "flash_tile", "prefill_tiles",
     "attn_oproj", "attn_oproj_ok", "attn_oproj_heads", "attn_oproj_heads_ok",

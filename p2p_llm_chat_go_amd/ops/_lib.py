@@ -56,6 +56,9 @@ _SIGS = {
     "p2p_car_all_gather": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p,
                            ctypes.c_longlong, c_void_p, c_void_p, c_int, c_void_p],
     "p2p_car_set_timeout_ms": [c_int],
+    "p2p_skinny_gemm_ar": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                           c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p, c_int,
+                           c_void_p, c_void_p],
     "p2p_attn_oproj": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                        c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_int, c_void_p,
                        c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
@@ -65,7 +68,7 @@ _SIGS = {
     "p2p_attn_oproj_heads_tune": [c_int],
     "p2p_paged_attention_mfma": [c_int],
     "p2p_l3_prefetch": [c_void_p, ctypes.c_size_t, c_int, c_void_p, c_void_p],
-    "p2p_gather_rows": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
+    "p2p_gather_rows": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     "p2p_rope_cache": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "p2p_argmax": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
@@ -129,10 +132,11 @@ def lib():
                 "HIP kernel library missing at %s -- run `python -m p2p_llm_chat_go_amd._build` "
                 "(or __graft_entry__.build())" % _LIB_PATH)
         L = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-        fn = getattr(L, "p2p_car_buffer_bytes", None)
-        if fn is not None:
-            fn.argtypes = [ctypes.c_size_t]
-            fn.restype = ctypes.c_size_t
+        for name in ("p2p_car_buffer_bytes", "p2p_far_buffer_bytes"):
+            fn = getattr(L, name, None)
+            if fn is not None:
+                fn.argtypes = [ctypes.c_size_t]
+                fn.restype = ctypes.c_size_t
         fn = getattr(L, "p2p_tiled_gemm_config", None)
         if fn is not None:
             fn.argtypes = [c_int, c_int, c_int]

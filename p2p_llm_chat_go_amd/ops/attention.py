@@ -212,16 +212,19 @@ def prefill_tiles(seq, pos, tile: int = QTILE) -> torch.Tensor:
 def flash_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                   block_tables: torch.Tensor, tiles: torch.Tensor, n_heads: int, n_kv: int,
                   out: torch.Tensor | None = None, scale: float | None = None,
-                  tiles_host: torch.Tensor | None = None, qtile: int | None = None) -> torch.Tensor:
+                  tiles_host: torch.Tensor | None = None, *, qtile: int) -> torch.Tensor:
     """Causal prefill attention on MFMA for query tiles (see ``prefill_tiles``).
 
     Equivalent to :func:`paged_attention` with one row per prompt token
     (ctx = pos + 1), but reads each K/V page once per query tile x G heads.  The
-    tiles must come from ``prefill_tiles(seq, pos, qtile)`` with ``qtile`` from
-    ``flash_tile`` (default ``flash_tile(n_heads, n_kv)``): > 16 runs the v2 kernel.
+    tiles must come from ``prefill_tiles(seq, pos, qtile)`` with the SAME ``qtile``
+    (from ``flash_tile``): > 16 runs the v2 kernel.  ``qtile`` is required -- the tile
+    width the tiles were cut with decides which kernel may read them.
     """
-    if qtile is None:
-        qtile = flash_tile(n_heads, n_kv)
+    if qtile is None or qtile < 1:
+        raise ValueError("flash_prefill: qtile (the prefill_tiles width) is required")
+    if tiles_host is not None and tiles_host.numel() and int(tiles_host[:, 1].max()) > qtile:
+        raise ValueError("flash_prefill: tiles are wider than qtile=%d" % qtile)
     R = q.shape[0]
     if scale is None:
         scale = 1.0 / math.sqrt(HEAD_DIM)

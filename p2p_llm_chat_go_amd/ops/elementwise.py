@@ -16,8 +16,10 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None =
         out.copy_(src[idx.long()])
         return out
     L = _lib.lib()
-    _lib.check(L.p2p_gather_rows(src.data_ptr(), idx.data_ptr(), T, H, out.data_ptr(),
-                                 out.stride(0), _lib.stream_ptr(src.device)), "gather_rows")
+    assert src.stride(1) == 1 and src.stride(0) == H
+    _lib.check(L.p2p_gather_rows(src.data_ptr(), idx.data_ptr(), T, H, src.shape[0],
+                                 out.data_ptr(), out.stride(0), _lib.stream_ptr(src.device)),
+               "gather_rows")
     return out
 
 

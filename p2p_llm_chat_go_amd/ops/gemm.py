@@ -12,12 +12,15 @@ numerics oracle in tests).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
 
 EPI_STORE, EPI_RESID, EPI_SILU, EPI_F32 = 0, 1, 2, 3
 EPI_QKV_ROPE, EPI_ARGMAX = 4, 5
+EPI_AR = 6  # TP row-parallel projection + fused all-reduce + residual (skinny_gemm_ar)
 SKINNY_MAX_M = 64
 
 # Autotuned launch codes: (N, K, epi, norm, m_tile[, "fp8"]) -> waves | (U << 8)
@@ -254,6 +257,43 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
                                      int(norm), os_.data_ptr(), out.stride(0), float(eps),
                                      _code(wt, mc, epi, norm, waves), sp, s), "skinny_gemm")
     return out
+
+
+_FAR_MAX_WAVES = int(os.environ.get("P2P_FAR_MAX_WAVES", "0"))
+
+
+def skinny_ar_ok(wt, M: int) -> bool:
+    """Would ``skinny_gemm_ar`` run this projection at M rows on its tuned kernel?  Only the
+    skinny kernel has the fused all-reduce epilogue: a shape whose tuned launch is the
+    tiled / mid-M kernel (prompt-sized M) keeps the partial store + one-shot kernel."""
+    if M > SKINNY_MAX_M:
+        return False
+    return not (_code(wt, M, EPI_AR, False, 0) & (TILED_FLAG | MIDM_FLAG))
+
+
+def skinny_gemm_ar(wt, x: torch.Tensor, h: torch.Tensor, car, waves: int = 0) -> torch.Tensor:
+    """h += sum over the TP group of x @ W^T, the all-reduce fused into the GEMM epilogue
+    (``csrc/kernels/fused_ar.h``): every block pushes its bf16 partial tile to every rank,
+    waits for the same tile of the peers and adds the rank-ordered sum to the residual --
+    one launch where the unfused path takes two (partial store, one-shot all-reduce), with
+    a bit-identical result.  ``car``: the group's ``parallel.custom_ar.CustomAllReduce``.
+    Every rank must make the same calls (same N, M) in the same order."""
+    N, K = tiled_shape(wt)
+    M = x.shape[0]
+    assert x.device.type == "cuda" and h.dtype == torch.bfloat16 and h.shape[0] == M
+    assert x.stride(1) == 1 and h.stride(1) == 1 and h.shape[1] == N
+    assert car.fused_ok(M, N, h.stride(0)), (M, N, h.stride(0))
+    code = _code(wt, M, EPI_AR, False, waves)
+    if _FAR_MAX_WAVES and not 0 < (code & 0xff) <= _FAR_MAX_WAVES:
+        # virtual ranks sharing one device: fewer spinning waves per rank so every rank's
+        # grid can be resident at once (tests; a real device runs only its own grid)
+        code = (code & ~0xff) | _FAR_MAX_WAVES
+    wp, sp = _wptr(wt)
+    _lib.check(_lib.lib().p2p_skinny_gemm_ar(
+        wp, x.data_ptr(), x.stride(0), M, K, N, h.data_ptr(), h.stride(0), car._far_bases,
+        car.rank, car.world, car.far_max_bytes, car.far_counters.data_ptr(), car.err.data_ptr(),
+        code, sp, _lib.stream_ptr(x.device)), "skinny_gemm_ar")
+    return h
 
 
 # ------------------------------------------------------------ fused epilogues

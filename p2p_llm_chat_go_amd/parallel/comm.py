@@ -39,11 +39,15 @@ class TPComm:
             car_max_bytes = int(os.environ.get("P2P_CAR_MAX_BYTES", str(4 << 20)))
         self.car_max_bytes = car_max_bytes
         self.car = None
+        # world-1 groups normally skip the IPC kernels; the TP rank proxy
+        # (bench/tp_rank_proxy.py) keeps them so one rank's launch structure is the real one
+        self.car_at_world1 = False
 
     def setup(self, device):
         """Collective-side allocations for ``device`` (call before graph capture)."""
         device = torch.device(device)
-        if self.want_custom_ar and device.type == "cuda" and self.car is None and self.world > 1:
+        if (self.want_custom_ar and device.type == "cuda" and self.car is None
+                and (self.world > 1 or self.car_at_world1)):
             from .custom_ar import CustomAllReduce
 
             self.car = CustomAllReduce(self.group, device, self.car_max_bytes)
@@ -86,6 +90,9 @@ class TPComm:
     def vocab_parallel_argmax(self, logits: torch.Tensor, out: torch.Tensor, v_local: int):
         v, i = logits.max(-1)
         g = i.to(torch.int64) + self.rank * v_local
+        if logits.device.type == "cuda" and self.backend != "nccl":
+            # gloo moves host memory only (virtual ranks on one GPU in tests)
+            v, g = v.cpu(), g.cpu()
         vals = [torch.empty_like(v) for _ in range(self.world)]
         idxs = [torch.empty_like(g) for _ in range(self.world)]
         dist.all_gather(vals, v, group=self.group)

@@ -55,32 +55,43 @@ class CustomAllReduce:
         # bytes and the one-shot has one hop less)
         self.two_shot_min = int(os.environ.get("P2P_CAR_2SHOT_MIN", str(512 << 10)))
         L = self.L = _lib.lib()
+        # partials of the fused row-parallel epilogue (ops.skinny_gemm_ar): up to 64 rows of
+        # a 16384-wide hidden state per call
+        self.far_max_bytes = int(os.environ.get("P2P_FAR_MAX_BYTES", str(2 << 20)))
+        self._opened = []
+        self._owned = []
         with torch.cuda.device(self.device):
-            size = L.p2p_car_buffer_bytes(self.max_bytes)
-            buf = ctypes.c_void_p()
-            _lib.check(L.p2p_car_alloc(size, ctypes.byref(buf)), "car_alloc")
-            self._own = buf
-            hsz = L.p2p_car_handle_size()
-            handle = ctypes.create_string_buffer(hsz)
-            _lib.check(L.p2p_car_get_handle(buf, handle), "car_get_handle")
-            handles = [None] * self.world
-            dist.all_gather_object(handles, handle.raw, group=group)
-            self._opened = []
-            bases = []
-            for r, hb in enumerate(handles):
-                if r == self.rank:
-                    bases.append(buf.value)
-                    continue
-                ptr = ctypes.c_void_p()
-                _lib.check(L.p2p_car_open_handle(ctypes.create_string_buffer(hb, hsz),
-                                                 ctypes.byref(ptr)), "car_open_handle")
-                self._opened.append(ptr)
-                bases.append(ptr.value)
-            self._bases = (ctypes.c_void_p * self.world)(*bases)
+            self._bases = self._map(L.p2p_car_buffer_bytes(self.max_bytes))
+            self._far_bases = self._map(L.p2p_far_buffer_bytes(self.far_max_bytes))
             self.counters = torch.zeros(64, dtype=torch.int32, device=self.device)
+            self.far_counters = torch.zeros(1024, dtype=torch.int32, device=self.device)
             self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         torch.cuda.synchronize(self.device)
-        dist.barrier(group=group)
+        dist.barrier(group=self.group)
+
+    def _map(self, size):
+        """Allocate an uncached buffer, exchange IPC handles over the group, map the peers'.
+        Returns the world's base pointers (own at [rank])."""
+        L = self.L
+        buf = ctypes.c_void_p()
+        _lib.check(L.p2p_car_alloc(size, ctypes.byref(buf)), "car_alloc")
+        self._owned.append(buf)
+        hsz = L.p2p_car_handle_size()
+        handle = ctypes.create_string_buffer(hsz)
+        _lib.check(L.p2p_car_get_handle(buf, handle), "car_get_handle")
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle.raw, group=self.group)
+        bases = []
+        for r, hb in enumerate(handles):
+            if r == self.rank:
+                bases.append(buf.value)
+                continue
+            ptr = ctypes.c_void_p()
+            _lib.check(L.p2p_car_open_handle(ctypes.create_string_buffer(hb, hsz),
+                                             ctypes.byref(ptr)), "car_open_handle")
+            self._opened.append(ptr)
+            bases.append(ptr.value)
+        return (ctypes.c_void_p * self.world)(*bases)
 
     def fits(self, t: torch.Tensor) -> bool:
         return (t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() % 8 == 0
@@ -139,12 +150,19 @@ class CustomAllReduce:
             raise CollectiveTimeout("custom all-reduce: a peer never arrived (timeout); "
                                     "the TP group is broken")
 
+    def fused_ok(self, M: int, N: int, ld: int) -> bool:
+        """Can ops.skinny_gemm_ar sum an [M, N] partial (row stride ld) through the fused
+        buffer?"""
+        return 1 <= M <= 64 and N % 16 == 0 and N // 16 <= 1024 and ld % 8 == 0 and \
+            ((M - 1) * ld + N) * 2 <= self.far_max_bytes
+
     def close(self):
-        if self._own is None:
+        if not self._owned:
             return
         torch.cuda.synchronize(self.device)
         for p in self._opened:
             self.L.p2p_car_close_handle(p)
         self._opened = []
-        self.L.p2p_car_free(self._own)
-        self._own = None
+        for b in self._owned:
+            self.L.p2p_car_free(b)
+        self._owned = []
