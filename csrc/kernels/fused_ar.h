@@ -4,26 +4,30 @@
 // Unfused, a TP row-parallel projection is two dependent launches: the GEMM stores its
 // bf16 partial, then the one-shot kernel (custom_allreduce.hip) pushes it to every peer,
 // waits and sums into the residual.  Fused, the GEMM's own epilogue does that work for
-// the tile it just produced:
-//   1. the block's [M x 16] bf16 partial (the value the unfused GEMM would store) is
-//      staged in LDS and pushed, 16 bytes per lane, into slot [parity][rank] of EVERY
-//      rank's fused buffer (xGMI writes, all peers at once);
-//   2. fence (system scope), then flag [parity][rank][block] := seq on every rank;
-//   3. wait for flag [parity][src][block] == seq of every source on the OWN buffer --
-//      block b only waits for block b of the peers (same grid and column mapping on
-//      every rank), never for a grid barrier;
-//   4. h[m, cols] += sum over ranks in rank order (fp32, one rounding): the unfused
+// the tile it just produced, with the payload carrying its own flag (low-latency "LL"
+// granules, cdna_hip_programming.md publish/consume recipe R2):
+//   1. the block's [M x 16] bf16 partial (the values the unfused GEMM would store) goes
+//      out as 8-byte granules {seq << 32 | two bf16}, one relaxed system-scope 64-bit
+//      store per granule, into slot [parity][rank] of EVERY rank's fused buffer (xGMI
+//      writes, all peers at once).  No release fence (the first version fenced with
+//      __threadfence_system, i.e. an L2 write-back per workgroup: +15 us per call on the
+//      70B TP=8 proxy), no separate flag word;
+//   2. the block sweeps the granules of ITS columns from every source on its own buffer
+//      until every tag == seq (relaxed polls, bounded) -- block b only waits for block b
+//      of the peers (same grid and column mapping on every rank), never a grid barrier;
+//   3. h[m, cols] += sum over ranks in rank order (fp32, one rounding): the unfused
 //      formula, so the two paths are bit-identical on every rank.
-// seq is the group's call index of this block (counters[block] + 1); block 0 keeps the
-// counters of blocks a narrower call does not launch in step, as the one-shot kernel
-// does.  Slot reuse: a rank writes parity p in call k+2 only after its call-(k+1) kernel
-// saw call-(k+1) flags of every peer, which each peer posts only after its call-k kernel
-// (the last reader of parity p) completed.  Spins are bounded; a timeout sets the error
-// word and later calls skip their waits (LlamaModel.check_faults raises on it).
+// seq is the group's call index of this block (counters[block] + 1, never 0); block 0
+// keeps the counters of blocks a narrower call does not launch in step, as the one-shot
+// kernel does.  A granule left from an earlier call carries an older seq, so it is never
+// taken for this call's.  Slot reuse: a rank writes parity p in call k+2 only after its
+// call-(k+1) kernel saw call-(k+1) granules of every peer, which each peer writes only
+// after its call-k kernel (the last reader of parity p) completed.  Spins are bounded; a
+// timeout sets the error word and later calls skip their waits (check_faults raises).
 //
 // Own buffer, separate from the one-shot kernel's (their call sequences interleave):
-//   flags : [2 parities][FAR_MAX_RANKS src][FAR_MAX_BLOCKS] u32
-//   data  : [2 parities][FAR_MAX_RANKS src][max_bytes]   (row-major [M, ldo] bf16)
+//   data : [2 parities][FAR_MAX_RANKS src][max_bytes]   granule (m, c) at (m * ldh / 2 + c)
+//          for column pair c = col / 2 -- twice the bytes of the bf16 partial
 #pragma once
 #include <stddef.h>
 
@@ -31,7 +35,7 @@
 
 constexpr int FAR_MAX_RANKS = 8;
 constexpr int FAR_MAX_BLOCKS = 1024;  // column groups of 16: hidden sizes up to 16384
-constexpr size_t FAR_FLAG_BYTES = 2ull * FAR_MAX_RANKS * FAR_MAX_BLOCKS * 4;
+constexpr size_t FAR_FLAG_BYTES = 0;  // no flag words: the granules carry the tags
 
 struct FusedArArgs {
   char* base[FAR_MAX_RANKS];  // every rank's fused buffer mapped here (own at [rank])
@@ -47,14 +51,24 @@ extern "C" long long p2p_car_spin_ticks();
 
 namespace far {
 
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64;
 
-__device__ __forceinline__ unsigned* flag(char* base, int parity, int src, int blk) {
-  return reinterpret_cast<unsigned*>(base) + ((size_t)parity * FAR_MAX_RANKS + src) * FAR_MAX_BLOCKS + blk;
+__device__ __forceinline__ u64* data(char* base, size_t max_bytes, int parity, int src) {
+  return reinterpret_cast<u64*>(base + FAR_FLAG_BYTES + ((size_t)parity * FAR_MAX_RANKS + src) * max_bytes);
 }
 
-__device__ __forceinline__ bf16* data(char* base, size_t max_bytes, int parity, int src) {
-  return reinterpret_cast<bf16*>(base + FAR_FLAG_BYTES + ((size_t)parity * FAR_MAX_RANKS + src) * max_bytes);
+__device__ __forceinline__ unsigned bf16_bits(float x) {
+  const bf16 b = f2bf(x);
+  unsigned short u;
+  __builtin_memcpy(&u, &b, 2);
+  return u;
+}
+
+__device__ __forceinline__ float bits_bf16(unsigned u) {
+  const unsigned short s = (unsigned short)u;
+  bf16 b;
+  __builtin_memcpy(&b, &s, 2);
+  return (float)b;
 }
 
 // Epilogue of ONE wave (the block's wave 0, after the split-K reduction).  v[mt][j] is the
@@ -63,72 +77,66 @@ __device__ __forceinline__ bf16* data(char* base, size_t max_bytes, int parity, 
 template <int MT>
 __device__ __forceinline__ void epilogue(const float (&v)[MT][4], int M, int g, int lane,
                                          bf16* __restrict__ h, int ldh, const FusedArArgs& fa) {
-  __shared__ __attribute__((aligned(16))) bf16 tile[MT * 16][16];
   const int r = lane & 15, q = lane >> 4;
   const int blk = blockIdx.x, nblk = gridDim.x;
+  const unsigned seq = fa.counters[blk] + 1;
+  const int parity = seq & 1;
+  const int failed = __hip_atomic_load(fa.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const size_t row_g = (size_t)ldh / 2;  // granules per row
+  const size_t c0 = (size_t)g * 8;       // first granule (column pair) of this block
+  // 1. publish: lanes with an even column pack (col, col + 1) with the tag
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = mt * 16 + q * 4 + j;
-      if (m < M) tile[m][r] = f2bf(v[mt][j]);  // the partial the unfused GEMM would store
+      const float hi = __shfl_xor(v[mt][j], 1, 64);
+      if (m < M && (r & 1) == 0) {
+        const u64 gr = ((u64)seq << 32) | ((u64)bf16_bits(hi) << 16) | bf16_bits(v[mt][j]);
+        const size_t off = (size_t)m * row_g + c0 + (r >> 1);
+        for (int p = 0; p < fa.world; ++p)
+          __hip_atomic_store(data(fa.base[p], fa.max_bytes, parity, fa.rank) + off, gr,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
-  const unsigned seq = fa.counters[blk] + 1;
-  const int parity = seq & 1;
-  const int failed = __hip_atomic_load(fa.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // LDS tile complete before other lanes read it (single wave: fence + wave barrier)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const int nch = 2 * M;  // 16-byte chunks: 8 columns of one row
-  const size_t col0 = (size_t)g * 16;
-  // 1. push to every rank (including this one)
-  for (int c = lane; c < nch; c += 64) {
-    const int m = c >> 1, hf = c & 1;
-    const v4u val = *reinterpret_cast<const v4u*>(&tile[m][hf * 8]);
-    const size_t off = (size_t)m * ldh + col0 + hf * 8;
-    for (int p = 0; p < fa.world; ++p)
-      *reinterpret_cast<v4u*>(data(fa.base[p], fa.max_bytes, parity, fa.rank) + off) = val;
-  }
-  __threadfence_system();
-  // 2. post
-  if (lane < fa.world)
-    __hip_atomic_store(flag(fa.base[lane], parity, fa.rank, blk), seq, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  // 3. wait for block `blk` of every source (bounded; skipped once a peer is known dead)
-  if (lane < fa.world && !failed) {
-    unsigned* f = flag(fa.base[fa.rank], parity, lane, blk);
-    const long long t0 = wall_clock64();
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+  // 2. + 3. sweep this block's granules of every source, then h += rank-ordered sum
+  const long long t0 = wall_clock64();
+  for (int i = lane; i < 8 * M; i += 64) {
+    const int m = i >> 3, c = i & 7;
+    const size_t off = (size_t)m * row_g + c0 + c;
+    unsigned* hp = reinterpret_cast<unsigned*>(h + (size_t)m * ldh + 2 * (c0 + c));
+    const unsigned hv = *hp;
+    float a0 = bits_bf16(hv & 0xffff), a1 = bits_bf16(hv >> 16);
+    u64 x[FAR_MAX_RANKS];
+#pragma unroll
+    for (int p = 0; p < FAR_MAX_RANKS; ++p)  // every source's granule in flight at once
+      x[p] = p < fa.world ? __hip_atomic_load(data(fa.base[fa.rank], fa.max_bytes, parity, p) + off,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                          : ((u64)seq << 32);
+    for (;;) {  // re-read the granules whose tag is not this call's yet (bounded)
+      bool ok = true;
+#pragma unroll
+      for (int p = 0; p < FAR_MAX_RANKS; ++p) ok &= (unsigned)(x[p] >> 32) == seq;
+      if (ok || failed) break;
       if (wall_clock64() - t0 > fa.spin_ticks) {
         atomicOr(fa.err, 1);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int p = 0; p < FAR_MAX_RANKS; ++p)
+        if (p < fa.world && (unsigned)(x[p] >> 32) != seq)
+          x[p] = __hip_atomic_load(data(fa.base[fa.rank], fa.max_bytes, parity, p) + off,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-  }
-  __builtin_amdgcn_wave_barrier();
-  // 4. h += sum in rank order (identical on every rank, = the unfused kernel's formula)
-  for (int c = lane; c < nch; c += 64) {
-    const int m = c >> 1, hf = c & 1;
-    const size_t off = (size_t)m * ldh + col0 + hf * 8;
-    bf16x8* hp = reinterpret_cast<bf16x8*>(h + off);
-    const bf16x8 hv = *hp;
-    float acc[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = (float)hv[j];
-    for (int p = 0; p < fa.world; ++p) {
-      const v4u raw = __builtin_nontemporal_load(
-          reinterpret_cast<const v4u*>(data(fa.base[fa.rank], fa.max_bytes, parity, p) + off));
-      bf16x8 pv;
-      __builtin_memcpy(&pv, &raw, 16);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += (float)pv[j];
+    for (int p = 0; p < FAR_MAX_RANKS; ++p) {  // fixed rank order: identical sums on every rank
+      if (p < fa.world) {
+        a0 += bits_bf16((unsigned)x[p] & 0xffff);
+        a1 += bits_bf16(((unsigned)x[p] >> 16) & 0xffff);
+      }
     }
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
-    *hp = o;
+    *hp = bf16_bits(a0) | (bf16_bits(a1) << 16);
   }
   if (lane == 0) fa.counters[blk] = seq;
   if (blk == 0)  // keep the counters of blocks a narrower call does not launch in step

@@ -1,0 +1,9 @@
+// Skinny GEMM instantiations for EPI_QKV_ROPE (see skinny_gemm_impl.h).
+#include "skinny_gemm_impl.h"
+
+int skinny_unit_qkv_rope(SKINNY_UNIT_ARGS) {
+  const EpiArgs& ea = *static_cast<const EpiArgs*>(ea_p);
+  if (norm)
+    return launch_e<EPI_QKV_ROPE, true>(mt, waves, Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+  return (int)hipErrorInvalidValue;
+}

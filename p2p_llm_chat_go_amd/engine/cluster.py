@@ -58,12 +58,21 @@ def _free_port() -> int:
 class LockstepEngine:
     """The leader's view of its engine group: every call that runs collectives is
     broadcast to the followers first (plan over the host pipes), then run locally.
-    Everything else (cfg, kv, limits) is the local engine's."""
+    Everything else (cfg, kv, limits) is the local engine's.
 
-    def __init__(self, engine, follower_conns):
+    ``dp_split`` (EP ``a2a`` mode: DP attention + expert all-to-all): each sequence lives
+    on ONE rank (its home: first KV page id mod world), so the group serves world x the
+    sequences of a replicated-attention group.  A prefill / decode call is split by home;
+    every rank runs its share padded to the group's largest share (equal row counts and
+    chunking, as the static-capacity all-to-all needs), followers send their tokens back
+    over the pipe, and the leader reassembles them in call order."""
+
+    def __init__(self, engine, follower_conns, dp_split: bool = False):
         self._eng = engine
         self._conns = list(follower_conns)
         self._lock = threading.Lock()
+        self.dp_split = dp_split
+        self.world = 1 + len(self._conns)
 
     def __getattr__(self, name):
         return getattr(self._eng, name)
@@ -80,8 +89,82 @@ class LockstepEngine:
             if p is not None and not p.greedy:
                 p.resolved_seed()
 
+    # ------------------------------------------------------------ dp_split
+    def _parts(self, block_tables):
+        homes = [bt[0] % self.world for bt in block_tables]
+        return [[b for b, h in enumerate(homes) if h == r] for r in range(self.world)]
+
+    @staticmethod
+    def _sub(xs, idx):
+        return None if xs is None else [xs[i] for i in idx]
+
+    def _recv(self, c):
+        try:
+            msg = c.recv()
+        except (EOFError, OSError):
+            raise RuntimeError("peer rank is dead (pipe closed)")
+        if msg[0] == "dead":
+            raise RuntimeError("peer rank is dead: %s" % (msg[1].strip().splitlines()[-1:],))
+        return msg[1]
+
+    def _prefill_split(self, prompts, block_tables, return_logits, sampling, starts):
+        parts = self._parts(block_tables)
+        rows = [sum(len(prompts[b]) - (starts[b] if starts else 0) for b in part)
+                for part in parts]
+        pad = max(1, max(rows))
+        for k, c in enumerate(self._conns, start=1):
+            idx = parts[k]
+            c.send(("prefill_part", self._sub(prompts, idx), self._sub(block_tables, idx),
+                    return_logits, self._sub(sampling, idx), self._sub(starts, idx), pad))
+        idx = parts[0]
+        mine = self._eng.prefill(self._sub(prompts, idx), self._sub(block_tables, idx),
+                                 return_logits=return_logits, sampling=self._sub(sampling, idx),
+                                 starts=self._sub(starts, idx), pad_rows=pad)
+        results = [mine] + [self._recv(c) for c in self._conns]
+        import torch
+
+        dev = self._eng.device
+        first = torch.zeros(len(prompts), dtype=torch.int32)
+        logits = None
+        for part, res in zip(parts, results):
+            if return_logits:
+                toks, lg = res
+                if logits is None:
+                    logits = torch.zeros(len(prompts), lg.shape[1], dtype=torch.float32)
+                if part:
+                    logits[part] = lg.float().cpu()
+            else:
+                toks = res
+            if part:
+                first[part] = toks.cpu() if hasattr(toks, "cpu") else torch.tensor(toks)
+        first = first.to(dev)
+        return (first, logits.to(dev)) if return_logits else first
+
+    def _decode_split(self, last_ids, pos, block_tables, ctx, k, params):
+        parts = self._parts(block_tables)
+        bmax = max(1, max(len(p) for p in parts))
+        for r, c in enumerate(self._conns, start=1):
+            idx = parts[r]
+            c.send(("decode_part", self._sub(last_ids, idx), self._sub(pos, idx),
+                    self._sub(block_tables, idx), ctx, k, self._sub(params, idx), bmax))
+        idx = parts[0]
+        mine = self._eng.decode_steps(self._sub(last_ids, idx), self._sub(pos, idx),
+                                      self._sub(block_tables, idx), ctx, k,
+                                      self._sub(params, idx), batch_bucket=bmax)
+        results = [mine] + [self._recv(c) for c in self._conns]
+        hist = [None] * len(last_ids)
+        for part, res in zip(parts, results):
+            for b, h in zip(part, res):
+                hist[b] = h
+        return hist
+
+    # ------------------------------------------------------------ engine calls
     def prefill(self, prompts, block_tables, return_logits=False, sampling=None, starts=None):
         self._resolve(sampling)
+        if self.dp_split:
+            with self._lock:
+                return self._prefill_split(prompts, block_tables, return_logits, sampling,
+                                           starts)
         with self._lock:
             self._bcast(("prefill", prompts, block_tables, return_logits, sampling, starts))
             return self._eng.prefill(prompts, block_tables, return_logits=return_logits,
@@ -89,14 +172,65 @@ class LockstepEngine:
 
     def decode_steps(self, last_ids, pos, block_tables, ctx, k, params=None):
         self._resolve(params)
+        if self.dp_split:
+            with self._lock:
+                return self._decode_split(last_ids, pos, block_tables, ctx, k, params)
         with self._lock:
             self._bcast(("decode", last_ids, pos, block_tables, ctx, k, params))
             return self._eng.decode_steps(last_ids, pos, block_tables, ctx, k, params)
 
     def generate(self, prompts, max_new_tokens=64, stop_on_eos=True, check_every=8):
+        if self.dp_split:
+            return self._generate_split(prompts, max_new_tokens, stop_on_eos, check_every)
         with self._lock:
             self._bcast(("generate", prompts, max_new_tokens, stop_on_eos, check_every))
             return self._eng.generate(prompts, max_new_tokens, stop_on_eos, check_every)
+
+    def _generate_split(self, prompts, max_new_tokens, stop_on_eos, check_every):
+        """Static-batch generate over the split calls (bench / tests; the server drives
+        prefill / decode_steps itself)."""
+        import time
+
+        from .engine import GenResult
+        from .kv_cache import pages_for
+
+        eng = self._eng
+        t0 = time.perf_counter_ns()
+        pages = [eng.kv.allocator.alloc(pages_for(len(p) + max_new_tokens)) for p in prompts]
+        try:
+            first = self.prefill(prompts, pages).cpu().tolist()
+            t1 = time.perf_counter_ns()
+            out = [[int(t)] for t in first]
+            eos = set(eng.cfg.eos_ids)
+            while len(out[0]) < max_new_tokens:
+                live = [b for b in range(len(prompts))
+                        if not (stop_on_eos and any(t in eos for t in out[b]))]
+                if not live:
+                    break
+                k = min(check_every, max_new_tokens - len(out[0]))
+                hist = self.decode_steps([out[b][-1] for b in range(len(prompts))],
+                                         [len(prompts[b]) + len(out[b]) - 1
+                                          for b in range(len(prompts))],
+                                         pages, max(len(p) for p in prompts) + max_new_tokens, k)
+                for b in range(len(prompts)):
+                    out[b] += [int(t) for t in hist[b]]
+            t2 = time.perf_counter_ns()
+        finally:
+            for p in pages:
+                eng.kv.allocator.free(p)
+        res = []
+        for b, p in enumerate(prompts):
+            toks, reason = out[b][:max_new_tokens], "length"
+            if stop_on_eos:
+                for j, t in enumerate(toks):
+                    if t in eng.cfg.eos_ids:
+                        toks, reason = toks[:j], "stop"
+                        break
+            res.append(GenResult(tokens=toks, prompt_eval_count=len(p),
+                                 prompt_eval_duration_ns=t1 - t0, eval_count=len(toks),
+                                 eval_duration_ns=t2 - t1, total_duration_ns=t2 - t0,
+                                 ttft_ns=t1 - t0, done_reason=reason))
+        return res
 
     def stop(self):
         for c in self._conns:
@@ -124,6 +258,16 @@ def _follower_loop(eng, conn):
         elif op == "generate":
             _, prompts, n, eos, every = msg
             eng.generate(prompts, n, eos, every)
+        elif op == "prefill_part":  # dp_split: this rank's share, result back to the leader
+            _, prompts, bts, ret, sampling, starts, pad = msg
+            res = eng.prefill(prompts, bts, return_logits=ret, sampling=sampling, starts=starts,
+                              pad_rows=pad)
+            res = (res[0].cpu(), res[1].cpu()) if ret else res.cpu()
+            conn.send(("part", res))
+        elif op == "decode_part":
+            _, ids, pos, bts, ctx, k, params, bmax = msg
+            conn.send(("part", eng.decode_steps(ids, pos, bts, ctx, k, params,
+                                                batch_bucket=bmax)))
         if eng.device.type == "cuda":
             import torch
 
@@ -214,7 +358,8 @@ def _leader_main(spec, replica, eng, parent_conn, follower_conns):
     from .tokenizer import get_tokenizer
 
     group = spec.get("tp", 1) * spec.get("ep", 1)
-    front = LockstepEngine(eng, follower_conns) if group > 1 else eng
+    split = spec.get("ep", 1) > 1 and spec.get("ep_mode", "allreduce") == "a2a"
+    front = LockstepEngine(eng, follower_conns, dp_split=split) if group > 1 else eng
     server = EngineServer(front, get_tokenizer(eng.cfg, spec.get("tokenizer")
                                                or spec.get("checkpoint")),
                           model_name=spec.get("model_name", "llama3.1"),
@@ -342,6 +487,28 @@ class ClusterServer:
         for rep in self._replicas:
             threading.Thread(target=self._reader, args=(rep,), daemon=True,
                              name="replica-%d-reader" % rep.idx).start()
+            threading.Thread(target=self._monitor, args=(rep,), daemon=True,
+                             name="replica-%d-monitor" % rep.idx).start()
+
+    def _monitor(self, rep: _Replica):
+        """A rank process that exits breaks its group: fail the replica's requests now
+        and end its other ranks, instead of waiting for a collective to time out (RCCL
+        paths -- prefill sums, all-to-alls -- would hang until the process-group timeout)."""
+        from multiprocessing.connection import wait
+
+        live = {p.sentinel: (k, p) for k, p in enumerate(rep.procs)}
+        while live and not self._closed:
+            ready = wait(list(live), timeout=1.0)
+            for s in ready:
+                k, p = live.pop(s)
+                if self._closed:
+                    return
+                why = "rank %d exited with code %s" % (k, p.exitcode)
+                self._mark_dead(rep, why)
+                for q in rep.procs:
+                    if q.is_alive():
+                        q.terminate()
+                return
 
     # ------------------------------------------------------------ plumbing
     def _reader(self, rep: _Replica):

@@ -163,7 +163,8 @@ class Engine:
 
     # -------------------------------------------------------------- prefill
     def prefill(self, prompts: list, block_tables: list, return_logits: bool = False,
-                sampling: list | None = None, starts: list | None = None):
+                sampling: list | None = None, starts: list | None = None,
+                pad_rows: int | None = None):
         """Run all prompts (flat rows, chunked at max_prefill_tokens).
 
         Returns int32 first tokens [B] on the device (and, with return_logits,
@@ -173,20 +174,29 @@ class Engine:
         starts: per sequence, the first position to run (the KV of earlier positions is
         already in its pages).  A running sequence rides along as one row (start =
         its last position): the server mixes decode rows into a prefill this way.
+        pad_rows: run exactly this many rows (>= the real ones), the rest dummy rows of an
+        extra sequence on the KV null page -- EP all-to-all ranks serving different
+        sequences (DP attention) must run the same chunks with equal row counts.
         """
         sampled = sampling is not None and not all(p.greedy for p in sampling)
         dev = self.device
         B = len(prompts)
-        max_ctx = max(len(p) for p in prompts)
-        ws = self.prefill_workspace(max_ctx)
-        max_pages = bucket(max_ctx, CTX_BUCKETS) // PAGE
-        bt = torch.zeros(B, max(max_pages, max(len(b) for b in block_tables)), dtype=torch.int32)
-        for b, pages in enumerate(block_tables):
-            bt[b, :len(pages)] = torch.tensor(pages, dtype=torch.int32)
         rows = []  # (seq, pos, token)
         for b, p in enumerate(prompts):
             s0 = starts[b] if starts else 0
             rows += [(b, i, p[i]) for i in range(s0, len(p))]
+        n_dummy = 0
+        if pad_rows is not None:
+            n_dummy = pad_rows - len(rows)
+            assert n_dummy >= 0, (pad_rows, len(rows))
+            rows += [(B, i, 0) for i in range(n_dummy)]  # sequence B: the null page
+        max_ctx = max([len(p) for p in prompts] + [n_dummy, 1])
+        ws = self.prefill_workspace(max_ctx)
+        max_pages = bucket(max_ctx, CTX_BUCKETS) // PAGE
+        bt = torch.zeros(B + (1 if n_dummy else 0),
+                         max([max_pages] + [len(b) for b in block_tables]), dtype=torch.int32)
+        for b, pages in enumerate(block_tables):
+            bt[b, :len(pages)] = torch.tensor(pages, dtype=torch.int32)
         first = torch.zeros(B, dtype=torch.int32, device=dev)
         all_logits = None
         if return_logits:
@@ -199,10 +209,12 @@ class Engine:
             pos = torch.tensor([r[1] for r in chunk], dtype=torch.int32)
             ids = torch.tensor([r[2] for r in chunk], dtype=torch.int32)
             slots = bt[seq.long(), (pos // PAGE).long()] * PAGE + pos % PAGE
+            if n_dummy:
+                slots[seq == B] = -1  # dummy rows write no KV
             # rows that end a sequence inside this chunk need logits
             outs, out_seq = [], []
             for j, (b, i, _t) in enumerate(chunk):
-                if i == len(prompts[b]) - 1:
+                if b < B and i == len(prompts[b]) - 1:
                     outs.append(j)
                     out_seq.append(b)
             greedy = all_logits is None and not sampled
@@ -255,14 +267,16 @@ class Engine:
 
     # --------------------------------------------------------------- decode
     def decode_steps(self, last_ids: list, pos: list, block_tables: list, ctx: int, k: int,
-                     params: list | None = None) -> list:
+                     params: list | None = None, batch_bucket: int | None = None) -> list:
         """k decode steps for running sequences (continuous batching): row b continues
         from token ``last_ids[b]`` at position ``pos[b]`` in its pages; ``params`` =
         per-row SamplingParams (None / all greedy: the fused-argmax graph).  Returns the
         k new tokens of every row (host lists).  Every TP/EP rank makes the same call
-        (engine.cluster broadcasts it), so the graphs' collectives line up."""
+        (engine.cluster broadcasts it), so the graphs' collectives line up.
+        batch_bucket: run the graph of this many rows (>= len(last_ids); DP-attention EP
+        ranks with different batches must replay the same bucket)."""
         greedy = params is None or all(p.greedy for p in params)
-        g = self.decode_graph(len(last_ids), ctx, greedy=greedy)
+        g = self.decode_graph(max(len(last_ids), batch_bucket or 1), ctx, greedy=greedy)
         st = g.state
         st.load(last_ids, pos, block_tables)
         if greedy:

@@ -55,9 +55,12 @@ class CustomAllReduce:
         # bytes and the one-shot has one hop less)
         self.two_shot_min = int(os.environ.get("P2P_CAR_2SHOT_MIN", str(512 << 10)))
         L = self.L = _lib.lib()
-        # partials of the fused row-parallel epilogue (ops.skinny_gemm_ar): up to 64 rows of
-        # a 16384-wide hidden state per call
-        self.far_max_bytes = int(os.environ.get("P2P_FAR_MAX_BYTES", str(2 << 20)))
+        tmo = int(os.environ.get("P2P_CAR_TIMEOUT_MS", "0"))
+        if tmo > 0:  # spin bound of every one-shot / fused call (default 5 s)
+            self.set_timeout_ms(tmo)
+        # partials of the fused row-parallel epilogue (ops.skinny_gemm_ar), as 8-byte tagged
+        # granules of two bf16 (4 bytes per element): up to 64 rows of a 16384-wide state
+        self.far_max_bytes = int(os.environ.get("P2P_FAR_MAX_BYTES", str(4 << 20)))
         self._opened = []
         self._owned = []
         with torch.cuda.device(self.device):
@@ -154,7 +157,7 @@ class CustomAllReduce:
         """Can ops.skinny_gemm_ar sum an [M, N] partial (row stride ld) through the fused
         buffer?"""
         return 1 <= M <= 64 and N % 16 == 0 and N // 16 <= 1024 and ld % 8 == 0 and \
-            ((M - 1) * ld + N) * 2 <= self.far_max_bytes
+            ((M - 1) * ld + N) * 4 <= self.far_max_bytes
 
     def close(self):
         if not self._owned:

@@ -166,7 +166,7 @@ def test_tp_node_suggest_over_http(tmp_path):
         sug = json.loads(body)["suggestion"]
         from p2p_llm_chat_go_amd.engine.tokenizer import suggest_prompt
 
-        # (same request order: the synthetic tokenizer's decode table grows as it encodes)
+        # (synthetic decoding is a pure function of the ids: any request order)
         ref = _reference("tiny-llama-gqa", [_req({"temperature": 0, "num_predict": 8},
                                                  prompt=suggest_prompt(MSG)), REQS[0]])
         assert sug == ref[0]
@@ -174,3 +174,28 @@ def test_tp_node_suggest_over_http(tmp_path):
         assert st == 200 and json.loads(body)["response"] == ref[1]
     finally:
         procs.close()
+
+
+def test_ep_a2a_cluster_dp_split_matches_single_engine():
+    """ENGINE_EP_MODE=a2a behind the node: DP attention (each sequence lives on one rank,
+    chosen by its first KV page) + expert all-to-all over 8 gloo ranks.  Concurrent
+    requests land on different ranks; every reply equals the single engine's."""
+    torch.set_num_threads(1)
+    reqs = [REQS[0], REQS[2], _req({"temperature": 0, "num_predict": 7}, prompt="Happy birthday!!"),
+            REQS[1], REQS[0]]
+    ref = _reference("tiny-mixtral-8e", reqs)
+    cs = ClusterServer("tiny-mixtral-8e", gpus=8, ep=8, device="cpu", sd_seed=SEED,
+                       warmup=False, ep_mode="a2a")
+    try:
+        out = [None] * len(reqs)
+
+        def go(i):
+            out[i] = json.loads(cs.handle_json(reqs[i]))["response"]
+
+        ts = [threading.Thread(target=go, args=(i,)) for i in range(len(reqs))]
+        [t.start() for t in ts]
+        [t.join(300) for t in ts]
+        assert out == ref
+        assert json.loads(cs.handle_json(REQS[2]))["response"] == ref[1]  # one sequence only
+    finally:
+        cs.close()

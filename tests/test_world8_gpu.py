@@ -56,7 +56,10 @@ def _check_logits(got, ref, what):
 
 
 def _worker(rank, world, port, q, kind, mode, env):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **env)
+    # 8 processes time-share one device: a rank's kernel can wait on a peer whose queue is
+    # not scheduled yet, so the spin bound is generous here (5 s on real GPUs)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), P2P_CAR_TIMEOUT_MS="30000",
+                      **env)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     WORLD = world
     try:
@@ -76,15 +79,18 @@ def _worker(rank, world, port, q, kind, mode, env):
         full_w = EngineWeights.from_state_dict(sd, cfg, "cuda") if rank == 0 else None
         del sd
         torch.cuda.empty_cache()
+        # a2a over gloo moves host memory (RCCL refuses 2+ ranks on one device): eager decode
+        graphs = mode != "a2a"
         eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_batch=2, comm=TPComm(),
-                     tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=True,
+                     tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=graphs,
                      ep_mode=mode if moe else "allreduce")
         prompts = _prompts(rank, per_rank=(mode == "a2a"))
         n_new = 8
         res = eng.generate(prompts, n_new, stop_on_eos=False)
         toks = [r.tokens for r in res]
         gs = list(eng._graphs.values())
-        assert gs and all(g.graph is not None for g in gs), "decode graph not captured at world 8"
+        assert not graphs or (gs and all(g.graph is not None for g in gs)), \
+            "decode graph not captured at world %d" % WORLD
         toks2 = [r.tokens for r in eng.generate(prompts, n_new, stop_on_eos=False)]  # replays
         assert toks2 == toks, ("graph replay changed the tokens", toks, toks2)
         # prefill logits (TP: the rank's vocab shard; EP: full vocab on every rank)
