@@ -16,7 +16,7 @@ from kernel_bench import graph_time  # noqa: E402
 
 def main():
     from p2p_llm_chat_go_amd.ops import _lib
-    L = _lib.lib()
+    L = _lib.experimental()
     Hq, Hkv, H = 32, 8, 4096
     for R, ctx_len in ((1, 50), (1, 100), (1, 250), (2, 100), (4, 100), (8, 100), (16, 200)):
         P = 1 + R * 4

@@ -17,7 +17,7 @@ from kernel_bench import graph_time  # noqa: E402
 
 
 def main():
-    L = _lib.lib()
+    L = _lib.experimental()  # csrc/experimental (built with --only experimental)
     fn = L.p2p_launch_probe
     fn.argtypes = [ctypes.c_int] * 4 + [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_void_p]

@@ -1,4 +1,4 @@
-"""Feasibility probe for a persistent batch-1 decode layer (csrc/kernels/persist_probe.hip):
+"""Feasibility probe for a persistent batch-1 decode layer (csrc/experimental/persist_probe.hip):
 the 8B layer's weight bytes (qkv 50.3 MB, attention stand-in, o_proj 33.5, gate_up 234.9,
 down 117.4) streamed as 5 launches per layer (graph) vs ONE launch for all 32 layers with
 grid barriers, with and without an LDS-DMA prefetch of each workgroup's next-phase slice
@@ -15,7 +15,7 @@ from p2p_llm_chat_go_amd.ops import _lib  # noqa: E402
 
 
 def main():
-    L = _lib.lib()
+    L = _lib.experimental()  # csrc/experimental (built with --only experimental)
     fn = L.p2p_persist_probe
     fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                    ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -53,12 +53,24 @@ def _headers(d):
     return glob.glob(os.path.join(d, "*.h")) + glob.glob(os.path.join(CSRC, "include", "*.h"))
 
 
-def build_kernels(force=False, jobs=8):
-    """Compile csrc/kernels/*.hip for gfx950 into one shared library (C ABI, ctypes)."""
+EXPERIMENTAL_LIB = os.path.join(LIBDIR, "libp2p_experimental.so")
+
+
+def build_kernels(force=False, jobs=8, experimental=False):
+    """Compile csrc/kernels/*.hip for gfx950 into one shared library (C ABI, ctypes).
+
+    experimental=True builds csrc/experimental/*.hip (measured-negative fusions and
+    hardware probes kept for the record and their benches) into a separate
+    ``libp2p_experimental.so`` instead; no default engine path loads it."""
     kdir = os.path.join(CSRC, "kernels")
+    out_lib = KERNEL_LIB
     srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")))
     hdrs = _headers(kdir)
     odir = os.path.join(BUILDDIR, "kernels")
+    if experimental:
+        srcs = sorted(glob.glob(os.path.join(CSRC, "experimental", "*.hip")))
+        odir = os.path.join(BUILDDIR, "experimental")
+        out_lib = EXPERIMENTAL_LIB
     os.makedirs(odir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     flags = [
@@ -75,9 +87,17 @@ def build_kernels(force=False, jobs=8):
         futs = [ex.submit(_run, [HIPCC] + flags + ["-c", s, "-o", o]) for s, o in todo]
         for f in futs:
             f.result()
-    if force or todo or _stale(KERNEL_LIB, objs):
-        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=%s" % ARCH] + objs + ["-o", KERNEL_LIB])
-    return KERNEL_LIB
+    # a source removed from the directory leaves its object behind: relink from the
+    # current source list whenever the library holds objects it should not
+    listed = out_lib + ".objs"
+    prev = open(listed).read().split("\n") if os.path.exists(listed) else None
+    if prev != objs and os.path.exists(out_lib):
+        os.remove(out_lib)
+    if force or todo or _stale(out_lib, objs):
+        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=%s" % ARCH] + objs + ["-o", out_lib])
+        with open(listed, "w") as f:
+            f.write("\n".join(objs))
+    return out_lib
 
 
 def _py_ext_suffix():
@@ -200,11 +220,16 @@ def build_sanitized(kind: str, force=False, jobs=8):
     return outs
 
 
-def build(force=False, jobs=8, only=None):
+def build(force=False, jobs=8, only=None, experimental=None):
     outs = []
-    if only in (None, "kernels"):
+    if experimental is None:
+        experimental = os.environ.get("P2P_BUILD_EXPERIMENTAL", "0") == "1"
+    if only in (None, "kernels", "experimental"):
         if shutil.which(HIPCC) or os.path.exists(HIPCC):
-            outs.append(build_kernels(force, jobs))
+            if only != "experimental":
+                outs.append(build_kernels(force, jobs))
+            if experimental or only == "experimental":
+                outs.append(build_kernels(force, jobs, experimental=True))
         else:
             print("hipcc not found; skipping HIP kernels", file=sys.stderr)
     if only in (None, "native"):
@@ -216,7 +241,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
-    ap.add_argument("--only", choices=["kernels", "native"], default=None)
+    ap.add_argument("--only", choices=["kernels", "native", "experimental"], default=None)
     ap.add_argument("--sanitize", choices=sorted(SANITIZERS), default=None,
                     help="build only the sanitizer variant of the daemons into bin/<kind>/")
     a = ap.parse_args(argv)

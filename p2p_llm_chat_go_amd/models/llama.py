@@ -60,7 +60,8 @@ class Workspace:
         self.sync = torch.zeros(2, device=dev, dtype=torch.int32)
         # head-split attention + o_proj (ops.attn_oproj_heads): fp32 partial slab + tickets
         self.heads_slab = self.heads_tickets = None
-        if dev.type == "cuda" and tp_size == 1 and cfg.hidden % ops.attention.HEADS_COLS == 0:
+        if (dev.type == "cuda" and tp_size == 1 and cfg.hidden % ops.attention.HEADS_COLS == 0
+                and os.environ.get("P2P_FUSED_ATTN_OPROJ", "0") == "heads"):  # experimental lib
             rows = min(max_rows, ops.attention.HEADS_MAX_ROWS)
             self.heads_slab, self.heads_tickets = ops.attn_oproj_heads_workspace(
                 rows, nkv, cfg.hidden, dev)
@@ -88,7 +89,8 @@ class LlamaModel:
         # the last head of each column block sums the partials -- for decode batches of
         # <= P2P_HEADS_MAX_ROWS rows at contexts <= 256.  Also measured slower (16.9 vs
         # 14.5 us at batch 1, profiles/r2_attn_oproj_heads_negative.jsonl: the 8-way fan-in
-        # tail ~4 us); "1": the hand-off kernel above; "0" (default): two kernels.
+        # tail ~4 us); "1": the hand-off kernel above; "0" (default): two kernels.  Both fused
+        # kernels live in the opt-in experimental library (csrc/experimental).
         mode = os.environ.get("P2P_FUSED_ATTN_OPROJ", "0")
         self.fuse_attn_oproj = mode == "1"
         self.fuse_heads = mode == "heads"

@@ -168,6 +168,37 @@ def lib():
         return _lib
 
 
+_EXP_PATH = os.path.join(os.path.dirname(_LIB_PATH), "libp2p_experimental.so")
+_exp = None
+
+# experimental library (csrc/experimental: measured-negative fusions, hardware probes)
+_EXP_SIGS = ("p2p_attn_oproj", "p2p_attn_oproj_heads", "p2p_attn_oproj_heads_tune",
+             "p2p_l3_prefetch")
+
+
+def experimental():
+    """The opt-in library of measured-negative kernels and probes (built by
+    ``python -m p2p_llm_chat_go_amd._build --only experimental``); raises if absent."""
+    global _exp
+    if _exp is not None:
+        return _exp
+    lib()  # the main library first (same HIP runtime)
+    with _lock:
+        if _exp is None:
+            if not os.path.exists(_EXP_PATH):
+                raise KernelError(
+                    "experimental kernel library missing at %s -- build it with "
+                    "`python -m p2p_llm_chat_go_amd._build --only experimental`" % _EXP_PATH)
+            L = ctypes.CDLL(_EXP_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name in _EXP_SIGS:
+                fn = getattr(L, name, None)
+                if fn is not None:
+                    fn.argtypes = _SIGS[name]
+                    fn.restype = c_int
+            _exp = L
+    return _exp
+
+
 def available() -> bool:
     try:
         lib()

@@ -109,7 +109,7 @@ def attn_oproj(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_k
         paged_attention(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_heads, n_kv,
                         max_ctx, out=attn, scale=scale)
         return skinny_gemm(wo, attn, EPI_RESID, out=h)
-    L = _lib.lib()
+    L = _lib.experimental()
     _lib.check(L.p2p_attn_oproj(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                 block_tables.data_ptr(), block_tables.stride(0), row_bt.data_ptr(),
                                 ctx_lens.data_ptr(), R, n_heads, n_kv, HEAD_DIM, float(scale),
@@ -157,7 +157,7 @@ def attn_oproj_heads(q, k_cache, v_cache, block_tables, row_bt, ctx_lens, n_head
         return skinny_gemm(wo, a, EPI_RESID, out=h)
     if slab.numel() < n_kv * R * N or tickets.numel() < N // HEADS_COLS:
         raise ValueError("attn_oproj_heads: workspace too small")
-    L = _lib.lib()
+    L = _lib.experimental()
     _lib.check(L.p2p_attn_oproj_heads(
         q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
         block_tables.stride(0), _lib.ptr(row_bt), ctx_lens.data_ptr(), R, n_heads, n_kv, HEAD_DIM,

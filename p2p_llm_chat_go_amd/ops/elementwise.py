@@ -35,7 +35,7 @@ def l3_prefetch(t: torch.Tensor, nbytes: int | None = None, grid: int = 0):
     sink = _SINKS.get(t.device)
     if sink is None:
         sink = _SINKS[t.device] = torch.zeros(256 * 4, dtype=torch.int32, device=t.device)
-    L = _lib.lib()
+    L = _lib.experimental()
     _lib.check(L.p2p_l3_prefetch(t.data_ptr(), n, grid, sink.data_ptr(),
                                  _lib.stream_ptr(t.device)), "l3_prefetch")
 
