@@ -88,6 +88,8 @@ def main():
         "ttft_p50_ms": round(statistics.median(ttft), 3),
         "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
         "mean_batch": round(toks / max(steps, 1), 2), "mixed": bool(a.mixed), "dtype": "bf16",
+        "engine_time_s": {k: round(srv.stats[k] - occ0[k], 4) for k in
+                          ("busy_s", "prefill_s", "decode_s", "prefill_calls", "decode_calls")},
         "data": "synthetic chat prompts, random-init weights"}), flush=True)
 
 

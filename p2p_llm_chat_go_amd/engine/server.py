@@ -17,6 +17,7 @@ serves one blocking request per click, `web/streamlit_app.py:163-165`).
 from __future__ import annotations
 
 import json
+import os
 import threading
 import time
 from concurrent.futures import Future
@@ -60,6 +61,10 @@ class EngineServer:
         # a prefill step also advances every running sequence by one token (its row rides
         # in the prefill batch): admissions no longer stall the running batch for a step
         self.mixed = mixed
+        # after a reply finishes, wait up to this long for the next request before the next
+        # step (closed-loop peers resubmit at once; a free slot left for a whole decode
+        # chunk costs batch occupancy): ENGINE_ADMIT_WAIT_US, default 500 us
+        self.admit_wait_s = float(os.environ.get("ENGINE_ADMIT_WAIT_US", "500")) * 1e-6
         self.default_max_tokens = default_max_tokens
         self.max_ctx = max_ctx or min(engine.cfg.max_pos, CTX_BUCKETS[-1],
                                       engine.kv.num_pages * 64)
@@ -76,7 +81,8 @@ class EngineServer:
         self._dead = None
         self.errors = 0
         self.stats = {"requests": 0, "tokens": 0, "prefill_tokens": 0, "decode_steps": 0,
-                      "busy_s": 0.0}
+                      "busy_s": 0.0, "prefill_s": 0.0, "decode_s": 0.0, "prefill_calls": 0,
+                      "decode_calls": 0}
         self._thread = threading.Thread(target=self._loop, name="engine-loop", daemon=True)
         self._thread.start()
 
@@ -323,6 +329,8 @@ class EngineServer:
                                     starts=starts if ride else None).cpu().tolist()
             eng.check_comm()
             t1 = time.perf_counter_ns()
+            self.stats["prefill_s"] += (t1 - t0) * 1e-9
+            self.stats["prefill_calls"] += 1
             self.stats["prefill_tokens"] += sum(len(self._reqs[i]["prompt"]) for i in plan.prefill)
             for i, tkn in zip(plan.prefill, first):
                 self._reqs[i]["t_first"] = t1
@@ -335,7 +343,13 @@ class EngineServer:
                    if self.sched.get(i).state == 1]
         if running:
             self._decode(eng, running)
-        self._retire()
+        if self._retire() and self.admit_wait_s > 0:
+            # a reply just went out: its peer (or a queued client) usually sends the next
+            # request within a fraction of a millisecond -- admit it at THIS step boundary
+            # instead of leaving its batch slot idle for a whole decode chunk
+            with self._lock:
+                if not self._pending and not self._stop:
+                    self._lock.wait(timeout=self.admit_wait_s)
 
     def _decode(self, eng: Engine, running: list):
         reqs = [self.sched.get(i) for i in running]
@@ -343,17 +357,29 @@ class EngineServer:
         ctx = max(r.prompt_len + r.max_new for r in reqs)
         remaining = min(r.max_new - len(r.tokens) for r in reqs)
         waiting = self.sched.n_waiting + len(self._pending)
-        k = max(1, min(self.decode_chunk if not waiting else 2, remaining))
+        # chunk length: long chunks amortise the host round trip; a waiting request or a
+        # free batch slot (a request may arrive any moment) shortens it to bound TTFT
+        chunk = self.decode_chunk
+        if waiting:
+            chunk = 2
+        elif len(running) < self.max_batch:
+            chunk = max(2, self.decode_chunk // 2)
+        k = max(1, min(chunk, remaining))
+        t0 = time.perf_counter()
         with span("server.decode", batch=len(running), steps=k):
             hist = eng.decode_steps([r.tokens[-1] for r in reqs], [r.pos for r in reqs],
                                     [list(r.pages) for r in reqs], ctx, k, params)
+        self.stats["decode_s"] += time.perf_counter() - t0
+        self.stats["decode_calls"] += 1
         self.stats["decode_steps"] += k
         self.sched.on_decode_tokens(running, hist)
         self._stream(running)
 
-    def _retire(self):
+    def _retire(self) -> int:
         now = time.perf_counter_ns()
+        done = 0
         for rid in self.sched.take_finished():
+            done += 1
             self._stream([rid])
             r = self._reqs.pop(rid, None)
             sr = self.sched.get(rid)
@@ -370,3 +396,4 @@ class EngineServer:
                     "total_duration": now - r["t_submit"],
                     "ttft_ns": t_first - r["t_submit"]})
             self.sched.release(rid)
+        return done

@@ -89,10 +89,12 @@ def reference_forward(sd: dict, cfg: ModelConfig, tokens: torch.Tensor) -> torch
     T = tokens.shape[0]
     H, D, nh, nkv = cfg.hidden, cfg.head_dim, cfg.n_heads, cfg.n_kv_heads
     G = nh // nkv
-    cs = rope_table(cfg, max_pos=T)
+    dev = sd["model.embed_tokens.weight"].device  # runs where the checkpoint lives
+    tokens = tokens.to(dev)
+    cs = rope_table(cfg, max_pos=T, device=dev)
     cos, sin = cs[..., 0][:, None, :], cs[..., 1][:, None, :]
     x = sd["model.embed_tokens.weight"].float()[tokens.long()]
-    mask = torch.full((T, T), float("-inf")).triu(1)
+    mask = torch.full((T, T), float("-inf"), device=dev).triu(1)
     for i in range(cfg.n_layers):
         p = "model.layers.%d." % i
         h = _rms(x, sd[p + "input_layernorm.weight"], cfg.eps)
