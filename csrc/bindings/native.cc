@@ -15,6 +15,7 @@
 #include "net/quic.h"
 #include "net/tls.h"
 #include "net/relay.h"
+#include "net/yamux.h"
 #include "runtime/scheduler.h"
 
 namespace py = pybind11;
@@ -226,6 +227,43 @@ std::tuple<bool, uint64_t, long, uint64_t, uint64_t> quic_echo(const std::string
 
 }  // namespace
 
+namespace {
+// In-memory connection for wire fixtures: reads come from a script (then EOF), writes
+// are recorded byte for byte.
+class MemConn : public Conn {
+ public:
+  explicit MemConn(Bytes script) : in_(std::move(script)) {}
+  using Conn::write_all;
+  size_t read_some(uint8_t* buf, size_t n) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    const size_t k = std::min(n, in_.size() - pos_);
+    std::copy(in_.begin() + pos_, in_.begin() + pos_ + k, buf);
+    pos_ += k;
+    return k;
+  }
+  void write_all(const uint8_t* buf, size_t n) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    out_.insert(out_.end(), buf, buf + n);
+  }
+  void close() override {}
+  Bytes written() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return out_;
+  }
+
+ private:
+  std::mutex mu_;
+  Bytes in_, out_;
+  size_t pos_ = 0;
+};
+
+Bytes ms_line(const std::string& s) {
+  Bytes b = uvarint(s.size() + 1);
+  append(b, s + "\n");
+  return b;
+}
+}  // namespace
+
 static p2p::Bytes hexb(const std::string& h) {
   p2p::Bytes b;
   for (size_t i = 0; i + 1 < h.size(); i += 2) b.push_back((uint8_t)std::stoi(h.substr(i, 2), nullptr, 16));
@@ -288,6 +326,56 @@ PYBIND11_MODULE(_native, m) {
     return quic_echo(kt, in, drop, streams, ku_interval);
   }, py::arg("key_type"), py::arg("payload"), py::arg("drop_rate") = 0.0, py::arg("streams") = 1,
      py::arg("key_update_interval") = 0);
+  // ---- wire fixtures: the exact bytes our implementation puts on the wire ----
+  m.def("wire_ms_select", [](const std::string& proto) {
+    // dialer side of multistream-select 1.0 (header + proposal pipelined), peer accepts
+    Bytes script = ms_line(kMultistreamProto);
+    append(script, ms_line(proto));
+    auto mc = std::make_shared<MemConn>(script);
+    BufConn bc(mc);
+    ms_select(bc, proto);
+    return B(mc->written());
+  });
+  m.def("wire_ms_handle", [](const std::vector<std::string>& proposals,
+                             const std::vector<std::string>& supported) {
+    // listener side: the dialer's header + proposals in order; returns what we answer
+    Bytes script = ms_line(kMultistreamProto);
+    for (auto& p : proposals) append(script, ms_line(p));
+    auto mc = std::make_shared<MemConn>(script);
+    BufConn bc(mc);
+    std::string chosen;
+    try {
+      chosen = ms_handle(bc, std::set<std::string>(supported.begin(), supported.end()));
+    } catch (const NetError&) {
+    }
+    return py::make_tuple(chosen, B(mc->written()));
+  });
+  m.def("wire_yamux_client_stream", [](const py::bytes& payload) {
+    // a dialer session opens stream 1, writes one message, half-closes (the chat send)
+    auto mc = std::make_shared<MemConn>(Bytes());
+    auto sess = std::make_shared<YamuxSession>(mc, true);
+    StreamPtr st = sess->open_stream();
+    st->write_all(U(payload));
+    st->close_write();
+    return B(mc->written());
+  });
+  m.def("noise_handshake_payload", [](const py::bytes& priv, const py::bytes& static_pub) {
+    return B(noise_handshake_payload(PrivateKey::unmarshal(U(priv)), U(static_pub)));
+  });
+  m.def("relay_voucher", [](const py::bytes& priv, const std::string& relay,
+                            const std::string& peer, uint64_t expire) {
+    return B(test_make_voucher(PrivateKey::unmarshal(U(priv)), PeerId::decode(relay),
+                               PeerId::decode(peer), expire));
+  });
+  m.def("relay_voucher_verify", [](const py::bytes& env, const std::string& relay,
+                                   const std::string& peer, uint64_t expire) {
+    try {
+      verify_voucher(U(env), PeerId::decode(relay), PeerId::decode(peer), expire);
+      return true;
+    } catch (const NetError&) {
+      return false;
+    }
+  });
   m.def("relay_voucher_check", []() {
     // {good voucher verifies, wrong peer rejected, wrong expiry rejected, foreign signer
     // rejected, tampered signature rejected}

@@ -424,6 +424,10 @@ PublicKey verify_payload(const Bytes& payload, const Bytes& remote_static) {
 }
 }  // namespace
 
+Bytes noise_handshake_payload(const PrivateKey& id_key, const Bytes& static_pub) {
+  return make_payload(id_key, static_pub);
+}
+
 std::shared_ptr<NoiseConn> NoiseConn::handshake(ConnPtr c, const PrivateKey& id_key,
                                                 bool initiator, const PeerId& expected) {
   auto nc = std::shared_ptr<NoiseConn>(new NoiseConn());

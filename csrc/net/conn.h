@@ -121,6 +121,11 @@ std::string ms_handle(BufConn& c, const std::set<std::string>& protos);
 // libp2p Noise: Noise_XX_25519_ChaChaPoly_SHA256, empty prologue, signed
 // static-key payload ("noise-libp2p-static-key:" || static pub), 2-byte
 // big-endian frame lengths, stream muxer list in the payload extensions.
+// The libp2p Noise handshake payload (NoiseHandshakePayload protobuf: identity_key = 1,
+// identity_sig = 2 over "noise-libp2p-static-key:" || static_pub, extensions = 4 with the
+// early-muxer list) exactly as the handshake sends it; exposed for wire fixtures.
+Bytes noise_handshake_payload(const PrivateKey& id_key, const Bytes& static_pub);
+
 class NoiseConn : public Conn {
  public:
   // Runs the handshake over `c`.  Initiator: `expected` (if non-empty) must match
