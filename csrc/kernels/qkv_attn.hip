@@ -1,0 +1,485 @@
+// Decode step: qkv projection + RoPE + KV-cache write + attention in ONE launch
+// (batch rows M <= 16, contexts <= 256 keys: the chat decode regime).
+//
+// Unfused, a decode layer runs the qkv GEMV (weight stream, ~11 us at 8B) and then the
+// paged-attention kernel, whose ~7 us are a launch plus a serial load chain (block table
+// -> page -> K/V) and a short computation.  Here the same grid holds two kinds of
+// workgroup:
+//   * consumers (the first M x Hkv blocks, dispatched first): one per (row, kv head).
+//     At kernel start they load the block table and the K/V rows of every CACHED key of
+//     their context -- that latency now hides behind the weight stream -- then wait for
+//     the current token's q (G heads), k and v, compute the attention and write it.
+//   * producers (one per 16-column group of the permuted qkv weight, as the skinny
+//     kernel's EPI_QKV_ROPE): stream the weights, apply RMSNorm (rstd from the A
+//     fragments) and RoPE, write k/v of the current token to the cache for later steps,
+//     and publish the rotated q/k and v to the consumers as 8-byte tagged granules
+//     {tag << 32 | two bf16} (cdna_hip_programming.md publish/consume recipe R2: the
+//     data is the flag, no fence, one relaxed agent-scope 64-bit store per granule).
+// The tag of (row, kv head) is counters[row * Hkv + h] + 1: producers read it before they
+// publish, the consumer advances it after it has every granule, so a granule left by an
+// earlier call or layer never carries the current tag.  Consumers only wait on producers,
+// producers never wait, and consumer blocks are few (M x Hkv <= 128): the grid always
+// drains.  Spins are bounded; a timeout sets the fault word (LlamaModel.check_faults).
+#include "common.h"
+
+namespace {
+
+constexpr int PAGE = 64;
+constexpr int HD = 128;
+constexpr int QA_U = 4;       // producer: k-steps per pipeline batch
+constexpr int VS = HD + 8;    // V row stride in LDS (bf16): conflict-free 16-B writes
+constexpr long long QA_SPIN_TICKS = 500000000ll;  // 5 s at the 100 MHz wall clock
+
+typedef unsigned long long u64;
+
+struct QAArgs {
+  const bf16x8* Wt;
+  const bf16* X;
+  int ldx, M, K;
+  float eps;
+  const int* pos;
+  const int* slots;
+  const float2* cs;  // [max_pos][64] (cos, sin)
+  bf16* kc;
+  bf16* vc;
+  int Hq, Hkv;
+  const int* bt;
+  int bt_stride;
+  const int* ctx_lens;
+  float scale;
+  bf16* out;
+  int ldo;
+  u64* gran;          // [M][Hkv][G + 2][64] granules
+  unsigned* counters; // [M][Hkv]
+  int* err;
+  int n_cons;         // consumer blocks = M * Hkv
+  int probe;          // bench probe: 2 = consumers stop after the granule sweep
+};
+
+__device__ __forceinline__ unsigned bits16(float x) {
+  const bf16 b = f2bf(x);
+  unsigned short u;
+  __builtin_memcpy(&u, &b, 2);
+  return u;
+}
+
+__device__ __forceinline__ bf16x2 as_bf16x2(unsigned u) {
+  bf16x2 r;
+  __builtin_memcpy(&r, &u, 4);
+  return r;
+}
+
+// ---------------------------------------------------------------- producer
+template <int G, int W>
+__device__ __forceinline__ void producer(const QAArgs& a, int g, char* smem) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int S = a.K >> 5;
+  const int s0 = (S * w) / W, s1 = (S * (w + 1)) / W;
+  const bf16x8* wp = a.Wt + (size_t)g * S * 64 + lane;
+  const bool xv = r < a.M;
+  const bf16* xp = a.X + (size_t)(xv ? r : 0) * a.ldx + 8 * q;
+  const int head = g >> 3, kk = g & 7;
+  const int d = (r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8);
+  // epilogue rows m = 4q + j: their positions / slots / (cos, sin) now, behind the stream
+  float2 rc[4];
+  int rslot[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = 4 * q + j;
+    const bool ok = m < a.M && w == 0;
+    rslot[j] = ok ? a.slots[m] : -1;
+    rc[j] = ok ? a.cs[(size_t)a.pos[m] * 64 + (d & 63)] : float2{1.f, 0.f};
+  }
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f;
+  auto load = [&](int s, bf16x8(&bw)[QA_U], bf16x8(&ax)[QA_U]) {
+#pragma unroll
+    for (int u = 0; u < QA_U; ++u) {
+      bw[u] = __builtin_nontemporal_load(wp + (size_t)(s + u) * 64);
+      ax[u] = xv ? *reinterpret_cast<const bf16x8*>(xp + (s + u) * 32) : zero_bf16x8();
+    }
+  };
+  auto compute = [&](const bf16x8(&bw)[QA_U], const bf16x8(&ax)[QA_U]) {
+#pragma unroll
+    for (int u = 0; u < QA_U; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[u], bw[u], acc, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xf = (float)ax[u][j];
+        ss = fmaf(xf, xf, ss);
+      }
+    }
+  };
+  const int n = s1 - s0, nb = n / QA_U;
+  if (nb > 0) {
+    bf16x8 bA[QA_U], bB[QA_U], aA[QA_U], aB[QA_U];
+    load(s0, bA, aA);
+    int b = 0;
+    for (; b + 2 < nb; b += 2) {
+      load(s0 + (b + 1) * QA_U, bB, aB);
+      compute(bA, aA);
+      load(s0 + (b + 2) * QA_U, bA, aA);
+      compute(bB, aB);
+    }
+    if (b + 1 < nb) {
+      load(s0 + (b + 1) * QA_U, bB, aB);
+      compute(bA, aA);
+      compute(bB, aB);
+    } else {
+      compute(bA, aA);
+    }
+  }
+  for (int s = s0 + nb * QA_U; s < s1; ++s) {
+    const bf16x8 b1 = __builtin_nontemporal_load(wp + (size_t)s * 64);
+    const bf16x8 a1 = xv ? *reinterpret_cast<const bf16x8*>(xp + s * 32) : zero_bf16x8();
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss = fmaf((float)a1[j], (float)a1[j], ss);
+  }
+  // split-K over the block's waves
+  ss += __shfl_xor(ss, 16, 64);
+  ss += __shfl_xor(ss, 32, 64);
+  float* red = reinterpret_cast<float*>(smem);  // [W - 1][4][64]
+  float* red_ss = red + (W - 1) * 4 * 64;       // [W][16]
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[((w - 1) * 4 + j) * 64 + lane] = acc[j];
+  }
+  if (q == 0) red_ss[w * 16 + r] = ss;
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int ww = 0; ww < W - 1; ++ww)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += red[(ww * 4 + j) * 64 + lane];
+  const int Hq = a.Hq, Hkv = a.Hkv;
+  int kvh, sl;
+  if (head < Hq) {
+    kvh = head / G;
+    sl = head % G;
+  } else if (head < Hq + Hkv) {
+    kvh = head - Hq;
+    sl = G;
+  } else {
+    kvh = head - Hq - Hkv;
+    sl = G + 1;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = 4 * q + j;
+    float t = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) t += red_ss[ww * 16 + (m & 15)];
+    const float v = acc[j] * rsqrtf(t / (float)a.K + a.eps);
+    const float vp = __shfl_xor(v, 8, 64);
+    float y = v;
+    if (head < Hq + Hkv) y = (r < 8) ? (v * rc[j].x - vp * rc[j].y) : (v * rc[j].x + vp * rc[j].y);
+    const float y1 = __shfl_xor(y, 1, 64);
+    if (m < a.M) {
+      const int slot = rslot[j];
+      if (head >= Hq && slot >= 0) {  // k / v of the current token -> cache (later steps)
+        bf16* cache = head < Hq + Hkv ? a.kc : a.vc;
+        cache[(((size_t)(slot / PAGE) * Hkv + kvh) * PAGE + slot % PAGE) * HD + d] = f2bf(y);
+      }
+      if ((r & 1) == 0) {  // lanes r, r + 1 hold dims d, d + 1: one granule
+        const unsigned tag = a.counters[m * Hkv + kvh] + 1;
+        const u64 gr = ((u64)tag << 32) | ((u64)bits16(y1) << 16) | bits16(y);
+        __hip_atomic_store(a.gran + (((size_t)m * Hkv + kvh) * (G + 2) + sl) * 64 + (d >> 1), gr,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- consumer
+// Wave w owns the 64 keys of page w of the row (contexts <= 256 keys).  The math is the
+// MFMA form of decode attention (v_mfma_f32_16x16x32_bf16, query heads on the N axis,
+// G <= 16 padded with zero rows):
+//   S^T[key][head] = K . Q^T   (A = 16 keys x 32 dims, prefetched from the page into
+//                               registers at kernel start; B = q fragments)
+//   O[head][dim]  += P . V     (A = P: the S^T accumulators after the softmax; B = V^T
+//                               fragments from the wave's V rows in LDS)
+// so the per-wave work after the hand-off is 32 MFMAs and a 4-way LDS merge (a scalar
+// P.V loop over 64 keys per wave took ~7 us here).  This step's token (key ctx - 1) is
+// not in the prefetched rows: its k row is patched into the K fragments and its v row
+// into the LDS V rows from the granules.
+constexpr int MKPW = 64;  // keys per wave = one page
+constexpr int KW = 4;     // key waves: 4 pages = 256 keys (waves >= KW only join the barriers)
+
+template <int G, int W>
+__device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
+  static_assert(G >= 1 && G <= 16, "query heads on the MFMA N axis");
+  static_assert(W >= KW, "one page per key wave");
+  const int Hkv = a.Hkv;
+  const int r = b / Hkv, h = b % Hkv;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kk = lane & 15, qd = lane >> 4;
+  const int ctx = a.ctx_lens[r];
+  const int nprev = ctx - 1;  // keys already in the cache; key nprev is this step's token
+  auto& vs = *reinterpret_cast<bf16(*)[KW][MKPW][VS]>(smem);
+  auto& so = *reinterpret_cast<float(*)[KW][G][HD]>(smem);  // after P.V (aliases vs)
+  char* p = smem + (sizeof(bf16) * KW * MKPW * VS > sizeof(float) * KW * G * HD
+                        ? sizeof(bf16) * KW * MKPW * VS
+                        : sizeof(float) * KW * G * HD);
+  auto& cur = *reinterpret_cast<unsigned(*)[G + 2][64]>(p);  // q heads, k, v: bf16 pairs
+  p += sizeof(unsigned) * (G + 2) * 64;
+  auto& sm = *reinterpret_cast<float(*)[KW][G]>(p);
+  p += sizeof(float) * KW * G;
+  auto& sl = *reinterpret_cast<float(*)[KW][G]>(p);
+
+  // 1. this wave's page: K fragments to registers, V rows to LDS (all loads in flight)
+  const int n_valid = w < KW ? min(max(ctx - w * MKPW, 0), MKPW) : 0;  // wave-uniform
+  bf16x8 kr[4][4];
+  // a page holding only this step's token is still loaded whole: its other rows (stale or
+  // zero, always finite) keep the masked P.V lanes finite (0 x NaN would poison O)
+  if (n_valid > 0) {
+    const int page = a.bt[(size_t)r * a.bt_stride + w];
+    const size_t pbase = ((size_t)page * Hkv + h) * PAGE * HD;
+    bf16x8 vr[4][4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const bf16x8* kp = reinterpret_cast<const bf16x8*>(a.kc + pbase + (size_t)(16 * bb + kk) * HD + 8 * qd);
+      const bf16x8* vp = reinterpret_cast<const bf16x8*>(a.vc + pbase + (size_t)(16 * bb + kk) * HD + 8 * qd);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) kr[bb][s2] = kp[4 * s2];
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) vr[bb][s2] = vp[4 * s2];
+    }
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        *reinterpret_cast<bf16x8*>(&vs[w][16 * bb + kk][32 * s2 + 8 * qd]) = vr[bb][s2];
+  } else {
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) kr[bb][s2] = zero_bf16x8();
+  }
+  // 2. the current token's q (G heads), k and v from the producers' granules
+  const unsigned tag = a.counters[r * Hkv + h] + 1;
+  const u64* gb = a.gran + ((size_t)r * Hkv + h) * (G + 2) * 64;
+  const int failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long t0 = wall_clock64();
+  for (int i = tid; i < (G + 2) * 64; i += W * 64) {
+    u64 x = __hip_atomic_load(gb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while ((unsigned)(x >> 32) != tag && !failed) {
+      if (wall_clock64() - t0 > QA_SPIN_TICKS) {
+        atomicOr(a.err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      x = __hip_atomic_load(gb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    cur[i >> 6][i & 63] = (unsigned)x;
+  }
+  __syncthreads();
+  if (a.probe & 2) {  // probe: hand-off only (no attention math)
+    if (tid == 0) a.counters[r * Hkv + h] = tag;
+    return;
+  }
+  auto frag = [&](int row, int s2) {  // 8 dims (32 s2 + 8 qd ..) of a granule row, as bf16x8
+    bf16x8 f;
+    const unsigned* src = &cur[row][16 * s2 + 4 * qd];
+    __builtin_memcpy(&f, src, 16);
+    return f;
+  };
+  // this step's token: k row into the K fragments, v row into the LDS V rows
+  if (w < KW && nprev >= w * MKPW && nprev < (w + 1) * MKPW) {
+    const int rn = nprev - w * MKPW;
+    if (kk == (rn & 15)) {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+        if (bb == (rn >> 4)) {
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) kr[bb][s2] = frag(G, s2);
+        }
+    }
+    *reinterpret_cast<unsigned*>(&vs[w][rn][2 * lane]) = cur[G + 1][lane];
+  }
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) qf[s2] = kk < G ? frag(min(kk, G - 1), s2) : zero_bf16x8();
+
+  float mg = -INFINITY, lg = 0.f;  // per head kk (every lane of column kk agrees)
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int c = 0; c < HD / 16; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (n_valid > 0) {
+    // S^T blocks: lane holds keys 16 bb + 4 qd + j (j < 4) of head kk
+    f32x4 st[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      st[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        st[bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[bb][s2], qf[s2], st[bb], 0, 0, 0);
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = 16 * bb + 4 * qd + j < n_valid;
+        st[bb][j] = ok ? st[bb][j] * a.scale : -INFINITY;
+        m = fmaxf(m, st[bb][j]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float pr = __expf(st[bb][j] - m);  // -inf -> 0
+        st[bb][j] = pr;
+        l += pr;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    mg = m;
+    lg = l;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's V rows are in LDS
+    __builtin_amdgcn_wave_barrier();
+    // P.V: k-step t covers key blocks 2t (A slots 0-3) and 2t+1 (slots 4-7)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 pa;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pa[j] = f2bf(st[2 * t][j]);
+        pa[4 + j] = f2bf(st[2 * t + 1][j]);
+      }
+#pragma unroll
+      for (int c = 0; c < HD / 16; ++c) {
+        bf16x8 vb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          vb[j] = vs[w][32 * t + 4 * qd + j][16 * c + kk];
+          vb[4 + j] = vs[w][32 * t + 16 + 4 * qd + j][16 * c + kk];
+        }
+        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[c], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // every wave's P.V has read its V rows: the region becomes `so`
+  // O accumulators: lane holds O[head 4 qd + j][dim 16 c + kk]
+  if (w < KW) {
+#pragma unroll
+    for (int c = 0; c < HD / 16; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int hd = 4 * qd + j;
+        if (hd < G) so[w][hd][16 * c + kk] = o[c][j];
+      }
+  }
+  if (w < KW && qd == 0 && kk < G) {
+    sm[w][kk] = mg;
+    sl[w][kk] = lg;
+  }
+  __syncthreads();
+  for (int i = tid; i < G * HD; i += W * 64) {
+    const int hd = i / HD, dd = i % HD;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < KW; ++ww) M = fmaxf(M, sm[ww][hd]);
+    float num = 0.f, den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < KW; ++ww) {
+        const float e = __expf(sm[ww][hd] - M);
+        num = fmaf(e, so[ww][hd][dd], num);
+        den = fmaf(e, sl[ww][hd], den);
+      }
+    }
+    a.out[(size_t)r * a.ldo + (size_t)(h * G + hd) * HD + dd] = f2bf(den > 0.f ? num / den : 0.f);
+  }
+  if (tid == 0) a.counters[r * Hkv + h] = tag;  // every granule of this call was consumed
+}
+
+template <int G>
+constexpr size_t consumer_lds() {
+  const size_t v = sizeof(bf16) * KW * MKPW * VS;
+  const size_t o = sizeof(float) * KW * G * HD;
+  return (v > o ? v : o) + sizeof(unsigned) * (G + 2) * 64 + 2 * sizeof(float) * KW * G;
+}
+
+template <int G, int W>
+__global__ __launch_bounds__(W * 64) void qkv_attn_kernel(QAArgs a) {
+  constexpr size_t kProd = sizeof(float) * ((W - 1) * 4 * 64 + W * 16);
+  constexpr size_t kCons = consumer_lds<G>();
+  __shared__ __attribute__((aligned(16))) char smem[kCons > kProd ? kCons : kProd];
+  if ((int)blockIdx.x < a.n_cons)
+    consumer<G, W>(a, blockIdx.x, smem);
+  else
+    producer<G, W>(a, blockIdx.x - a.n_cons, smem);
+}
+
+template <int W>
+int launch_qa(const QAArgs& a, int G, int groups, hipStream_t stream) {
+  const dim3 grid(a.n_cons + groups), block(W * 64);
+  switch (G) {
+    case 1: hipLaunchKernelGGL((qkv_attn_kernel<1, W>), grid, block, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((qkv_attn_kernel<2, W>), grid, block, 0, stream, a); break;
+    case 4: hipLaunchKernelGGL((qkv_attn_kernel<4, W>), grid, block, 0, stream, a); break;
+    case 8: hipLaunchKernelGGL((qkv_attn_kernel<8, W>), grid, block, 0, stream, a); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+static int g_qa_probe = 0;
+
+// Bench probes (bench/qkv_attn_bench.py): 1 = producers only, 2 = hand-off without the
+// attention math; 0 = the real kernel.
+P2P_API void p2p_qkv_attn_probe(int mode) { g_qa_probe = mode; }
+
+// Fused decode qkv + RoPE + KV write + attention (see the file header).  Wt: the qkv
+// weight in fragment-major order with rope_row_perm rows (as p2p_skinny_gemm_qkv_rope),
+// bf16 only; M <= 16 rows, row r uses block-table row r and attends to ctx_lens[r] <= 256
+// keys (this step's token at position ctx - 1, its slot in slots[r]).  gran: u64
+// [M][Hkv][Hq / Hkv + 2][64], counters: u32 [M][Hkv] (zeroed once, private to this call
+// site's buffers), err: device int (fault word).
+P2P_API int p2p_qkv_attn(const void* Wt, const void* X, int ldx, int M, int K, int Hq, int Hkv,
+                         const int* pos, const int* slots, const void* cos_sin, void* k_cache,
+                         void* v_cache, const int* block_tables, int bt_stride,
+                         const int* ctx_lens, float scale, void* out, int ldo, float eps,
+                         void* gran, unsigned* counters, int* err, int waves, hipStream_t stream) {
+  if (M < 1 || M > 16 || K % 32 || Hkv <= 0 || Hq % Hkv || bt_stride * PAGE < 1)
+    return (int)hipErrorInvalidValue;
+  QAArgs a;
+  a.Wt = (const bf16x8*)Wt;
+  a.X = (const bf16*)X;
+  a.ldx = ldx;
+  a.M = M;
+  a.K = K;
+  a.eps = eps;
+  a.pos = pos;
+  a.slots = slots;
+  a.cs = (const float2*)cos_sin;
+  a.kc = (bf16*)k_cache;
+  a.vc = (bf16*)v_cache;
+  a.Hq = Hq;
+  a.Hkv = Hkv;
+  a.bt = block_tables;
+  a.bt_stride = bt_stride;
+  a.ctx_lens = ctx_lens;
+  a.scale = scale;
+  a.out = (bf16*)out;
+  a.ldo = ldo;
+  a.gran = (u64*)gran;
+  a.counters = counters;
+  a.err = err;
+  a.n_cons = (g_qa_probe & 1) ? 0 : M * Hkv;  // probe 1: producers only
+  a.probe = g_qa_probe;
+  const int groups = (Hq + 2 * Hkv) * (HD / 16);
+  // producer waves per block (split-K): 8 when the projection has few column groups (the
+  // 70B TP=8 shard: 80), as the skinny kernel's heuristic would pick; else 4
+  int W = waves;
+  if (W != 4 && W != 8) W = (groups * 8 * 2 <= 4096 && (K / 32) / 8 >= 8) ? 8 : 4;
+  return W == 8 ? launch_qa<8>(a, Hq / Hkv, groups, stream) : launch_qa<4>(a, Hq / Hkv, groups, stream);
+}

@@ -66,6 +66,11 @@ class Workspace:
             self.heads_slab, self.heads_tickets = ops.attn_oproj_heads_workspace(
                 rows, nkv, cfg.hidden, dev)
         self.row_ids = torch.arange(max_rows, device=dev, dtype=torch.int32)  # identity row_bt
+        # decode qkv + attention in one launch (ops.qkv_attn): granules + tag counters
+        self.qa = None
+        if dev.type == "cuda" and max_rows <= ops.attention.QKV_ATTN_MAX_ROWS and \
+                ops.qkv_attn_ok(max_rows, nq, nkv, max_ctx):
+            self.qa = ops.qkv_attn_workspace(max_rows, nq, nkv, dev)
         self.err = torch.zeros(1, device=dev, dtype=torch.int32)
 
 
@@ -94,6 +99,10 @@ class LlamaModel:
         mode = os.environ.get("P2P_FUSED_ATTN_OPROJ", "0")
         self.fuse_attn_oproj = mode == "1"
         self.fuse_heads = mode == "heads"
+        # decode (rows <= 16, contexts <= 256): qkv projection + RoPE + KV write + attention
+        # as ONE launch (ops.qkv_attn): the attention's block-table -> K/V load chain runs
+        # behind the qkv weight stream.  P2P_QKV_ATTN=0: the two kernels.
+        self.fuse_qkv_attn = os.environ.get("P2P_QKV_ATTN", "1") == "1"
         self.heads_max_rows = int(os.environ.get("P2P_HEADS_MAX_ROWS", "4"))
         # TP prefill: row-parallel GEMMs of >= this many rows overlap their all-reduce
         # (chunked, separate communication stream); decode-size sums use the one-shot AR
@@ -186,8 +195,17 @@ class LlamaModel:
         heads = (not fused and self.fuse_heads and tiles is None and ws.heads_slab is not None
                  and R <= self.heads_max_rows and isinstance(self.w.layers[0].o, torch.Tensor)
                  and ops.attn_oproj_heads_ok(R, self.nq, self.nkv, max_ctx, cfg.hidden))
+        qa = (self.fuse_qkv_attn and not fused and not heads and tiles is None
+              and row_bt is None and ws.qa is not None and isinstance(self.w.layers[0].qkv, torch.Tensor)
+              and ops.qkv_attn_ok(R, self.nq, self.nkv, max_ctx))
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)
+            if qa:
+                ops.qkv_attn(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, kc, vc,
+                             block_tables, ctx_lens[:R], attn, ws.qa, ws.err, eps=cfg.eps)
+                self._row_parallel(lw.o, attn, h, ws, R)
+                self._mlp(lw, ws, R)
+                continue
             ops.qkv_rope_gemm(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc,
                               vc, eps=cfg.eps)
             if heads:
@@ -231,7 +249,8 @@ class LlamaModel:
         costs one small device read, call where the host syncs anyway."""
         if self.device.type == "cuda" and int(ws.err.item()) != 0:
             ws.err.zero_()
-            raise RuntimeError("fused attention/o_proj hand-off timed out (results invalid)")
+            raise RuntimeError("fused in-launch hand-off (qkv -> attention, attention -> "
+                               "o_proj) timed out (results invalid)")
         if self.device.type == "cuda" and ops.tiled_split_fault():
             raise RuntimeError("split-K GEMM slice wait timed out (results invalid)")
         if self.comm is not None and hasattr(self.comm, "check"):

@@ -56,6 +56,9 @@ _SIGS = {
     "p2p_car_all_gather": [c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p,
                            ctypes.c_longlong, c_void_p, c_void_p, c_int, c_void_p],
     "p2p_car_set_timeout_ms": [c_int],
+    "p2p_qkv_attn": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                     c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_float, c_void_p,
+                     c_int, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "p2p_skinny_gemm_ar": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                            c_void_p, c_int, c_int, ctypes.c_size_t, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p],
@@ -154,6 +157,10 @@ def lib():
             if fn is not None:
                 fn.argtypes = [c_int]
                 fn.restype = None
+        fn = getattr(L, "p2p_qkv_attn_probe", None)
+        if fn is not None:
+            fn.argtypes = [c_int]
+            fn.restype = None
         fn = getattr(L, "p2p_skinny_gemm_tune", None)
         if fn is not None:
             fn.argtypes = [c_int, c_int]

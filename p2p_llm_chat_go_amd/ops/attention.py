@@ -85,6 +85,52 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
 FUSED_MAX_ROWS = 16
 FUSED_MAX_CTX = 256
 
+# decode qkv + RoPE + KV write + attention in one launch (csrc/kernels/qkv_attn.hip)
+QKV_ATTN_MAX_ROWS = 16
+QKV_ATTN_MAX_CTX = 256
+
+
+def qkv_attn_ok(R: int, n_heads: int, n_kv: int, max_ctx: int) -> bool:
+    return (1 <= R <= QKV_ATTN_MAX_ROWS and max_ctx <= QKV_ATTN_MAX_CTX and n_kv > 0
+            and n_heads % n_kv == 0 and n_heads // n_kv in (1, 2, 4, 8))
+
+
+def qkv_attn_workspace(rows: int, n_heads: int, n_kv: int, device) -> tuple:
+    """(granules u64 [rows][n_kv][G + 2][64], tag counters u32 [rows][n_kv]), zeroed."""
+    G = n_heads // n_kv
+    gran = torch.zeros(rows * n_kv * (G + 2) * 64, dtype=torch.int64, device=device)
+    cnt = torch.zeros(rows * n_kv, dtype=torch.int32, device=device)
+    return gran, cnt
+
+
+QKV_ATTN_WAVES = int(os.environ.get("P2P_QA_WAVES", "0"))  # 0: heuristic (4 or 8)
+
+
+def qkv_attn(wt, x, pos, slots, cos_sin, n_heads, n_kv, k_cache, v_cache, block_tables,
+             ctx_lens, out, workspace, err, eps=1e-5, scale=None, waves=None):
+    """Decode step's qkv projection (RMSNorm folded, rope_row_perm rows) + RoPE + paged-KV
+    write + attention in one launch (csrc/kernels/qkv_attn.hip): out[r] = attention of
+    row r's q over its ctx_lens[r] keys (this step's token last), block-table row r.
+    Same numbers as qkv_rope_gemm followed by paged_attention (up to summation order)."""
+    from .gemm import tiled_shape
+
+    R = x.shape[0]
+    N, K = tiled_shape(wt)
+    assert N == (n_heads + 2 * n_kv) * HEAD_DIM and x.stride(1) == 1
+    if scale is None:
+        scale = 1.0 / math.sqrt(HEAD_DIM)
+    gran, cnt = workspace
+    assert gran.numel() >= R * n_kv * (n_heads // n_kv + 2) * 64 and cnt.numel() >= R * n_kv
+    L = _lib.lib()
+    _lib.check(L.p2p_qkv_attn(
+        wt.data_ptr(), x.data_ptr(), x.stride(0), R, K, n_heads, n_kv, pos.data_ptr(),
+        slots.data_ptr(), cos_sin.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+        block_tables.data_ptr(), block_tables.stride(0), ctx_lens.data_ptr(), float(scale),
+        out.data_ptr(), out.stride(0), float(eps), gran.data_ptr(), cnt.data_ptr(),
+        err.data_ptr(), QKV_ATTN_WAVES if waves is None else int(waves),
+        _lib.stream_ptr(x.device)), "qkv_attn")
+    return out
+
 
 def attn_oproj_ok(R: int, n_heads: int, n_kv: int, max_ctx: int, N: int) -> bool:
     """Shapes the fused attention + o_proj kernel handles (else run the two ops)."""
