@@ -52,7 +52,9 @@ def main():
     tok = get_tokenizer(cfg)
     eng = Engine(cfg, device=dev, seed=7, max_batch=max(a.peers, 1), max_prefill_tokens=1024)
     eng.warmup(tuple(sorted({1, 2, 4, 8, a.peers} - {0})), ctx=256)
-    srv = EngineServer(eng, tok, max_batch=a.peers, decode_chunk=8, mixed=bool(a.mixed))
+    srv = EngineServer(eng, tok, max_batch=a.peers,
+                       decode_chunk=int(os.environ.get("ENGINE_DECODE_CHUNK", "8")),
+                       mixed=bool(a.mixed))
     prompts = [tok.chat_ids(suggest_prompt(SAMPLE_MESSAGES[i % len(SAMPLE_MESSAGES)]))
                for i in range(a.peers)]
 
@@ -80,6 +82,7 @@ def main():
     srv.close()
     toks = sum(r["eval_count"] for r in results)
     ttft = sorted(r["ttft_ns"] / 1e6 for r in results)
+    queue = sorted((r["ttft_ns"] - r["prompt_eval_duration"]) / 1e6 for r in results)
     steps = srv.stats["decode_steps"] - occ0["decode_steps"]
     print(json.dumps({
         "metric": "suggest-reply tokens/sec (continuous batching)", "value": round(toks / el, 2),
@@ -87,6 +90,9 @@ def main():
         "new_tokens": a.new_tokens, "elapsed_s": round(el, 3),
         "ttft_p50_ms": round(statistics.median(ttft), 3),
         "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
+        "queue_p50_ms": round(statistics.median(queue), 3),
+        "queue_p99_ms": round(queue[min(len(queue) - 1, int(0.99 * len(queue)))], 3),
+        "decode_chunk": srv.decode_chunk, "admit_wait_us": round(srv.admit_wait_s * 1e6),
         "mean_batch": round(toks / max(steps, 1), 2), "mixed": bool(a.mixed), "dtype": "bf16",
         "engine_time_s": {k: round(srv.stats[k] - occ0[k], 4) for k in
                           ("busy_s", "prefill_s", "decode_s", "prefill_calls", "decode_calls")},

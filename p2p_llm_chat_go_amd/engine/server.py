@@ -343,13 +343,19 @@ class EngineServer:
                    if self.sched.get(i).state == 1]
         if running:
             self._decode(eng, running)
-        if self._retire() and self.admit_wait_s > 0:
-            # a reply just went out: its peer (or a queued client) usually sends the next
-            # request within a fraction of a millisecond -- admit it at THIS step boundary
-            # instead of leaving its batch slot idle for a whole decode chunk
+        done = self._retire()
+        if done and self.admit_wait_s > 0:
+            # replies just went out: their peers (or queued clients) usually send the next
+            # requests within a fraction of a millisecond -- admit them at THIS step
+            # boundary instead of leaving their batch slots idle for a whole step.  Wait
+            # (bounded) until as many requests are pending as replies were sent.
+            deadline = time.perf_counter() + self.admit_wait_s
             with self._lock:
-                if not self._pending and not self._stop:
-                    self._lock.wait(timeout=self.admit_wait_s)
+                while len(self._pending) < done and not self._stop:
+                    left = deadline - time.perf_counter()
+                    if left <= 0:
+                        break
+                    self._lock.wait(timeout=left)
 
     def _decode(self, eng: Engine, running: list):
         reqs = [self.sched.get(i) for i in running]
