@@ -53,7 +53,7 @@ class CustomAllReduce:
         self.max_bytes = int(max_bytes)
         # two-shot from this many bytes (and 4+ ranks: at 2 ranks both forms move the same
         # bytes and the one-shot has one hop less)
-        self.two_shot_min = int(os.environ.get("P2P_CAR_2SHOT_MIN", str(512 << 10)))
+        self.two_shot_min = int(os.environ.get("P2P_CAR_2SHOT_MIN", str(256 << 10)))
         L = self.L = _lib.lib()
         tmo = int(os.environ.get("P2P_CAR_TIMEOUT_MS", "0"))
         if tmo > 0:  # spin bound of every one-shot / fused call (default 5 s)
