@@ -898,7 +898,7 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
 // m-tile of 192 / 320 rows: at these M the tiles are bound by the per-CU LDS-DMA fill
 // rate, so the bytes staged per useful output decide, and 128-row tiles would stream
 // every weight column 2-3 times (25 % padding) while 256x256 pads up to 44 %.
-int pick_tile(int M, int N) {
+static int pick_tile(int M, int N) {
   if (M <= 64) return N % 128 == 0 ? 4 : 0;
   if (N % 128 == 0 && ((M > 128 && M <= 192) || (M > 256 && M <= 320)))
     return M <= 192 ? 7 : 6;
@@ -918,7 +918,7 @@ int pick_tile(int M, int N) {
 // Per-row RMSNorm statistics for the prefill GEMMs (one wave per row, every 16-byte load
 // of the row issued before the first use): rstd[m] = rsqrt(mean_k X[m,k]^2 + eps).  Run
 // once per normed projection instead of inside every n-tile's k loop.
-__global__ __launch_bounds__(256) void row_rstd_kernel(const bf16* __restrict__ X, int ldx, int M,
+static __global__ __launch_bounds__(256) void row_rstd_kernel(const bf16* __restrict__ X, int ldx, int M,
                                                        int K, float eps, float* __restrict__ out) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
@@ -970,6 +970,7 @@ static const float* pre_rstd(const void* X, int ldx, int M, int K, float eps, hi
 
 }  // namespace pgemm
 
+#ifndef PGEMM_NO_DISPATCH  // (wide_gemm.hip uses the split-K helpers only)
 static int g_prefill_tile = 0;  // 0 = heuristic (benchmarks can force 1..3)
 
 // Used by the p2p_tiled_gemm* entry points (tiled_gemm.hip).  Returns
@@ -1015,3 +1016,4 @@ static int prefill_dispatch(const void* Wt, const void* X, int ldx, int M, int K
   }
   return (int)hipErrorInvalidValue;
 }
+#endif  // PGEMM_NO_DISPATCH

@@ -45,6 +45,10 @@ int skinny_unit_argmax(SKINNY_UNIT_ARGS);
 int skinny_unit_ar(SKINNY_UNIT_ARGS);
 
 constexpr int MIDM_FLAG = 1 << 25;  // launch-code bit (ops.gemm.MIDM_FLAG)
+constexpr int WIDE_FLAG = 1 << 26;  // launch-code bit (ops.gemm.WIDE_FLAG), K slices in bits 8..15
+extern "C" int p2p_wide_dispatch(const void* Wt, const void* X, int ldx, int M, int K, int N,
+                                 int epi, int norm, void* out, int ldo, float eps, const void* ea_p,
+                                 int req_split, hipStream_t st);
 
 // Picks the split-K factor: enough waves to keep ~8+ MB of weight loads in flight,
 // but every wave resident in the first dispatch round (256 CUs x 4 SIMDs x
@@ -76,6 +80,10 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
     groups = N / 32;
     up_off = groups;
   }
+  // bit 26: the wide mid-M kernel (wide_gemm.hip; bf16 dense weights, K % 256 == 0)
+  if ((waves & WIDE_FLAG) && epi != EPI_AR)
+    return p2p_wide_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, &ea, (waves >> 8) & 0xff,
+                             stream);
   // bit 25: the mid-M LDS-DMA kernel (midm_gemm.h; bf16 dense weights, K % 128 == 0)
   if ((waves & MIDM_FLAG) && !ea.wscale && !ea.moe_cnt && K % 128 == 0) {
     switch (epi) {
@@ -209,7 +217,7 @@ P2P_API int p2p_skinny_gemm_ar(const void* Wt, const void* X, int ldx, int M, in
   ea.far.counters = counters;
   ea.far.err = err;
   ea.far.spin_ticks = p2p_car_spin_ticks();
-  waves &= ~(MIDM_FLAG | (1 << 24));  // skinny only
+  waves &= ~(WIDE_FLAG | MIDM_FLAG | (1 << 24));  // skinny only
   return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_AR, 0, h, ldh, 0.f, waves, ea, stream);
 }
 

@@ -222,7 +222,11 @@ P2P_API void p2p_tiled_split_parallel(int on) { pgemm::g_split_parallel = on ? 1
 
 // Nonzero if a parallel split-K slice waited past its spin bound since the last call
 // (its tile's output is invalid); clears the word.  Synchronises the current device.
+extern "C" int p2p_wide_split_fault();  // wide_gemm.hip (its own split workspace)
+
 P2P_API int p2p_tiled_split_fault() {
+  const int wv = p2p_wide_split_fault();
+  if (wv) return wv;
   if (!pgemm::g_split_ws.buf) return 0;
   int* w = (int*)((char*)pgemm::g_split_ws.buf + pgemm::g_split_ws.bytes - sizeof(unsigned));
   int v = 0;

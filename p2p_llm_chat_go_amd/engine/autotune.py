@@ -40,13 +40,17 @@ def _graph_time(fn, reps=3):
     return best
 
 
-def _configs(K, M=1, tiled=False, midm=False):
+def _configs(K, M=1, tiled=False, midm=False, wide=False):
     """Launch codes: waves | U << 8 | NG << 16 (NG = column groups per block, M > 16);
     G.TILED_FLAG = the split-K LDS-DMA tiled kernel (M > 16, tileable shapes);
-    G.MIDM_FLAG = the whole-K LDS-DMA kernel (M > 1, bf16 weights, K % 128 == 0)."""
+    G.MIDM_FLAG = the whole-K LDS-DMA kernel (M > 1, bf16 weights, K % 128 == 0);
+    G.WIDE_FLAG = the wide kernel (M > 1, bf16 weights, wide_ok shapes), heuristic K split
+    and the two neighbouring powers of two."""
     out = [G.TILED_FLAG] if (tiled and M > 16) else []
     if midm and M > 1 and K % 128 == 0:
         out.append(G.MIDM_FLAG)
+    if wide and M > 1:
+        out += [G.WIDE_FLAG, G.WIDE_FLAG | (4 << 8), G.WIDE_FLAG | (8 << 8)]
     # NG=2 at M <= 16 (twice the weight bytes in flight per wave) is supported by the kernel
     # but was never faster at the 8B decode shapes (two bench runs, w1-w8): not tuned
     for ng in ((1,) if M <= 16 else (1, 2)):
@@ -62,6 +66,9 @@ def describe(code: int) -> str:
         return "tiled"
     if code & G.MIDM_FLAG:
         return "midm"
+    if code & G.WIDE_FLAG:
+        sk = (code >> 8) & 0xff
+        return "wide/s%s" % (sk if sk else "auto")
     ng = (code >> 16) & 0xff
     return "w%d/U%d%s" % (code & 0xff, (code >> 8) & 0xff, "/NG%d" % ng if ng > 1 else "")
 
@@ -103,7 +110,8 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
             N, K = G.tiled_shape(wts[0])
             times = {}
             bf = not G._is_f8(wts[0])
-            for code in _configs(K, M, G.tiled_ok(N, K, epi) and bf, midm=bf):
+            for code in _configs(K, M, G.tiled_ok(N, K, epi) and bf, midm=bf,
+                                 wide=bf and G.wide_ok(N, K, epi)):
                 times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
             best = min(times, key=times.get)
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)

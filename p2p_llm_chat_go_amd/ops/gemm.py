@@ -123,6 +123,14 @@ def set_tiled_min_m(m: int):
     TILED_MIN_M = int(m)
 
 
+def wide_ok(N, K, epi) -> bool:
+    """Shapes the wide mid-M kernel tiles: 128 output columns per workgroup (SwiGLU: 64
+    gate/up pairs), K in 256-wide chunks."""
+    if K % 256:
+        return False
+    return (N // 2) % 64 == 0 if epi == EPI_SILU else N % 128 == 0
+
+
 def tiled_ok(N, K, epi) -> bool:
     if K % 64:
         return False
@@ -141,6 +149,11 @@ TILED_FLAG = 1 << 24
 # per workgroup over the whole K, activations + weights streamed through an LDS ring);
 # bf16 dense weights, K % 128 == 0, M <= 64 (autotuned against skinny / tiled)
 MIDM_FLAG = 1 << 25
+# launch-code bit: the wide mid-M kernel (csrc/kernels/wide_gemm.hip: 8 waves x 16 columns
+# per workgroup share the activation chunks in LDS, each wave streams its own weight group
+# into VGPRs, split-K over workgroups); bits 8..15 = K slices (0 = heuristic); bf16 dense
+# weights, K % 256 == 0, 1 < M <= 64
+WIDE_FLAG = 1 << 26
 
 
 def _want_tiled(wt, M, N, K, epi, norm, waves) -> bool:
@@ -268,7 +281,7 @@ def skinny_ar_ok(wt, M: int) -> bool:
     tiled / mid-M kernel (prompt-sized M) keeps the partial store + one-shot kernel."""
     if M > SKINNY_MAX_M:
         return False
-    return not (_code(wt, M, EPI_AR, False, 0) & (TILED_FLAG | MIDM_FLAG))
+    return not (_code(wt, M, EPI_AR, False, 0) & (TILED_FLAG | MIDM_FLAG | WIDE_FLAG))
 
 
 def skinny_gemm_ar(wt, x: torch.Tensor, h: torch.Tensor, car, waves: int = 0) -> torch.Tensor:

@@ -111,6 +111,18 @@ def test_midm_gemm_every_epilogue(M, K):
     _every_epilogue(M, MIDM_FLAG, 1000 + M, K=K)
 
 
+@pytest.mark.parametrize("M", [2, 16, 17, 44, 64])
+@pytest.mark.parametrize("K,split", [(1024, 0), (1024, 1), (1536, 4), (2048, 3), (2048, 8)])
+def test_wide_gemm_every_epilogue(M, K, split):
+    """The wide mid-M kernel (launch-code bit ops.gemm.WIDE_FLAG: 8 waves x 16 columns share
+    LDS activation chunks, split-K over workgroups with the parallel slab reduction) on every
+    epilogue vs fp32 references; 1536 / 4 slices gives slices of one and two chunks."""
+    from p2p_llm_chat_go_amd.ops.gemm import WIDE_FLAG
+
+    _every_epilogue(M, WIDE_FLAG | (split << 8), 2000 + M + K + split, K=K)
+    assert ops.tiled_split_fault() == 0
+
+
 def _every_epilogue(M, code, seed, K=1024):
     from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
 
