@@ -63,10 +63,14 @@ def main():
                     if f not in best or t < best[f][0]:
                         best[f] = (t, describe(code))
                 row.update({f: "%s %.1fus" % (d, t) for f, (t, d) in sorted(best.items())})
-            for s in splits:
-                code = G.WIDE_FLAG | (s << 8)
-                t = _graph_time(lambda: [fn(wt, code) for wt in wts]) * 1000 / len(wts)
-                row["wide_s%s" % (s if s else "auto")] = round(t, 2)
+            from p2p_llm_chat_go_amd.ops import _lib
+            for res in (1, 0) if os.environ.get("WIDE_AB_RES", "0") == "1" else (1,):
+                _lib.lib().p2p_wide_resident(res)
+                for s in splits:
+                    code = G.WIDE_FLAG | (s << 8)
+                    t = _graph_time(lambda: [fn(wt, code) for wt in wts]) * 1000 / len(wts)
+                    row["wide%s_s%s" % ("" if res else "ring", s if s else "auto")] = round(t, 2)
+            _lib.lib().p2p_wide_resident(1)
             assert ops.tiled_split_fault() == 0
             print(json.dumps(row), flush=True)
 

@@ -39,6 +39,17 @@ __device__ __forceinline__ bf16x8 zero_bf16x8() {
   return z;
 }
 
+// acc + sum of squares of 8 bf16 values: four v_dot2c_f32_bf16 (the RMSNorm statistics
+// ride in the GEMM k loops; 8 widen + 8 FMA per fragment made them VALU-heavy there)
+__device__ __forceinline__ float sumsq8(const bf16x8& v, float acc) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const bf16x2 t = {v[2 * p], v[2 * p + 1]};
+    acc = __builtin_amdgcn_fdot2_f32_bf16(t, t, acc, false);
+  }
+  return acc;
+}
+
 // x * sigmoid(x) with v_rcp_f32 (~1 ulp) instead of an IEEE division: the division
 // sequence (div_scale / div_fmas / div_fixup, ~10 VALU) dominated the SwiGLU epilogue of
 // the prefill GEMM (a 256x256 tile stores 128 outputs per thread)

@@ -189,3 +189,24 @@ P2P_API int p2p_advance(int* ids, unsigned long long* keys, int* pos, int* ctx, 
                      ctx, slots, bt, bt_stride, hist, hist_stride, step, B);
   return (int)hipGetLastError();
 }
+
+// Row-major X [M, K] -> fragment-major Xf: 16-row m-tiles, each K/32 MFMA A fragments of
+// 1 KiB (lane l of fragment (mt, s) holds X[16 mt + (l & 15)][32 s + 8 (l >> 4) .. + 7]);
+// rows past M are zero.  One thread per 16-byte chunk.
+__global__ __launch_bounds__(256) void pack_frag_kernel(const bf16* __restrict__ X, int ldx, int M,
+                                                         int S, int chunks, bf16x8* __restrict__ Xf) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= chunks) return;
+  const int lane = i & 63, s = (i >> 6) % S, mt = (i >> 6) / S;
+  const int row = mt * 16 + (lane & 15);
+  Xf[i] = row < M ? *reinterpret_cast<const bf16x8*>(X + (size_t)row * ldx + 32 * s + 8 * (lane >> 4))
+                  : zero_bf16x8();
+}
+
+P2P_API int p2p_pack_frag(const void* X, int ldx, int M, int K, void* Xf, hipStream_t st) {
+  if (M <= 0 || K % 32 || ldx % 8) return (int)hipErrorInvalidValue;
+  const int S = K / 32, chunks = ((M + 15) / 16) * S * 64;
+  hipLaunchKernelGGL(pack_frag_kernel, dim3((chunks + 255) / 256), dim3(256), 0, st, (const bf16*)X,
+                     ldx, M, S, chunks, (bf16x8*)Xf);
+  return (int)hipGetLastError();
+}

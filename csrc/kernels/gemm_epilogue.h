@@ -42,6 +42,7 @@ struct EpiArgs {
   int u;   // requested pipeline depth (0 = default)
   int ng;  // requested column groups per block (skinny GEMM, M > 16; 0/1 = one)
   const float* rstd_in;  // prefill GEMM NORM: per-row rstd precomputed (null = in-loop sums)
+  int afrag;  // skinny GEMM: X is fragment-major (p2p_pack_frag), 16-row m-tiles of K/32 x 1 KiB
   FusedArArgs far;       // EPI_AR: the group's fused all-reduce buffers
 };
 

@@ -125,13 +125,7 @@ __global__ __launch_bounds__(NT, 2) void midm_kernel(const bf16x8* __restrict__ 
 #pragma unroll
       for (int b = 0; b < NB; ++b)
         acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bw[b], acc[b][mt], 0, 0, 0);
-      if constexpr (NORM) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = (float)af[mt][e];
-          ss[mt] = fmaf(v, v, ss[mt]);
-        }
-      }
+      if constexpr (NORM) ss[mt] = sumsq8(af[mt], ss[mt]);
     }
   }
   wait_vmcnt<0>();
@@ -168,6 +162,28 @@ __global__ __launch_bounds__(NT, 2) void midm_kernel(const bf16x8* __restrict__ 
         for (int ww = 0; ww < 4; ++ww) v += red[(((ww * NB + b) * MT + mt) * 4 + j) * 64 + lane];
         tot[b][j] = v;
       }
+    // epilogue operands of the 4 rows as one batch (residual values / rows' KV slot and
+    // (cos, sin)): loaded per element between the stores they were 4 dependent round trips
+    float resv[4];
+    float2 csv[4];
+    int slotv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = 16 * mt + 4 * q + j;
+      resv[j] = 0.f;
+      csv[j] = float2{1.f, 0.f};
+      slotv[j] = -1;
+      if constexpr (EPI == EPI_RESID)
+        if (m < M) resv[j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + g * 16 + r];
+      if constexpr (EPI == EPI_QKV_ROPE) {
+        if (m < M) {
+          const int kk = g & 7;
+          const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+          csv[j] = ea.cs[(size_t)ea.pos[m] * 64 + dd];
+          slotv[j] = ea.slots[m];
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = 16 * mt + 4 * q + j;
@@ -180,15 +196,10 @@ __global__ __launch_bounds__(NT, 2) void midm_kernel(const bf16x8* __restrict__ 
         scale = rsqrtf(t2 / (float)K + eps);
       }
       if constexpr (EPI == EPI_QKV_ROPE) {
-        const int kk = g & 7;
-        const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
-        float2 cs = float2{1.f, 0.f};
-        int slot = -1;
-        if (valid) {
-          cs = ea.cs[(size_t)ea.pos[m] * 64 + dd];
-          slot = ea.slots[m];
-        }
-        epi_store<EPI>(m, valid, g, r, tot[0][j] * scale, 0.f, out, ldo, ea, cs, slot);
+        epi_store<EPI>(m, valid, g, r, tot[0][j] * scale, 0.f, out, ldo, ea, csv[j], slotv[j]);
+      } else if constexpr (EPI == EPI_RESID) {
+        if (valid)
+          reinterpret_cast<bf16*>(out)[(size_t)m * ldo + g * 16 + r] = f2bf(resv[j] + tot[0][j] * scale);
       } else {
         epi_store<EPI>(m, valid, g, r, tot[0][j] * scale, tot[NB - 1][j] * scale, out, ldo, ea);
       }

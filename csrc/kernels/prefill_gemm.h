@@ -235,11 +235,7 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           if ((i & 3) != wn) continue;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = (float)af[i][e];
-            ss[i] = fmaf(v, v, ss[i]);
-          }
+          ss[i] = sumsq8(af[i], ss[i]);
         }
       }
     }
@@ -281,12 +277,53 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
+      // one fragment row's epilogue operands as one batch (residual values; the rows'
+      // positions -> (cos, sin) and KV slots): per element, between the stores they may
+      // alias, they were FN x 4 dependent round trips per fragment row
+      float resv[4][FN];
+      float2 csv[4][FN];
+      int slotv[4];
+      if constexpr (EPI == EPI_RESID || EPI == EPI_QKV_ROPE) {
+        int posv[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int m = m0 + wm_ * (BM / 2) + 16 * i + 4 * q + jj;
+          posv[jj] = 0;
+          slotv[jj] = -1;
+          if constexpr (EPI == EPI_QKV_ROPE && !MOE)
+            if (m < M) {
+              posv[jj] = ea.pos[m];
+              slotv[jj] = ea.slots[m];
+            }
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            resv[jj][j] = 0.f;
+            if constexpr (EPI == EPI_RESID && !MOE)
+              if (m < M) resv[jj][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + (nt_i * (BN / 16) + bg[j]) * 16 + r];
+          }
+        }
+        if constexpr (EPI == EPI_QKV_ROPE && !MOE) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              const int g = nt_i * (BN / 16) + bg[j];
+              const int kk = g & 7;
+              const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+              const bool ok = m0 + wm_ * (BM / 2) + 16 * i + 4 * q + jj < M;
+              csv[jj][j] = ok ? ea.cs[(size_t)posv[jj] * 64 + dd] : float2{1.f, 0.f};
+            }
+        }
+      }
+      float scv[4];  // the rows' rstd (loads, with the operands above)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) scv[jj] = scale_of(i, jj);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int rl = wm_ * (BM / 2) + 16 * i + 4 * q + jj;
         int m = m0 + rl;
         const bool valid = m < M;
-        float scale = scale_of(i, jj);
+        float scale = scv[jj];
         if constexpr (MOE) {
           m = valid ? mrows[m] : 0;  // output row = the slot
           if (ea.row_w && valid) scale *= ea.row_w[m];
@@ -297,20 +334,17 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
           for (int j = 0; j < H; ++j)
             epi_store<EPI>(m, valid, nt_i * (BN / 32) + wn_ * H + j, r, ac[i][j][jj] * scale,
                            ac[i][j + H][jj] * scale, out, ldo, ea);
-        } else if constexpr (EPI == EPI_QKV_ROPE) {
+        } else if constexpr (EPI == EPI_QKV_ROPE && !MOE) {
 #pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            const int g = nt_i * (BN / 16) + bg[j];
-            const int kk = g & 7;
-            const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
-            float2 c = float2{1.f, 0.f};
-            int slot = -1;
-            if (valid) {
-              c = ea.cs[(size_t)ea.pos[m] * 64 + dd];
-              slot = ea.slots[m];
-            }
-            epi_store<EPI>(m, valid, g, r, ac[i][j][jj] * scale, 0.f, out, ldo, ea, c, slot);
-          }
+          for (int j = 0; j < FN; ++j)
+            epi_store<EPI>(m, valid, nt_i * (BN / 16) + bg[j], r, ac[i][j][jj] * scale, 0.f, out,
+                           ldo, ea, csv[jj][j], valid ? slotv[jj] : -1);
+        } else if constexpr (EPI == EPI_RESID && !MOE) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            if (valid)
+              reinterpret_cast<bf16*>(out)[(size_t)m * ldo + (nt_i * (BN / 16) + bg[j]) * 16 + r] =
+                  f2bf(resv[jj][j] + ac[i][j][jj] * scale);
         } else {
 #pragma unroll
           for (int j = 0; j < FN; ++j)
@@ -593,11 +627,7 @@ __global__ __launch_bounds__(NT) void prefill_gemm8_kernel(const bf16x8* __restr
         if (i != wn) continue;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = (float)af[i][ks][e];
-            ss[4 * q + i] = fmaf(v, v, ss[4 * q + i]);
-          }
+          ss[4 * q + i] = sumsq8(af[i][ks], ss[4 * q + i]);
       }
     }
   };
@@ -662,12 +692,52 @@ __global__ __launch_bounds__(NT) void prefill_gemm8_kernel(const bf16x8* __restr
   const int r = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
+    // one fragment row's epilogue operands as one batch (see prefill_gemm_kernel)
+    float resv[4][FN];
+    float2 csv[4][FN];
+    int slotv[4];
+    if constexpr (EPI == EPI_RESID || EPI == EPI_QKV_ROPE) {
+      int posv[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int m = m0 + wm * (BM / 2) + 16 * i + 4 * q + jj;
+        posv[jj] = 0;
+        slotv[jj] = -1;
+        if constexpr (EPI == EPI_QKV_ROPE)
+          if (m < M) {
+            posv[jj] = ea.pos[m];
+            slotv[jj] = ea.slots[m];
+          }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          resv[jj][j] = 0.f;
+          if constexpr (EPI == EPI_RESID)
+            if (m < M) resv[jj][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + (nt_i * (BN / 16) + bgi[j]) * 16 + r];
+        }
+      }
+      if constexpr (EPI == EPI_QKV_ROPE) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int g = nt_i * (BN / 16) + bgi[j];
+            const int kk = g & 7;
+            const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+            const bool ok = m0 + wm * (BM / 2) + 16 * i + 4 * q + jj < M;
+            csv[jj][j] = ok ? ea.cs[(size_t)posv[jj] * 64 + dd] : float2{1.f, 0.f};
+          }
+      }
+    }
+    float scv[4];  // the rows' precomputed rstd, loaded with the operands above
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      scv[jj] = pre ? ea.rstd_in[min(m0 + wm * (BM / 2) + 16 * i + 4 * q + jj, M - 1)] : 1.f;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int rl = wm * (BM / 2) + 16 * i + 4 * q + jj;
       const int m = m0 + rl;
       const bool valid = m < M;
-      float scale = pre ? ea.rstd_in[min(m, M - 1)] : 1.f;
+      float scale = scv[jj];
       if constexpr (NORM) scale = rsqrtf(ss_row[rl] / (float)K + eps);
       if constexpr (EPI == EPI_SILU) {
 #pragma unroll
@@ -676,18 +746,15 @@ __global__ __launch_bounds__(NT) void prefill_gemm8_kernel(const bf16x8* __restr
                          acc[i][j + 2][jj] * scale, out, ldo, ea);
       } else if constexpr (EPI == EPI_QKV_ROPE) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int g = nt_i * (BN / 16) + bgi[j];
-          const int kk = g & 7;
-          const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
-          float2 c = float2{1.f, 0.f};
-          int slot = -1;
-          if (valid) {
-            c = ea.cs[(size_t)ea.pos[m] * 64 + dd];
-            slot = ea.slots[m];
-          }
-          epi_store<EPI>(m, valid, g, r, acc[i][j][jj] * scale, 0.f, out, ldo, ea, c, slot);
-        }
+        for (int j = 0; j < FN; ++j)
+          epi_store<EPI>(m, valid, nt_i * (BN / 16) + bgi[j], r, acc[i][j][jj] * scale, 0.f, out,
+                         ldo, ea, csv[jj][j], valid ? slotv[jj] : -1);
+      } else if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          if (valid)
+            reinterpret_cast<bf16*>(out)[(size_t)m * ldo + (nt_i * (BN / 16) + bgi[j]) * 16 + r] =
+                f2bf(resv[jj][j] + acc[i][j][jj] * scale);
       } else {
 #pragma unroll
         for (int j = 0; j < FN; ++j)
@@ -934,11 +1001,7 @@ static __global__ __launch_bounds__(256) void row_rstd_kernel(const bf16* __rest
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = (float)v[j][e];
-        s = fmaf(f, f, s);
-      }
+      s = sumsq8(v[j], s);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);

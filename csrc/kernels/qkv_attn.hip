@@ -105,11 +105,7 @@ __device__ __forceinline__ void producer(const QAArgs& a, int g, char* smem) {
 #pragma unroll
     for (int u = 0; u < QA_U; ++u) {
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[u], bw[u], acc, 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xf = (float)ax[u][j];
-        ss = fmaf(xf, xf, ss);
-      }
+      ss = sumsq8(ax[u], ss);
     }
   };
   const int n = s1 - s0, nb = n / QA_U;

@@ -112,12 +112,14 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
   // (0 = default), bits 16..23 = column groups per block (M > 16 only; 0 = 1)
   const int u_req = (waves >> 8) & 0xff;
   const int ng_req = (waves >> 16) & 0xff;
+  const int afrag = (waves >> 27) & 1;  // bit 27: X is fragment-major (p2p_pack_frag)
   waves &= 0xff;
   if (waves <= 0) waves = pick_waves(groups, K, mt);
   if (epi == EPI_SILU && mt == 4 && waves > 4) waves = 4;
   EpiArgs ea2 = ea;
   ea2.u = u_req;
   ea2.ng = ng_req;
+  ea2.afrag = afrag && !ea.moe_cnt;
   static const skinny_unit_fn units[] = {skinny_unit_store, skinny_unit_resid, skinny_unit_silu,
                                           skinny_unit_f32, skinny_unit_qkv_rope,
                                           skinny_unit_argmax, skinny_unit_ar};

@@ -70,13 +70,17 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 
   const bf16* xp[MT];
   bool xv[MT];
+  // fragment-major X (ea.afrag, p2p_pack_frag): A fragment (mt, s) is 1 KiB contiguous, so
+  // an A load is 8 whole cache lines instead of 16 half lines of 16 rows
+  const bool af = !MOE && ea.afrag;
+  const int xs = af ? 512 : 32;  // elements between consecutive k-steps of one lane
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int row = mt * 16 + r;
-    xv[mt] = row < M;
+    xv[mt] = af ? mt * 16 < M : row < M;
     int xrow = xv[mt] ? row : 0;
     if constexpr (MOE) xrow = xv[mt] ? mrows[row] / ea.x_div : 0;
-    xp[mt] = X + (size_t)xrow * ldx + 8 * q;
+    xp[mt] = af ? X + ((size_t)mt * (K >> 5) * 64 + lane) * 8 : X + (size_t)xrow * ldx + 8 * q;
   }
 
   // EPI_QKV_ROPE: fetch (cos, sin) and the KV slot of this lane's output rows now,
@@ -118,7 +122,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     for (int h = 0; h < KP; ++h)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        ax[h * MT + mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + (s * KP + h) * 32)
+        ax[h * MT + mt] = xv[mt] ? *reinterpret_cast<const bf16x8*>(xp[mt] + (size_t)(s * KP + h) * xs)
                                  : zero_bf16x8();
   };
   auto load = [&](int s, WR(&bw)[U][NW], bf16x8(&ax)[U][KP * MT]) {
@@ -141,13 +145,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 #pragma unroll
         for (int b = 0; b < NW; ++b)
           acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[b], acc[b][mt], 0, 0, 0);
-        if constexpr (NORM) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xf = (float)a[j];
-            ss[mt] = fmaf(xf, xf, ss[mt]);
-          }
-        }
+        if constexpr (NORM) ss[mt] = sumsq8(a, ss[mt]);
       }
     }
   };
@@ -185,6 +183,32 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     loadx(s, a1);
     compute1(b1, a1);
   }
+
+  // ---- epilogue operands, issued by the finishing wave (0) right after its main loop as
+  // one batch, so they land during the split-K reduction: the residual values (EPI_RESID)
+  // and, at NG > 1, the rows' (cos, sin) (EPI_QKV_ROPE).  Loaded element by element inside
+  // the store loop they were a chain of NG x MT x 4 dependent round trips (each store may
+  // alias the next load): +7 us on the 44-row qkv, +1 us per row-quad on the residual GEMMs.
+  float resv[NG][MT][4];
+  float2 csv[NG][MT][4];
+#pragma unroll
+  for (int c = 0; c < NG; ++c)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mt * 16 + q * 4 + j;
+        const bool ok = w == 0 && m < M;
+        resv[c][mt][j] = 0.f;
+        csv[c][mt][j] = float2{1.f, 0.f};
+        if constexpr (EPI == EPI_RESID && !MOE)
+          if (ok) resv[c][mt][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + (g0 + c) * 16 + r];
+        if constexpr (EPI == EPI_QKV_ROPE && NG > 1) {
+          const int kk = (g0 + c) & 7;
+          const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+          if (ok) csv[c][mt][j] = ea.cs[(size_t)rpos[mt][j] * 64 + dd];
+        }
+      }
 
   // ---- split-K reduction across the block's waves ----
   if constexpr (NORM) {
@@ -284,16 +308,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           else s1 = s0;
         }
         if constexpr (EPI == EPI_QKV_ROPE) {
-          float2 cs;
-          if constexpr (NG == 1) {
-            cs = rc[mt][j];
-          } else {
-            const int kk = g & 7;
-            const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
-            cs = m < M ? ea.cs[(size_t)rpos[mt][j] * 64 + dd] : float2{1.f, 0.f};
-          }
+          const float2 cs = NG == 1 ? rc[mt][j] : csv[c][mt][j];
           epi_store<EPI>(orow, m < M, g, r, acc[c][mt][j] * s0, 0.f, out, ldo, ea, cs,
                          rslot[mt][j]);
+        } else if constexpr (EPI == EPI_RESID && !MOE) {
+          if (m < M)
+            reinterpret_cast<bf16*>(out)[(size_t)orow * ldo + g * 16 + r] =
+                f2bf(resv[c][mt][j] + acc[c * NB][mt][j] * s0);
         } else {
           epi_store<EPI>(orow, m < M, g, r, acc[c * NB][mt][j] * s0,
                          acc[c * NB + NB - 1][mt][j] * s1, out, ldo, ea);

@@ -87,13 +87,7 @@ __global__ __launch_bounds__(NT) void tiled_gemm_kernel(const bf16x8* __restrict
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       a[adst[i]] = ra[i];
-      if constexpr (NORM) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = (float)ra[i][j];
-          ss[i] = fmaf(v, v, ss[i]);
-        }
-      }
+      if constexpr (NORM) ss[i] = sumsq8(ra[i], ss[i]);
     }
   };
 

@@ -33,6 +33,7 @@ namespace wide {
 
 constexpr int NT = 512;   // 8 waves
 constexpr int KC = 8;     // k-steps per chunk: wave w DMA-loads k-step w of every m-tile
+constexpr int MAX_SPLIT = 16;  // K slices per tile (the rstd reduction unrolls over them)
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 using pgemm::SplitArgs;
 
@@ -43,7 +44,14 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // tile = column block: 8 groups of 16 columns (SILU: waves 0-3 gate groups 4t..4t+3,
 // waves 4-7 the up groups 4t..4t+3 + up_off; output columns 64t..64t+63)
-template <int MT, int EPI, bool NORM, bool SPLIT>
+// chunks of a K slice whose activations fit LDS at once (the RES variant): <= 144 KiB
+template <int MT>
+constexpr int res_chunks() { return 18 / MT; }
+
+// RES: the slice's whole activation block is DMA'd into LDS up front (one barrier), so the
+// waves never meet again in the k loop and each streams its weights at its own pace;
+// otherwise the activations stream through a ring with a barrier per chunk.
+template <int MT, int EPI, bool NORM, bool SPLIT, bool RES>
 __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict__ Wt,
                                                        const bf16* __restrict__ X, int ldx, int M,
                                                        int K, int n_tiles, int up_off,
@@ -57,7 +65,8 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   constexpr int RING = D + 2;
   constexpr int SLOT = MT * KC * 64;  // bf16x8 per ring slot
   constexpr int PER_CHUNK = MT + KC;  // vmem instructions per thread per chunk
-  __shared__ __attribute__((aligned(16))) bf16x8 ring[RING * SLOT];
+  constexpr int NSLOT = RES ? res_chunks<MT>() : RING;
+  __shared__ __attribute__((aligned(16))) bf16x8 ring[NSLOT * SLOT];
   __shared__ float ss_l[2][4][16];
 
   const int splitk = SPLIT ? sp.splitk : 1;
@@ -78,22 +87,29 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     asrc[i] = X + (size_t)row * ldx + 32 * w + 8 * (lane >> 4);
   }
 
-  auto issue = [&](int c, bf16x8(&wr)[KC]) {
-    bf16x8* base = ring + ((c - c0) % RING) * SLOT;
+  auto issue_a = [&](int c) {
+    bf16x8* base = ring + ((c - c0) % NSLOT) * SLOT;
 #pragma unroll
     for (int i = 0; i < MT; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (size_t)c * KC * 32),
                                        (lds_ptr_t)(base + (i * KC + w) * 64), 16, 0, 0);
+  };
+  auto issue_w = [&](int c, bf16x8(&wr)[KC]) {
 #pragma unroll
     for (int k = 0; k < KC; ++k) wr[k] = __builtin_nontemporal_load(wsrc + (size_t)(c * KC + k) * 64);
   };
+  auto issue = [&](int c, bf16x8(&wr)[KC]) {
+    if constexpr (!RES) issue_a(c);
+    issue_w(c, wr);
+  };
 
+  constexpr int PC = RES ? KC : PER_CHUNK;  // vmem instructions per chunk in the k loop
   auto wait_chunks = [&](int k) {  // at most k chunks of this thread's loads in flight
     switch (k) {
       case 0: wait_vmcnt<0>(); break;
-      case 1: wait_vmcnt<PER_CHUNK>(); break;
-      case 2: wait_vmcnt<2 * PER_CHUNK>(); break;
-      default: wait_vmcnt<(D >= 3 ? 3 : 2) * PER_CHUNK>(); break;
+      case 1: wait_vmcnt<PC>(); break;
+      case 2: wait_vmcnt<2 * PC>(); break;
+      default: wait_vmcnt<(D >= 3 ? 3 : 2) * PC>(); break;
     }
   };
 
@@ -104,7 +120,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   const int sq_mt = w & 3, sq_par = w >> 2;
 
   auto compute = [&](int c, const bf16x8(&wr)[KC]) {
-    const bf16x8* base = ring + ((c - c0) % RING) * SLOT;
+    const bf16x8* base = ring + ((c - c0) % NSLOT) * SLOT;
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
       bf16x8 a[MT];
@@ -118,12 +134,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       if (sq_mt < MT) {
 #pragma unroll
         for (int k = 0; k < KC; k += 2) {
-          const bf16x8 v = base[(sq_mt * KC + k + sq_par) * 64 + lane];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float f = (float)v[e];
-            ss = fmaf(f, f, ss);
-          }
+          ss = sumsq8(base[(sq_mt * KC + k + sq_par) * 64 + lane], ss);
         }
       }
     }
@@ -133,6 +144,8 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   // computed; the counted wait + barrier makes chunk t complete (every wave's DMA part), and
   // the ring slot refilled at step t (chunk t+D's) was last read at t-2, before barrier t-1
   bf16x8 wr[RS][KC];
+  if constexpr (RES)  // the whole slice's activations first (host: n <= res_chunks)
+    for (int c = 0; c < n; ++c) issue_a(c0 + c);
 #pragma unroll
   for (int j = 0; j < D; ++j)
     if (j < n) issue(c0 + j, wr[j]);
@@ -143,8 +156,10 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       if (t >= n) break;
       if (t + D < n) issue(c0 + t + D, wr[(j + D) % RS]);
       wait_chunks(min(D, n - 1 - t));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if (!RES || t == 0) {  // RES: chunk 0's weights landed => this wave's DMA parts too
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
       compute(c0 + t, wr[j]);
     }
   }
@@ -157,8 +172,50 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   }
   const int r = lane & 15, q = lane >> 4;
 
-  // epilogue of one 16-column output group (g = global group index of epi_store)
-  auto epilogue = [&](int g, const f32x4 (&v)[MT], const f32x4 (&u)[MT], auto&& rstd_of) {
+  // The output group this wave finishes, if any: group w (SILU: gate/up pair w < 4); under
+  // split-K only slice (w % splitk) finishes it.
+  const bool fin = w < (SILU ? 4 : 8) && (!SPLIT || (w % splitk) == split);
+  const int g = SILU ? tile * 4 + w : tile * 8 + w;
+  // Epilogue operands, fetched as ONE batch per lane right after the main loop (they land
+  // while the slices meet): the residual values (EPI_RESID), the rows' positions, KV slots
+  // and (cos, sin) (EPI_QKV_ROPE).  Element-by-element in the epilogue they were a chain of
+  // MT x 4 dependent round trips per lane (a residual add loads, then stores, each element).
+  float res[MT][4];
+  float2 csv[MT][4];
+  int slotv[MT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = 16 * i + 4 * q + j;
+      const bool ok = fin && m < M;
+      res[i][j] = 0.f;
+      slotv[i][j] = -1;
+      csv[i][j] = float2{1.f, 0.f};
+      if constexpr (EPI == EPI_RESID)
+        if (ok) res[i][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + g * 16 + r];
+      if constexpr (EPI == EPI_QKV_ROPE)
+        if (ok) slotv[i][j] = ea.slots[m];
+    }
+  if constexpr (EPI == EPI_QKV_ROPE) {
+    const int kk = g & 7;
+    const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+    int posv[MT][4];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = 16 * i + 4 * q + j;
+        posv[i][j] = (fin && m < M) ? ea.pos[m] : -1;
+      }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (posv[i][j] >= 0) csv[i][j] = ea.cs[(size_t)posv[i][j] * 64 + dd];
+  }
+
+  auto epilogue = [&](const f32x4 (&v)[MT], const f32x4 (&u)[MT], auto&& rstd_of) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -167,15 +224,10 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
         const bool valid = m < M;
         const float sc = rstd_of(i, j);
         if constexpr (EPI == EPI_QKV_ROPE) {
-          const int kk = g & 7;
-          const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
-          float2 c = float2{1.f, 0.f};
-          int slot = -1;
-          if (valid) {
-            c = ea.cs[(size_t)ea.pos[m] * 64 + dd];
-            slot = ea.slots[m];
-          }
-          epi_store<EPI>(m, valid, g, r, v[i][j] * sc, 0.f, out, ldo, ea, c, slot);
+          epi_store<EPI>(m, valid, g, r, v[i][j] * sc, 0.f, out, ldo, ea, csv[i][j], slotv[i][j]);
+        } else if constexpr (EPI == EPI_RESID) {
+          if (valid)
+            reinterpret_cast<bf16*>(out)[(size_t)m * ldo + g * 16 + r] = f2bf(res[i][j] + v[i][j] * sc);
         } else {
           epi_store<EPI>(m, valid, g, r, v[i][j] * sc, u[i][j] * sc, out, ldo, ea);
         }
@@ -204,7 +256,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
 #pragma unroll
       for (int j = 0; j < 4; ++j) up[i][j] = SILU ? xch[((w * MT + i) * 4 + j) * 64 + lane] : 0.f;
     }
-    epilogue(SILU ? tile * 4 + w : tile * 8 + w, acc, up, [&](int i, int j) {
+    epilogue(acc, up, [&](int i, int j) {
       if constexpr (!NORM) return 1.f;
       const int rr = 4 * q + j;
       return rstd_from(ss_l[0][i][rr] + ss_l[1][i][rr]);
@@ -250,41 +302,80 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       }
     }
     __syncthreads();
-    // slice `split` finishes output groups o with o % splitk == split (SILU: 4 pairs)
-    const int o = w;
-    if (o >= (SILU ? 4 : 8) || (o % splitk) != split) return;
+    // every slice's partials are visible.  Rows' rstd: one lane per row sums the slices'
+    // row sums (all loads issued before the first add) into LDS
+    __shared__ float rstd_l[64];
+    if constexpr (NORM) {
+      if (tid < 16 * MT) {
+        float pv[MAX_SPLIT];
+#pragma unroll
+        for (int s2 = 0; s2 < MAX_SPLIT; ++s2)
+          pv[s2] = __hip_atomic_load(&sp.ss_slab[((size_t)tile * splitk + min(s2, splitk - 1)) * 64 + tid],
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float t2 = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < MAX_SPLIT; ++s2) t2 += s2 < splitk ? pv[s2] : 0.f;
+        rstd_l[tid] = rstd_from(t2);
+      }
+      __syncthreads();
+    }
+    if (!fin) return;
+    // the finished group's partials, summed in slice order; loads in batches of 4 slices
+    // (clamped indices: straight-line code, one wait per batch)
     f32x4 tot[MT], up[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       tot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       up[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    for (int s2 = 0; s2 < splitk; ++s2) {
+    for (int s0 = 0; s0 < splitk; s0 += 4) {
+      f32x4 pt[4][MT], pu[4][MT];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        tot[i] += pgemm::load_sc1(rsl, (int)((tile_v + (((size_t)s2 * 8 + o) * MT + i) * 64 + lane) * 16));
-        if constexpr (SILU)
-          up[i] += pgemm::load_sc1(rsl, (int)((tile_v + (((size_t)s2 * 8 + o + 4) * MT + i) * 64 + lane) * 16));
+      for (int s = 0; s < 4; ++s) {
+        const int s2 = min(s0 + s, splitk - 1);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          pt[s][i] = pgemm::load_sc1(rsl, (int)((tile_v + (((size_t)s2 * 8 + w) * MT + i) * 64 + lane) * 16));
+          if constexpr (SILU)
+            pu[s][i] = pgemm::load_sc1(rsl, (int)((tile_v + (((size_t)s2 * 8 + w + 4) * MT + i) * 64 + lane) * 16));
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (s0 + s >= splitk) break;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          tot[i] += pt[s][i];
+          if constexpr (SILU) up[i] += pu[s][i];
+        }
       }
     }
-    epilogue(SILU ? tile * 4 + o : tile * 8 + o, tot, up, [&](int i, int j) {
+    epilogue(tot, up, [&](int i, int j) {
       if constexpr (!NORM) return 1.f;
-      const int rr = 16 * i + 4 * q + j;
-      float t2 = 0.f;
-      for (int s2 = 0; s2 < splitk; ++s2)
-        t2 += __hip_atomic_load(&sp.ss_slab[((size_t)tile * splitk + s2) * 64 + rr],
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return rstd_from(t2);
+      return rstd_l[16 * i + 4 * q + j];
     });
   }
 }
 
-static int g_max_split = 16;
+static int g_max_split = MAX_SPLIT;
+static int g_res = 1;  // RES variant where a slice's activations fit LDS (A/B: 0 = ring only)
+
+template <int MT, int EPI, bool NORM, bool SPLIT, bool RES>
+int launch_v(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles, int up_off,
+             void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st,
+             const SplitArgs& sp) {
+  hipLaunchKernelGGL((wide_gemm_kernel<MT, EPI, NORM, SPLIT, RES>), dim3(n_tiles * sp.splitk),
+                     dim3(NT), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, n_tiles, up_off,
+                     out, ldo, eps, ea, sp);
+  return (int)hipGetLastError();
+}
 
 template <int MT, int EPI, bool NORM>
 int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles, int up_off,
               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st, int splitk) {
   using namespace pgemm;
+  const int nc = K / (32 * KC);
+  const bool res = g_res && (nc + splitk - 1) / splitk <= res_chunks<MT>();
   if (splitk > 1) {
     const size_t slab = (size_t)n_tiles * splitk * 8 * MT * 64 * sizeof(f32x4);
     const size_t ssb = (size_t)n_tiles * splitk * 64 * sizeof(float);
@@ -295,16 +386,12 @@ int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles,
     unsigned* ctr = (unsigned*)(ws + g_split_ws.bytes - kCounterBytes);
     constexpr size_t nw = kCounterBytes / sizeof(unsigned);
     SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), ctr, ctr + nw / 2, (int*)(ctr + nw - 1), 1};
-    hipLaunchKernelGGL((wide_gemm_kernel<MT, EPI, NORM, true>), dim3(n_tiles * splitk), dim3(NT), 0,
-                       st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, n_tiles, up_off, out, ldo,
-                       eps, ea, sp);
-    return (int)hipGetLastError();
+    return res ? launch_v<MT, EPI, NORM, true, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, sp)
+               : launch_v<MT, EPI, NORM, true, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, sp);
   }
   SplitArgs none{1, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
-  hipLaunchKernelGGL((wide_gemm_kernel<MT, EPI, NORM, false>), dim3(n_tiles), dim3(NT), 0, st,
-                     (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea,
-                     none);
-  return (int)hipGetLastError();
+  return res ? launch_v<MT, EPI, NORM, false, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none)
+             : launch_v<MT, EPI, NORM, false, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none);
 }
 
 // K slices: the grid must stay <= one block per CU (every slice of a tile resident for the
@@ -312,7 +399,8 @@ int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles,
 static int pick_split(int n_tiles, int nc, int req) {
   const int cus = pgemm::cu_count();
   if (cus <= 0) return 1;
-  int s = req > 0 ? std::min(req, nc) : std::min(cus / n_tiles, std::min(g_max_split, nc / 2));
+  int s = req > 0 ? std::min(std::min(req, nc), MAX_SPLIT)
+                  : std::min(cus / n_tiles, std::min(g_max_split, nc / 2));
   while (s > 1 && n_tiles * s > cus) --s;
   return std::max(1, s);
 }
@@ -384,4 +472,9 @@ extern "C" int p2p_wide_split_fault() {
 }
 
 // Benchmarks: cap on the K-slice count of the heuristic (1 = never split).
-P2P_API void p2p_wide_max_split(int s) { wide::g_max_split = s >= 1 ? s : 16; }
+// A/B: 1 = activations resident in LDS where a slice fits (default), 0 = the ring always.
+P2P_API void p2p_wide_resident(int on) { wide::g_res = on ? 1 : 0; }
+
+P2P_API void p2p_wide_max_split(int s) {
+  wide::g_max_split = (s >= 1 && s <= wide::MAX_SPLIT) ? s : wide::MAX_SPLIT;
+}

@@ -72,6 +72,7 @@ _SIGS = {
     "p2p_paged_attention_mfma": [c_int],
     "p2p_l3_prefetch": [c_void_p, ctypes.c_size_t, c_int, c_void_p, c_void_p],
     "p2p_gather_rows": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
+    "p2p_pack_frag": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "p2p_rope_cache": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "p2p_argmax": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],

@@ -154,6 +154,26 @@ MIDM_FLAG = 1 << 25
 # into VGPRs, split-K over workgroups); bits 8..15 = K slices (0 = heuristic); bf16 dense
 # weights, K % 256 == 0, 1 < M <= 64
 WIDE_FLAG = 1 << 26
+# launch-code bit: the skinny kernel's X is fragment-major (pack_frag), not row-major
+AFRAG_FLAG = 1 << 27
+
+
+def pack_frag(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Row-major [M, K] bf16 -> fragment-major copy (16-row m-tiles of K/32 MFMA A fragments,
+    padded rows zero) for the skinny GEMM's AFRAG_FLAG launches: every A-fragment load is
+    then 1 KiB contiguous.  Returns a [ceil(M/16)*16, K] buffer (fragment order inside)."""
+    M, K = x.shape
+    rows = (M + 15) // 16 * 16
+    if out is None:
+        out = torch.empty(rows, K, device=x.device, dtype=torch.bfloat16)
+    if x.device.type != "cuda":
+        xp = torch.zeros(rows, K, dtype=x.dtype)
+        xp[:M] = x
+        out.copy_(xp.reshape(rows // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(rows, K))
+        return out
+    _lib.check(_lib.lib().p2p_pack_frag(x.data_ptr(), x.stride(0), M, K, out.data_ptr(),
+                                        _lib.stream_ptr(x.device)), "pack_frag")
+    return out
 
 
 def _want_tiled(wt, M, N, K, epi, norm, waves) -> bool:

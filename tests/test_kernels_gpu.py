@@ -112,15 +112,46 @@ def test_midm_gemm_every_epilogue(M, K):
 
 
 @pytest.mark.parametrize("M", [2, 16, 17, 44, 64])
-@pytest.mark.parametrize("K,split", [(1024, 0), (1024, 1), (1536, 4), (2048, 3), (2048, 8)])
-def test_wide_gemm_every_epilogue(M, K, split):
+@pytest.mark.parametrize("K,split", [(1024, 0), (1024, 1), (1536, 4), (2048, 3), (2048, 8),
+                                     (5120, 1)])
+@pytest.mark.parametrize("res", [True, False])
+def test_wide_gemm_every_epilogue(M, K, split, res):
     """The wide mid-M kernel (launch-code bit ops.gemm.WIDE_FLAG: 8 waves x 16 columns share
     LDS activation chunks, split-K over workgroups with the parallel slab reduction) on every
-    epilogue vs fp32 references; 1536 / 4 slices gives slices of one and two chunks."""
+    epilogue vs fp32 references; 1536 / 4 slices gives slices of one and two chunks.  res:
+    the slice's activations resident in LDS where they fit (else, and with res off, the
+    ring); 5120 unsplit never fits (20 chunks)."""
+    from p2p_llm_chat_go_amd.ops import _lib
     from p2p_llm_chat_go_amd.ops.gemm import WIDE_FLAG
 
-    _every_epilogue(M, WIDE_FLAG | (split << 8), 2000 + M + K + split, K=K)
+    _lib.lib().p2p_wide_resident(int(res))
+    try:
+        _every_epilogue(M, WIDE_FLAG | (split << 8), 2000 + M + K + split, K=K)
+    finally:
+        _lib.lib().p2p_wide_resident(1)
     assert ops.tiled_split_fault() == 0
+
+
+@pytest.mark.parametrize("M", [3, 17, 44, 64])
+def test_skinny_gemm_fragment_major_x(M):
+    """AFRAG launches (X packed by ops.gemm.pack_frag) give the row-major launch's result on
+    the store / residual / SwiGLU epilogues."""
+    from p2p_llm_chat_go_amd.ops import gemm as G
+
+    torch.manual_seed(M)
+    K, N = 2048, 512
+    W = ops.tile_weight((torch.randn(N, K) * 0.05).to(torch.bfloat16)).to(DEV)
+    x = torch.randn(M, K).to(torch.bfloat16).to(DEV)
+    xp = G.pack_frag(x)
+    for epi, norm in ((ops.EPI_STORE, True), (ops.EPI_RESID, False), (ops.EPI_SILU, True)):
+        n_out = N // 2 if epi == ops.EPI_SILU else N
+        h = torch.randn(M, n_out).to(torch.bfloat16).to(DEV)
+        a, b = h.clone(), h.clone()
+        for code in (4, 2 | (4 << 8) | (2 << 16)):
+            ops.skinny_gemm(W, x, epi, norm=norm, out=a, waves=code)
+            ops.skinny_gemm(W, xp[:M], epi, norm=norm, out=b, waves=code | G.AFRAG_FLAG)
+            torch.cuda.synchronize()
+            assert torch.equal(a, b), (epi, code)
 
 
 def _every_epilogue(M, code, seed, K=1024):
