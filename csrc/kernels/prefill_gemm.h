@@ -955,6 +955,8 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
     case 5: return launch<64, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 6: return launch<320, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 7: return launch<192, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 8: return launch<384, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 9: return launch<448, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -967,6 +969,9 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
 // every weight column 2-3 times (25 % padding) while 256x256 pads up to 44 %.
 static int pick_tile(int M, int N) {
   if (M <= 64) return N % 128 == 0 ? 4 : 0;
+  // (one-m-tile 384 / 448-row tiles for 321-448 rows measured 1.1-1.3x SLOWER than the
+  // 128x128 split-K / phased 256x256 picks below: profiles/r3_prefill_tiles_384_448.jsonl;
+  // they stay selectable by tiled_config for A/B only)
   if (N % 128 == 0 && ((M > 128 && M <= 192) || (M > 256 && M <= 320)))
     return M <= 192 ? 7 : 6;
   const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};
@@ -1044,7 +1049,7 @@ static int prefill_dispatch(const void* Wt, const void* X, int ldx, int M, int K
   using namespace pgemm;
   if (M <= 0 || K % BK) return (int)hipErrorInvalidValue;
   int tile = g_prefill_tile ? g_prefill_tile : pick_tile(M, N);
-  const int bn = (tile == 3 || tile == 4 || tile == 6 || tile == 7) ? 128 : 256;
+  const int bn = (tile == 3 || tile == 4 || tile >= 6) ? 128 : 256;
   if (!tile || N % bn) return (int)hipErrorInvalidValue;
   const int up_off = (epi == EPI_SILU) ? N / 32 : 0;
   // normed projections from 128 rows: rstd by row_rstd_kernel, GEMM without in-loop sums
