@@ -35,7 +35,7 @@ def main():
                 best = None
                 for code in _configs(K, M, False, midm=False):
                     t = _graph_time(lambda: [ops.skinny_gemm(w, xin, epi, norm=norm, out=out,
-                                                             waves=code | flag)
+                                                             waves=code | flag, x_packed=bool(flag))
                                              for w in wts]) * 1000 / 32
                     if best is None or t < best[0]:
                         best = (t, describe(code))
@@ -46,7 +46,8 @@ def main():
             a = torch.zeros(M, n_out, device="cuda", dtype=torch.bfloat16)
             b = torch.zeros(M, n_out, device="cuda", dtype=torch.bfloat16)
             ops.skinny_gemm(wts[0], x, epi, norm=norm, out=a, waves=4)
-            ops.skinny_gemm(wts[0], xp[:M], epi, norm=norm, out=b, waves=4 | G.AFRAG_FLAG)
+            ops.skinny_gemm(wts[0], xp[:M], epi, norm=norm, out=b, waves=4 | G.AFRAG_FLAG,
+                            x_packed=True)
             row["max_diff"] = float((a.float() - b.float()).abs().max())
             print(json.dumps(row), flush=True)
         del wts

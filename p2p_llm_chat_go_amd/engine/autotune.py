@@ -66,6 +66,8 @@ def describe(code: int) -> str:
         return "tiled"
     if code & G.MIDM_FLAG:
         return "midm"
+    if code & G.AFRAG_FLAG:
+        return "packed+" + describe(code & ~G.AFRAG_FLAG)
     if code & G.WIDE_FLAG:
         sk = (code >> 8) & 0xff
         return "wide/s%s" % (sk if sk else "auto")
@@ -110,8 +112,13 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
             N, K = G.tiled_shape(wts[0])
             times = {}
             bf = not G._is_f8(wts[0])
-            for code in _configs(K, M, G.tiled_ok(N, K, epi) and bf, midm=bf,
-                                 wide=bf and G.wide_ok(N, K, epi)):
+            codes = _configs(K, M, G.tiled_ok(N, K, epi) and bf, midm=bf,
+                             wide=bf and G.wide_ok(N, K, epi))
+            if bf and epi == G.EPI_QKV_ROPE and M > 16:
+                # pack the activations fragment-major first (one extra launch, timed with the
+                # GEMM): measured to pay on the qkv shape only (profiles/r3_afrag_probe.jsonl)
+                codes += [c | G.AFRAG_FLAG for c in _configs(K, M) if (c >> 16) & 0xff]
+            for code in codes:
                 times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
             best = min(times, key=times.get)
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)

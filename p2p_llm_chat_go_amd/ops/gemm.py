@@ -158,6 +158,22 @@ WIDE_FLAG = 1 << 26
 AFRAG_FLAG = 1 << 27
 
 
+_PACK_BUF: dict = {}
+
+
+def _packed(x: torch.Tensor) -> torch.Tensor:
+    """x packed fragment-major into a per-device grow-only buffer (a captured graph keeps
+    the address: the buffer is sized at autotune time, before any capture)."""
+    M, K = x.shape
+    n = (M + 15) // 16 * 16 * K
+    buf = _PACK_BUF.get(x.device)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(max(n, 64 * 16384), device=x.device, dtype=torch.bfloat16)
+        _PACK_BUF[x.device] = buf
+    out = buf[:n].view((M + 15) // 16 * 16, K)
+    return pack_frag(x, out=out)[:M]
+
+
 def pack_frag(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """Row-major [M, K] bf16 -> fragment-major copy (16-row m-tiles of K/32 MFMA A fragments,
     padded rows zero) for the skinny GEMM's AFRAG_FLAG launches: every A-fragment load is
@@ -260,8 +276,11 @@ def _ref(wt, x, epi, norm, out, eps):
 
 
 def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: bool = False,
-                out: torch.Tensor | None = None, eps: float = 1e-5, waves: int = 0) -> torch.Tensor:
-    """out = epi(rstd(x) * x @ W^T) for x [M, K] with M <= 64 (rows > 64 are chunked)."""
+                out: torch.Tensor | None = None, eps: float = 1e-5, waves: int = 0,
+                x_packed: bool = False) -> torch.Tensor:
+    """out = epi(rstd(x) * x @ W^T) for x [M, K] with M <= 64 (rows > 64 are chunked).
+    A launch code with AFRAG_FLAG packs x fragment-major first (pack_frag) unless
+    ``x_packed`` says the caller already did (then x is pack_frag's output, rows <= 64)."""
     N, K = tiled_shape(wt)
     M = x.shape[0]
     assert x.shape[1] == K and x.dtype == torch.bfloat16, (x.shape, K, x.dtype)
@@ -286,9 +305,12 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
         xs = x[m0:m0 + mc]
         os_ = out[m0:m0 + mc]
         wp, sp = _wptr(wt)
+        code = _code(wt, mc, epi, norm, waves)
+        if code & AFRAG_FLAG and not x_packed:
+            xs = _packed(xs)  # a launch of its own: the autotuner times pack + GEMM together
         _lib.check(L.p2p_skinny_gemm(wp, xs.data_ptr(), x.stride(0), mc, K, N, epi,
                                      int(norm), os_.data_ptr(), out.stride(0), float(eps),
-                                     _code(wt, mc, epi, norm, waves), sp, s), "skinny_gemm")
+                                     code, sp, s), "skinny_gemm")
     return out
 
 
@@ -370,11 +392,15 @@ def qkv_rope_gemm(wt, x, pos, slots, cos_sin, n_heads, n_kv, q_out, k_cache, v_c
     for m0 in range(0, M, SKINNY_MAX_M):
         mc = min(SKINNY_MAX_M, M - m0)
         wp, sp = _wptr(wt)
+        code = _code(wt, mc, EPI_QKV_ROPE, True, waves)
+        xs = x[m0:m0 + mc]
+        if code & AFRAG_FLAG:
+            xs = _packed(xs)
         _lib.check(L.p2p_skinny_gemm_qkv_rope(
-            wp, x[m0:].data_ptr(), x.stride(0), mc, K, n_heads, n_kv,
+            wp, xs.data_ptr(), x.stride(0), mc, K, n_heads, n_kv,
             pos[m0:].data_ptr(), slots[m0:].data_ptr(), cos_sin.data_ptr(), q_out[m0:].data_ptr(),
             q_out.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), float(eps),
-            _code(wt, mc, EPI_QKV_ROPE, True, waves), sp, s), "skinny_gemm_qkv_rope")
+            code, sp, s), "skinny_gemm_qkv_rope")
     return q_out
 
 

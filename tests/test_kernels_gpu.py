@@ -149,9 +149,17 @@ def test_skinny_gemm_fragment_major_x(M):
         a, b = h.clone(), h.clone()
         for code in (4, 2 | (4 << 8) | (2 << 16)):
             ops.skinny_gemm(W, x, epi, norm=norm, out=a, waves=code)
-            ops.skinny_gemm(W, xp[:M], epi, norm=norm, out=b, waves=code | G.AFRAG_FLAG)
+            ops.skinny_gemm(W, xp[:M], epi, norm=norm, out=b, waves=code | G.AFRAG_FLAG,
+                            x_packed=True)
             torch.cuda.synchronize()
             assert torch.equal(a, b), (epi, code)
+            c = h.clone()  # the wrapper packs row-major x itself for an AFRAG launch code
+            for _ in range(2):
+                c.copy_(h)
+                ops.skinny_gemm(W, x, epi, norm=norm, out=c, waves=code | G.AFRAG_FLAG)
+            torch.cuda.synchronize()
+            if epi != ops.EPI_RESID:
+                assert torch.equal(a, c), (epi, code)
 
 
 def _every_epilogue(M, code, seed, K=1024):
