@@ -114,6 +114,10 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
             bf = not G._is_f8(wts[0])
             codes = _configs(K, M, G.tiled_ok(N, K, epi) and bf, midm=bf,
                              wide=bf and G.wide_ok(N, K, epi))
+            if bf and epi == G.EPI_ARGMAX and M == 1 and G.wide_ok(N, K, epi):
+                # the 1 GB LM head stream: the wide kernel's 8 x 3 chunks of weights in flight
+                # per workgroup against the skinny launches
+                codes += [G.WIDE_FLAG]
             if bf and epi == G.EPI_QKV_ROPE and M > 16:
                 # pack the activations fragment-major first (one extra launch, timed with the
                 # GEMM): measured to pay on the qkv shape only (profiles/r3_afrag_probe.jsonl)
