@@ -244,17 +244,32 @@ class LlamaModel:
         return logits
 
     def check_faults(self, ws: Workspace):
-        """Raise if a bounded wait timed out -- a fused kernel's cross-workgroup hand-off or
-        a one-shot TP collective whose peer never arrived (the tokens would be wrong);
-        costs one small device read, call where the host syncs anyway."""
-        if self.device.type == "cuda" and int(ws.err.item()) != 0:
-            ws.err.zero_()
-            raise RuntimeError("fused in-launch hand-off (qkv -> attention, attention -> "
-                               "o_proj) timed out (results invalid)")
-        if self.device.type == "cuda" and ops.tiled_split_fault():
-            raise RuntimeError("split-K GEMM slice wait timed out (results invalid)")
+        """Raise if a bounded wait timed out -- a fused kernel's cross-workgroup hand-off, a
+        split-K GEMM slice, or a one-shot TP collective whose peer never arrived (the tokens
+        would be wrong).  Call where the host syncs anyway (every rank of a TP/EP group at
+        the same point).  A kernel fault is local to the rank that saw it, so a group first
+        takes the MAX of the ranks' fault bits and every rank raises together (a follower
+        raising alone would split the group and surface later as a collective timeout);
+        a broken collective (CollectiveTimeout) raises at once -- the group cannot run
+        another collective."""
+        fault = 0
+        if self.device.type == "cuda":
+            if int(ws.err.item()) != 0:
+                ws.err.zero_()
+                fault |= 1
+            if ops.tiled_split_fault():
+                fault |= 2
         if self.comm is not None and hasattr(self.comm, "check"):
             self.comm.check()
+        if self.device.type == "cuda" and self.comm is not None and \
+                getattr(self.comm, "world", 1) > 1 and hasattr(self.comm, "max_int"):
+            fault = self.comm.max_int(fault)
+        if fault & 1:
+            raise RuntimeError("fused in-launch hand-off (qkv -> attention, attention -> "
+                               "o_proj) timed out on a rank of the group (results invalid)")
+        if fault & 2:
+            raise RuntimeError("split-K GEMM slice wait timed out on a rank of the group "
+                               "(results invalid)")
 
     def finalize_greedy(self, ws: Workspace, n: int, out=None):
         """keys -> token ids (TP: all-reduce MAX of the keys across vocab shards first)."""

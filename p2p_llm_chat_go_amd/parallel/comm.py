@@ -132,6 +132,15 @@ class TPComm:
         dist.all_to_all_single(a, b, out_splits, in_splits, group=self.group)
         return out
 
+    def max_int(self, v: int) -> int:
+        """MAX of a small int over the group (host value in, host value out): the ranks'
+        fault bits (LlamaModel.check_faults)."""
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" \
+            else torch.device("cpu")
+        t = torch.tensor([int(v)], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
     def check(self):
         """Raise if a one-shot collective timed out waiting for a peer."""
         if self.car is not None:

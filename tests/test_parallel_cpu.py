@@ -190,3 +190,37 @@ def test_tp_peer_death_raises_cpu():
             break
     assert rank == 0 and ok, info
     assert ps[1].exitcode == 3
+
+
+def _max_int_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    from p2p_llm_chat_go_amd.parallel.comm import TPComm
+
+    comm = TPComm()
+    # rank 1 alone saw a split-K fault (bit 2): every rank must see it (check_faults then
+    # raises on all of them together)
+    got = comm.max_int(2 if rank == 1 else 0)
+    dist.destroy_process_group()
+    _put_exit(q, (rank, got))
+
+
+def test_fault_bits_shared_across_group():
+    import multiprocessing as mp
+    import socket
+
+    ctx = mp.get_context("spawn")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_max_int_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(30)
+    assert res == [(0, 2), (1, 2)]
