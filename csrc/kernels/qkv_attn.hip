@@ -81,6 +81,17 @@ __device__ __forceinline__ void producer(const QAArgs& a, int g, char* smem) {
   const bf16* xp = a.X + (size_t)(xv ? r : 0) * a.ldx + 8 * q;
   const int head = g >> 3, kk = g & 7;
   const int d = (r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8);
+  // epilogue rows m = 4q + j: their positions / slots / (cos, sin) now, behind the stream
+  float2 rc[4];
+  int rslot[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = 4 * q + j;
+    const bool ok = m < a.M && w == 0;
+    rslot[j] = ok ? a.slots[m] : -1;
+    rc[j] = ok ? a.cs[(size_t)a.pos[m] * 64 + (d & 63)] : float2{1.f, 0.f};
+  }
+
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
   auto load = [&](int s, bf16x8(&bw)[QA_U], bf16x8(&ax)[QA_U]) {
@@ -123,22 +134,6 @@ __device__ __forceinline__ void producer(const QAArgs& a, int g, char* smem) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) ss = fmaf((float)a1[j], (float)a1[j], ss);
   }
-  // epilogue rows m = 4q + j: their slots / (cos, sin), issued by the finishing wave after
-  // its stream (they land during the split-K reduction; before the stream, the dependent
-  // pos -> cs pair held back wave 0's first weight loads by a round trip)
-  float2 rc[4];
-  int rslot[4];
-  int rpos[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int m = 4 * q + j;
-    const bool ok = m < a.M && w == 0;
-    rslot[j] = ok ? a.slots[m] : -1;
-    rpos[j] = ok ? a.pos[m] : -1;
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    rc[j] = rpos[j] >= 0 ? a.cs[(size_t)rpos[j] * 64 + (d & 63)] : float2{1.f, 0.f};
   // split-K over the block's waves
   ss += __shfl_xor(ss, 16, 64);
   ss += __shfl_xor(ss, 32, 64);

@@ -83,12 +83,15 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
     xp[mt] = af ? X + ((size_t)mt * (K >> 5) * 64 + lane) * 8 : X + (size_t)xrow * ldx + 8 * q;
   }
 
-  // EPI_QKV_ROPE: the KV slot and position of this lane's output rows now (independent
-  // loads that land behind the weight stream); the (cos, sin) they index is fetched right
-  // after the stream (a dependent pair here held the first weight loads back a round trip)
+  // EPI_QKV_ROPE: fetch (cos, sin) and the KV slot of this lane's output rows now,
+  // so the epilogue's dependent pos -> table loads overlap the weight stream.
+  // (NG > 1: the rows' slots/positions only; the table is read in the epilogue.)
+  float2 rc[MT][4];
   int rslot[MT][4];
   int rpos[MT][4];
   if constexpr (EPI == EPI_QKV_ROPE) {
+    const int kk = g0 & 7;
+    const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -99,6 +102,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
         const bool ok = m < M && w == 0;
         rslot[mt][j] = ok ? ea.slots[mm] : -1;
         rpos[mt][j] = ok ? ea.pos[mm] : 0;
+        if constexpr (NG == 1)
+          rc[mt][j] = ok ? ea.cs[(size_t)rpos[mt][j] * 64 + dd] : float2{1.f, 0.f};
       }
   }
 
@@ -198,7 +203,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
         csv[c][mt][j] = float2{1.f, 0.f};
         if constexpr (EPI == EPI_RESID && !MOE)
           if (ok) resv[c][mt][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + (g0 + c) * 16 + r];
-        if constexpr (EPI == EPI_QKV_ROPE) {  // (cos, sin) behind the stream, not before it
+        if constexpr (EPI == EPI_QKV_ROPE && NG > 1) {
           const int kk = (g0 + c) & 7;
           const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
           if (ok) csv[c][mt][j] = ea.cs[(size_t)rpos[mt][j] * 64 + dd];
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
           else s1 = s0;
         }
         if constexpr (EPI == EPI_QKV_ROPE) {
-          const float2 cs = csv[c][mt][j];
+          const float2 cs = NG == 1 ? rc[mt][j] : csv[c][mt][j];
           epi_store<EPI>(orow, m < M, g, r, acc[c][mt][j] * s0, 0.f, out, ldo, ea, cs,
                          rslot[mt][j]);
         } else if constexpr (EPI == EPI_RESID && !MOE) {
