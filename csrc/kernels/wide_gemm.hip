@@ -380,9 +380,9 @@ int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles,
     const size_t slab = (size_t)n_tiles * splitk * 8 * MT * 64 * sizeof(f32x4);
     const size_t ssb = (size_t)n_tiles * splitk * 64 * sizeof(float);
     char* ws = nullptr;
-    if ((size_t)n_tiles * sizeof(unsigned) >= kCounterBytes / 2 || !split_ws(slab + ssb, st, &ws) ||
-        slab + ssb >= 0x7FFFFFFF)
-      return (int)hipErrorInvalidValue;  // (the caller retries without splitting)
+    if ((size_t)n_tiles * sizeof(unsigned) >= kCounterBytes / 2 || slab + ssb >= 0x7FFFFFFF ||
+        !split_ws(slab + ssb, st, &ws))  // (no workspace growth while a graph is captured)
+      return launch_mt<MT, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, 1);
     unsigned* ctr = (unsigned*)(ws + g_split_ws.bytes - kCounterBytes);
     constexpr size_t nw = kCounterBytes / sizeof(unsigned);
     SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), ctr, ctr + nw / 2, (int*)(ctr + nw - 1), 1};
