@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--jitter", type=int, default=16,
                     help="reply lengths vary in [new-tokens - jitter, new-tokens]")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--max-prefill", type=int, default=1024,
+                    help="prefill rows per engine step (a burst of prompts beyond it waits a step)")
     ap.add_argument("--mixed", type=int, default=1,
                     help="1: running sequences ride in prefill steps (mixed batches)")
     ap.add_argument("--gpus", type=int, default=1, help="serve through engine.cluster on N GPUs")
@@ -50,7 +52,8 @@ def main():
     dev = torch.device(a.device, local) if a.device == "cuda" else torch.device(a.device)
     cfg = get_config(a.model)
     tok = get_tokenizer(cfg)
-    eng = Engine(cfg, device=dev, seed=7, max_batch=max(a.peers, 1), max_prefill_tokens=1024)
+    eng = Engine(cfg, device=dev, seed=7, max_batch=max(a.peers, 1),
+                 max_prefill_tokens=a.max_prefill)
     eng.warmup(tuple(sorted({1, 2, 4, 8, a.peers} - {0})), ctx=256)
     srv = EngineServer(eng, tok, max_batch=a.peers,
                        decode_chunk=int(os.environ.get("ENGINE_DECODE_CHUNK", "8")),

@@ -65,6 +65,11 @@ class EngineServer:
         # step (closed-loop peers resubmit at once; a free slot left for a whole decode
         # chunk costs batch occupancy): ENGINE_ADMIT_WAIT_US, default 500 us
         self.admit_wait_s = float(os.environ.get("ENGINE_ADMIT_WAIT_US", "500")) * 1e-6
+        # prefill-first: while prompts still wait after a prefill step (a burst larger than
+        # one step's prefill budget), run the next prefill before decoding the running set
+        # (their next tokens wait one prefill; the burst's last first token does not wait
+        # for decode chunks): ENGINE_PREFILL_FIRST, default on
+        self.prefill_first = os.environ.get("ENGINE_PREFILL_FIRST", "1") != "0"
         self.default_max_tokens = default_max_tokens
         self.max_ctx = max_ctx or min(engine.cfg.max_pos, CTX_BUCKETS[-1],
                                       engine.kv.num_pages * 64)
@@ -341,6 +346,8 @@ class EngineServer:
             self._stream(ids)
         running = [i for i in list(plan.decode) + list(plan.prefill)
                    if self.sched.get(i).state == 1]
+        if plan.prefill and self.prefill_first and self.sched.n_waiting > 0:
+            running = []  # the rest of the burst first (see prefill_first)
         if running:
             self._decode(eng, running)
         done = self._retire()
