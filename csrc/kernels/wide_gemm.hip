@@ -12,9 +12,10 @@
 //     through LDS as well and fills only 192 of 256 CUs at the qkv shape.
 // Here a workgroup of 8 waves owns 128 output columns (SwiGLU: 64 gate + the matching
 // 64 up columns) and a K slice:
-//   * the activation slice streams through a 3-slot LDS ring by LDS-DMA
-//     (global_load_lds_dwordx4, fragment-major image, conflict-free ds_read_b128) and
-//     is read by all 8 waves: 16 activation rows cost 1/8 of a weight byte, not 1;
+//   * the activation slice streams through an LDS ring of D + 2 chunk slots by LDS-DMA
+//     (global_load_lds_dwordx4, fragment-major image, conflict-free ds_read_b128), or sits
+//     in LDS whole when it fits (RES), and is read by all 8 waves: 16 activation rows cost
+//     1/8 of a weight byte, not 1;
 //   * each wave streams its OWN 16-column weight group straight into VGPRs (one 1 KiB
 //     non-temporal load per k-step, fragment-major in HBM), 2-3 chunks of 8 k-steps ahead
 //     (128-192 KiB of weights + the activation chunks in flight per CU: a one-chunk-ahead
@@ -26,6 +27,8 @@
 //     waves w with w % splitk == s, summing the slices in slice order (deterministic).
 // RMSNorm: the block squares the activation fragments it already holds in LDS (one
 // m-tile per wave pair); the row sums of the slices meet in the reduction.
+// Measured (docs/ARCHITECTURE.md "Wide mid-M family"): the autotuner's pick at 33-64 rows
+// for gate_up, down and qkv; the split-K seam (~5-6 us) is what it still pays on N <= 6144.
 #define PGEMM_NO_DISPATCH
 #include "prefill_gemm.h"
 
@@ -42,12 +45,12 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// tile = column block: 8 groups of 16 columns (SILU: waves 0-3 gate groups 4t..4t+3,
-// waves 4-7 the up groups 4t..4t+3 + up_off; output columns 64t..64t+63)
 // chunks of a K slice whose activations fit LDS at once (the RES variant): <= 144 KiB
 template <int MT>
 constexpr int res_chunks() { return 18 / MT; }
 
+// tile = column block: 8 groups of 16 columns (SILU: waves 0-3 gate groups 4t..4t+3,
+// waves 4-7 the up groups 4t..4t+3 + up_off; output columns 64t..64t+63).
 // RES: the slice's whole activation block is DMA'd into LDS up front (one barrier), so the
 // waves never meet again in the k loop and each streams its weights at its own pace;
 // otherwise the activations stream through a ring with a barrier per chunk.
