@@ -955,8 +955,6 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
     case 5: return launch<64, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 6: return launch<320, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 7: return launch<192, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
-    case 8: return launch<384, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
-    case 9: return launch<448, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -970,8 +968,8 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
 static int pick_tile(int M, int N) {
   if (M <= 64) return N % 128 == 0 ? 4 : 0;
   // (one-m-tile 384 / 448-row tiles for 321-448 rows measured 1.1-1.3x SLOWER than the
-  // 128x128 split-K / phased 256x256 picks below: profiles/r3_prefill_tiles_384_448.jsonl;
-  // they stay selectable by tiled_config for A/B only)
+  // 128x128 split-K / phased 256x256 picks below and were removed:
+  // profiles/r3_prefill_tiles_384_448.jsonl)
   if (N % 128 == 0 && ((M > 128 && M <= 192) || (M > 256 && M <= 320)))
     return M <= 192 ? 7 : 6;
   const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};

@@ -234,7 +234,7 @@ P2P_API int p2p_tiled_split_fault() {
 
 P2P_API void p2p_tiled_gemm_config(int version, int tile, int splitk) {
   if (version == 1 || version == 2) g_tiled_version = version;
-  g_prefill_tile = (tile >= 0 && tile <= 9) ? tile : 0;
+  g_prefill_tile = (tile >= 0 && tile <= 7) ? tile : 0;
   pgemm::g_splitk = splitk >= 0 ? splitk : 0;
 }
 
