@@ -31,22 +31,28 @@ def main():
     for _ in range(3):
         eng.prefill(prompts, pages).cpu()
     torch.cuda.synchronize()
-    walls, gpus = [], []
+    walls, gpus, enq = [], [], []
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(a.iters):
         t0 = time.perf_counter()
         e0.record()
         first = eng.prefill(prompts, pages)
         e1.record()
+        enq.append((time.perf_counter() - t0) * 1e3)  # host: every launch enqueued
         first.cpu()
         walls.append((time.perf_counter() - t0) * 1e3)
         torch.cuda.synchronize()
         gpus.append(e0.elapsed_time(e1))
     walls.sort()
     gpus.sort()
+    enq.sort()
     print(json.dumps({"model": cfg.name, "peers": a.peers, "prompt_tokens": len(prompts[0]),
                       "prefill_wall_ms_p50": round(walls[len(walls) // 2], 3),
                       "prefill_gpu_event_ms_p50": round(gpus[len(gpus) // 2], 3),
+                      # host time to enqueue the whole prefill (launch-bound when close
+                      # to the wall time: the GPU then waits on the host)
+                      "prefill_host_enqueue_ms_p50": round(enq[len(enq) // 2], 3),
+                      "prefill_graph": bool(getattr(eng, "prefill_graphs_enabled", False)),
                       "tuning": {"%s@M%d" % k: "%s %.1fus" % v for k, v in eng.tuning.items()}}),
           flush=True)
 

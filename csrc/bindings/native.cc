@@ -319,6 +319,29 @@ PYBIND11_MODULE(_native, m) {
     }
     return py::bytes(out);
   }, py::arg("key_type"), py::arg("payload"), py::arg("security") = "noise");
+  // Fault injection (SURVEY §5 "drop connection mid-stream"): a throw-away host dials
+  // `addr` (…/p2p/<id>), opens a /p2p-llm-chat/1.0.0 stream, writes `payload` and then
+  // ends it with `mode`: "close" (FIN: a well-formed send, the reference's s.Close()) or
+  // "reset" (RST before EOF: the receiver's io.ReadAll fails, go/cmd/node/main.go:160-164).
+  m.def("chat_inject", [](const std::string& addr, const py::bytes& payload,
+                          const std::string& mode) {
+    std::string data = payload;
+    py::gil_scoped_release rel;
+    PeerId pid;
+    Multiaddr ma = Multiaddr::parse(addr).without_peer(&pid);
+    auto h = std::make_shared<Host>(PrivateKey::generate(KeyType::Ed25519));
+    h->connect(pid, {ma}, 5000);
+    StreamCtx s = h->new_stream(pid, kChatProto, 5000);
+    s.io->write_all(data);
+    if (mode == "reset") {
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));  // partial bytes arrive first
+      s.stream->reset();
+    } else {
+      s.stream->close();
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    h->close();
+  }, py::arg("addr"), py::arg("payload"), py::arg("mode") = "reset");
   m.def("quic_echo", [](const std::string& kt, const py::bytes& payload, double drop, int streams,
                         uint64_t ku_interval) {
     std::string in = payload;

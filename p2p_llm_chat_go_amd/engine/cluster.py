@@ -44,6 +44,7 @@ import threading
 import time
 import traceback
 from concurrent.futures import Future
+from concurrent.futures import TimeoutError as FutureTimeout
 
 
 def _free_port() -> int:
@@ -61,8 +62,9 @@ class LockstepEngine:
     Everything else (cfg, kv, limits) is the local engine's.
 
     ``dp_split`` (EP ``a2a`` mode: DP attention + expert all-to-all): each sequence lives
-    on ONE rank (its home: first KV page id mod world), so the group serves world x the
-    sequences of a replicated-attention group.  A prefill / decode call is split by home;
+    on ONE rank (its home, chosen once when the sequence is admitted: the rank with the
+    fewest live sequences, ties rotating; kept keyed by the sequence's first KV page), so
+    the group serves world x the sequences of a replicated-attention group.  A prefill / decode call is split by home;
     every rank runs its share padded to the group's largest share (equal row counts and
     chunking, as the static-capacity all-to-all needs), followers send their tokens back
     over the pipe, and the leader reassembles them in call order."""
@@ -73,6 +75,9 @@ class LockstepEngine:
         self._lock = threading.Lock()
         self.dp_split = dp_split
         self.world = 1 + len(self._conns)
+        self._homes = {}   # dp_split: first KV page of a sequence -> its home rank
+        self._load = [0] * self.world  # live sequences per rank (as of the last decode call)
+        self._rr = 0
 
     def __getattr__(self, name):
         return getattr(self._eng, name)
@@ -90,8 +95,30 @@ class LockstepEngine:
                 p.resolved_seed()
 
     # ------------------------------------------------------------ dp_split
-    def _parts(self, block_tables):
-        homes = [bt[0] % self.world for bt in block_tables]
+    def _parts(self, block_tables, fresh=(), decode=False):
+        """Split a call's sequences by home rank.  ``fresh``: indices of sequences admitted
+        by this call (a prompt from position 0): each gets a home now, on the rank with the
+        fewest live sequences (ties rotate).  Deriving the home from the page id instead
+        piles sequences onto a few ranks whenever the allocator's page pattern shares a
+        factor with the world size.  A decode call carries every running
+        sequence, so it refreshes the live counts."""
+        fresh = set(fresh)
+        homes = [None if b in fresh else self._homes.get(bt[0])
+                 for b, bt in enumerate(block_tables)]
+        load = [0] * self.world if decode else list(self._load)
+        if decode:
+            for h in homes:
+                if h is not None:
+                    load[h] += 1
+        W = self.world
+        for b, bt in enumerate(block_tables):
+            if homes[b] is None:
+                h = min(range(W), key=lambda r: (load[r], (r - self._rr) % W))
+                self._rr = (h + 1) % W
+                homes[b] = h
+                load[h] += 1
+                self._homes[bt[0]] = h
+        self._load = load
         return [[b for b, h in enumerate(homes) if h == r] for r in range(self.world)]
 
     @staticmethod
@@ -108,7 +135,8 @@ class LockstepEngine:
         return msg[1]
 
     def _prefill_split(self, prompts, block_tables, return_logits, sampling, starts):
-        parts = self._parts(block_tables)
+        parts = self._parts(block_tables, fresh=[b for b in range(len(prompts))
+                                                 if not starts or starts[b] == 0])
         rows = [sum(len(prompts[b]) - (starts[b] if starts else 0) for b in part)
                 for part in parts]
         pad = max(1, max(rows))
@@ -141,7 +169,7 @@ class LockstepEngine:
         return (first, logits.to(dev)) if return_logits else first
 
     def _decode_split(self, last_ids, pos, block_tables, ctx, k, params):
-        parts = self._parts(block_tables)
+        parts = self._parts(block_tables, decode=True)
         bmax = max(1, max(len(p) for p in parts))
         for r, c in enumerate(self._conns, start=1):
             idx = parts[r]
@@ -575,7 +603,13 @@ class ClusterServer:
             raise RuntimeError("no live engine replica (%s)" % errs)
         return min(live, key=lambda r: (r.outstanding, r.idx))
 
-    def _call(self, kind, text, emit=None, timeout=600.0):
+    def _call(self, kind, text, emit=None, timeout=None):
+        """Route one request.  The replica's EngineServer enforces ENGINE_TIMEOUT itself
+        (cancel + error reply); this side waits a little longer as a backstop for a
+        replica that stopped answering altogether, then cancels and gives up."""
+        if timeout is None:
+            t = float(os.environ.get("ENGINE_TIMEOUT", "60"))
+            timeout = t + 5.0 if t > 0 else None
         rep = self._pick()
         rid = next(self._rid)
         fut = Future()
@@ -585,7 +619,22 @@ class ClusterServer:
         with rep.lock:
             rep.outstanding += 1
         self._send(rep, (kind, rid, text))
-        return fut.result(timeout)
+        try:
+            return fut.result(timeout)
+        except FutureTimeout:
+            with self._wlock:
+                gone = self._waiters.pop(rid, None) is not None
+            if gone:
+                with rep.lock:
+                    rep.outstanding -= 1
+                try:
+                    self._send(rep, ("cancel", rid))
+                except Exception:  # noqa: BLE001 -- the replica is already marked dead
+                    pass
+            from .server import EngineTimeout
+
+            raise EngineTimeout("engine replica %d did not answer within %gs" % (rep.idx, timeout)) \
+                from None
 
     # ------------------------------------------------------------- hooks
     def handle_json(self, req_text: str) -> str:

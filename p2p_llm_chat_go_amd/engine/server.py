@@ -21,6 +21,7 @@ import os
 import threading
 import time
 from concurrent.futures import Future
+from concurrent.futures import TimeoutError as FutureTimeout
 
 import torch
 
@@ -48,6 +49,12 @@ class _RiderRow:
         return self.tok
 
 
+class EngineTimeout(TimeoutError):
+    """A request got no reply within the engine deadline (ENGINE_TIMEOUT); it was
+    cancelled.  The node answers /suggest with 503 "LLM unavailable: ..." -- the reference
+    UI's 60 s bound on the co-pilot call (`web/streamlit_app.py:95,99-101`)."""
+
+
 class EngineServer:
     def __init__(self, engine: Engine, tokenizer=None, model_name: str = "llama3.1",
                  max_batch: int | None = None, decode_chunk: int = 8,
@@ -71,6 +78,13 @@ class EngineServer:
         # for decode chunks): ENGINE_PREFILL_FIRST, default on
         self.prefill_first = os.environ.get("ENGINE_PREFILL_FIRST", "1") != "0"
         self.default_max_tokens = default_max_tokens
+        # per-request deadline (s): the reference UI bounds the co-pilot call at 60 s
+        # (`web/streamlit_app.py:95`); past it the request is cancelled (KV pages freed at
+        # the next step) and the caller gets EngineTimeout.  ENGINE_TIMEOUT=0: no deadline
+        self.request_timeout_s = float(os.environ.get("ENGINE_TIMEOUT", "60"))
+        # fault injection (SURVEY §5 "stall engine"): the loop sleeps until this time
+        # before its next step (stall(); ENGINE_FAULT_STALL_S stalls the first step)
+        self._stall_until = time.perf_counter() + float(os.environ.get("ENGINE_FAULT_STALL_S", "0"))
         self.max_ctx = max_ctx or min(engine.cfg.max_pos, CTX_BUCKETS[-1],
                                       engine.kv.num_pages * 64)
         N = load_native()
@@ -133,8 +147,24 @@ class EngineServer:
             self._cancels.add(fut)
             self._lock.notify()
 
-    def generate(self, prompt_ids, params: SamplingParams, timeout: float = 600.0) -> dict:
-        return self.submit(prompt_ids, params).result(timeout)
+    def generate(self, prompt_ids, params: SamplingParams, timeout: float | None = None) -> dict:
+        """Blocking request with the engine deadline (``timeout`` s, default
+        ENGINE_TIMEOUT): on expiry the request is cancelled and EngineTimeout raised."""
+        t = self.request_timeout_s if timeout is None else float(timeout)
+        fut = self.submit(prompt_ids, params)
+        try:
+            return fut.result(t if t > 0 else None)
+        except FutureTimeout:
+            self.cancel(fut)
+            raise EngineTimeout("engine did not answer within %gs (request cancelled)" % t) \
+                from None
+
+    def stall(self, seconds: float):
+        """Fault injection: the engine loop takes no step for ``seconds`` (tests of the
+        request deadline; a hung GPU looks like this from the HTTP side)."""
+        with self._lock:
+            self._stall_until = time.perf_counter() + float(seconds)
+            self._lock.notify()
 
     def close(self):
         with self._lock:
@@ -192,6 +222,8 @@ class EngineServer:
             ids = self.tok.chat_ids(req.get("prompt", ""))
         q = queue.Queue()
         fut = self.submit(ids, params, on_tokens=q.put)
+        t_lim = self.request_timeout_s
+        deadline = time.perf_counter() + t_lim if t_lim > 0 else None
         model = req.get("model", self.model_name)
         toks, text_sent, alive = [], "", True
 
@@ -223,6 +255,10 @@ class EngineServer:
             except queue.Empty:
                 if fut.done() and q.empty():
                     break
+                if deadline is not None and time.perf_counter() > deadline:
+                    self.cancel(fut)
+                    raise EngineTimeout("engine did not answer within %gs (request "
+                                        "cancelled)" % t_lim)
         r = fut.result()
         toks = r["tokens"]
         flush(final=True)
@@ -274,6 +310,10 @@ class EngineServer:
                 while (not self._stop and not self._pending and self.sched.n_running == 0
                        and self.sched.n_waiting == 0):
                     self._lock.wait(timeout=0.5)
+                if self._stop:
+                    break
+                while not self._stop and time.perf_counter() < self._stall_until:
+                    self._lock.wait(timeout=min(0.05, self._stall_until - time.perf_counter()))
                 if self._stop:
                     break
             t_busy = time.perf_counter()
@@ -351,14 +391,18 @@ class EngineServer:
         if running:
             self._decode(eng, running)
         done = self._retire()
-        if done and self.admit_wait_s > 0:
+        free = self.max_batch - self.sched.n_running - self.sched.n_waiting
+        if done and free > 0 and self.admit_wait_s > 0:
             # replies just went out: their peers (or queued clients) usually send the next
             # requests within a fraction of a millisecond -- admit them at THIS step
             # boundary instead of leaving their batch slots idle for a whole step.  Wait
-            # (bounded) until as many requests are pending as replies were sent.
+            # (bounded) until as many requests are pending as replies were sent, capped by
+            # the free slots (already-queued requests fill slots first; with no free slot
+            # an arrival could not be admitted anyway, so the running batch never waits)
+            want = min(done, free)
             deadline = time.perf_counter() + self.admit_wait_s
             with self._lock:
-                while len(self._pending) < done and not self._stop:
+                while len(self._pending) < want and not self._stop:
                     left = deadline - time.perf_counter()
                     if left <= 0:
                         break

@@ -249,9 +249,10 @@ class LlamaModel:
         would be wrong).  Call where the host syncs anyway (every rank of a TP/EP group at
         the same point).  A kernel fault is local to the rank that saw it, so a group first
         takes the MAX of the ranks' fault bits and every rank raises together (a follower
-        raising alone would split the group and surface later as a collective timeout);
-        a broken collective (CollectiveTimeout) raises at once -- the group cannot run
-        another collective."""
+        raising alone would split the group and surface later as a collective timeout).
+        A rank's own one-shot timeout (comm.check) is fault bit 4: it too is shared
+        before raising, so the peers raise CollectiveTimeout with it instead of blocking
+        in the MAX collective until the process-group timeout."""
         fault = 0
         if self.device.type == "cuda":
             if int(ws.err.item()) != 0:
@@ -259,11 +260,25 @@ class LlamaModel:
                 fault |= 1
             if ops.tiled_split_fault():
                 fault |= 2
+        local_timeout = None
         if self.comm is not None and hasattr(self.comm, "check"):
-            self.comm.check()
-        if self.device.type == "cuda" and self.comm is not None and \
-                getattr(self.comm, "world", 1) > 1 and hasattr(self.comm, "max_int"):
+            try:
+                self.comm.check()
+            except Exception as e:  # noqa: BLE001 -- raised below, after the group agrees
+                local_timeout = e
+                fault |= 4
+        if self.comm is not None and getattr(self.comm, "world", 1) > 1 and \
+                hasattr(self.comm, "max_int"):
+            # every rank takes part in the MAX before anyone raises, so a rank whose own
+            # one-shot wait timed out does not leave its peers blocked in this collective
             fault = self.comm.max_int(fault)
+        if fault & 4:
+            if local_timeout is not None:
+                raise local_timeout
+            from ..parallel.custom_ar import CollectiveTimeout
+
+            raise CollectiveTimeout("a one-shot collective timed out on a peer rank of the "
+                                    "group (the TP group is broken)")
         if fault & 1:
             raise RuntimeError("fused in-launch hand-off (qkv -> attention, attention -> "
                                "o_proj) timed out on a rank of the group (results invalid)")

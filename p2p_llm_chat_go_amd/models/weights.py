@@ -102,8 +102,20 @@ class EngineWeights:
         qs, ks = nh // tp_size * D, nkv // tp_size * D
         dev = torch.device(device)
 
-        def get(name):
-            return sd[name].to(dev)
+        sliced = hasattr(sd, "get_rows_cols")
+
+        def get(name, rows=None, cols=None):
+            """The [rows, cols] slice of a tensor on the target device.  A LazySafetensors
+            store reads only that slice from disk (safetensors get_slice), so a TP rank
+            moves only its own shard of each sharded tensor."""
+            if sliced:
+                return sd.get_rows_cols(name, rows, cols).to(dev)
+            t = sd[name]
+            if rows is not None:
+                t = t[rows[0]:rows[1]]
+            if cols is not None:
+                t = t[:, cols[0]:cols[1]]
+            return t.to(dev)
 
         def tile(w):
             return ops.tile_weight(w.to(torch.bfloat16).contiguous())
@@ -113,13 +125,13 @@ class EngineWeights:
             p = "model.layers.%d." % i
             g_in = get(p + "input_layernorm.weight")
             g_post = get(p + "post_attention_layernorm.weight")
-            q = get(p + "self_attn.q_proj.weight")[tp_rank * qs:(tp_rank + 1) * qs]
-            k = get(p + "self_attn.k_proj.weight")[tp_rank * ks:(tp_rank + 1) * ks]
-            v = get(p + "self_attn.v_proj.weight")[tp_rank * ks:(tp_rank + 1) * ks]
+            q = get(p + "self_attn.q_proj.weight", rows=(tp_rank * qs, (tp_rank + 1) * qs))
+            k = get(p + "self_attn.k_proj.weight", rows=(tp_rank * ks, (tp_rank + 1) * ks))
+            v = get(p + "self_attn.v_proj.weight", rows=(tp_rank * ks, (tp_rank + 1) * ks))
             qkv = ops.fold_norm(torch.cat([q, k, v], 0), g_in)
             # fused qkv+RoPE epilogue row order (ops.rope_row_perm)
             qkv = qkv[ops.rope_row_perm(qkv.shape[0] // D, D).to(qkv.device)]
-            o = get(p + "self_attn.o_proj.weight")[:, tp_rank * qs:(tp_rank + 1) * qs]
+            o = get(p + "self_attn.o_proj.weight", cols=(tp_rank * qs, (tp_rank + 1) * qs))
             lw = LayerWeights(qkv=tile(qkv), o=tile(o))
             if cfg.is_moe:
                 E = cfg.n_experts
@@ -131,23 +143,24 @@ class EngineWeights:
                 Fs = F // tp_size
                 for e in range(ep_rank * el, (ep_rank + 1) * el):
                     q_ = p + "block_sparse_moe.experts.%d." % e
-                    w1 = get(q_ + "w1.weight")[tp_rank * Fs:(tp_rank + 1) * Fs]
-                    w3 = get(q_ + "w3.weight")[tp_rank * Fs:(tp_rank + 1) * Fs]
+                    w1 = get(q_ + "w1.weight", rows=(tp_rank * Fs, (tp_rank + 1) * Fs))
+                    w3 = get(q_ + "w3.weight", rows=(tp_rank * Fs, (tp_rank + 1) * Fs))
                     w13.append(tile(ops.fold_norm(torch.cat([w1, w3], 0), g_post)))
-                    w2.append(tile(get(q_ + "w2.weight")[:, tp_rank * Fs:(tp_rank + 1) * Fs]))
+                    w2.append(tile(get(q_ + "w2.weight", cols=(tp_rank * Fs, (tp_rank + 1) * Fs))))
                 lw.w13 = torch.stack(w13).contiguous()
                 lw.w2 = torch.stack(w2).contiguous()
             else:
                 Fs = F // tp_size
-                gate = get(p + "mlp.gate_proj.weight")[tp_rank * Fs:(tp_rank + 1) * Fs]
-                up = get(p + "mlp.up_proj.weight")[tp_rank * Fs:(tp_rank + 1) * Fs]
+                gate = get(p + "mlp.gate_proj.weight", rows=(tp_rank * Fs, (tp_rank + 1) * Fs))
+                up = get(p + "mlp.up_proj.weight", rows=(tp_rank * Fs, (tp_rank + 1) * Fs))
                 lw.gate_up = tile(ops.fold_norm(torch.cat([gate, up], 0), g_post))
-                lw.down = tile(get(p + "mlp.down_proj.weight")[:, tp_rank * Fs:(tp_rank + 1) * Fs])
+                lw.down = tile(get(p + "mlp.down_proj.weight", cols=(tp_rank * Fs, (tp_rank + 1) * Fs)))
             layers.append(lw)
         embed = get("model.embed_tokens.weight").to(torch.bfloat16).contiguous()
-        head = embed if cfg.tie_embeddings else get("lm_head.weight")
         Vs = cfg.vocab // tp_size
-        head = ops.fold_norm(head[tp_rank * Vs:(tp_rank + 1) * Vs], get("model.norm.weight"))
+        vrows = (tp_rank * Vs, (tp_rank + 1) * Vs)
+        head = embed[vrows[0]:vrows[1]] if cfg.tie_embeddings else get("lm_head.weight", rows=vrows)
+        head = ops.fold_norm(head, get("model.norm.weight"))
         return cls(cfg, embed, tile(head), layers, tp_rank, tp_size, ep_rank, ep_size)
 
     @classmethod
@@ -192,9 +205,11 @@ class EngineWeights:
 
 class LazySafetensors:
     """Read-on-access view of an HF checkpoint directory's ``*.safetensors`` shards (no
-    pickle).  ``EngineWeights.from_state_dict`` takes one tensor at a time and keeps only
-    its rank's slice, so a TP rank never holds the whole checkpoint in host memory (a 70B
-    checkpoint is ~140 GB; eight ranks each loading it whole would be ~1.1 TB)."""
+    pickle).  ``EngineWeights.from_state_dict`` asks for one tensor slice at a time
+    (``get_rows_cols``), and only that slice is read from disk (safetensors ``get_slice``):
+    a TP rank reads and holds only its own shard of every sharded tensor (a 70B checkpoint
+    is ~140 GB; eight ranks each reading it whole would be ~1.1 TB of I/O).  Replicated
+    tensors (norm gains, the embedding table, the MoE router) are read whole."""
 
     def __init__(self, path: str):
         from safetensors import safe_open
@@ -219,6 +234,15 @@ class LazySafetensors:
 
     def __getitem__(self, name):
         return self._handles[self._where[name]].get_tensor(name)
+
+    def get_rows_cols(self, name, rows=None, cols=None):
+        """tensor[rows[0]:rows[1], cols[0]:cols[1]] read from disk as that slice only."""
+        if rows is None and cols is None:
+            return self[name]
+        sl = self._handles[self._where[name]].get_slice(name)
+        r = slice(*rows) if rows is not None else slice(None)
+        c = slice(*cols) if cols is not None else slice(None)
+        return sl[r, c] if len(sl.get_shape()) > 1 else sl[r]
 
 
 def load_safetensors_dir(path: str, device="cpu") -> dict:

@@ -39,6 +39,10 @@ class CollectiveTimeout(RuntimeError):
     """A one-shot collective gave up waiting for a peer rank (dead or hung)."""
 
 
+# ranks the fused all-reduce epilogue's buffer holds (csrc/kernels/fused_ar.h FAR_MAX_RANKS)
+FAR_MAX_RANKS = 8
+
+
 class CustomAllReduce:
     MAX_RANKS = 8
 
@@ -155,8 +159,9 @@ class CustomAllReduce:
 
     def fused_ok(self, M: int, N: int, ld: int) -> bool:
         """Can ops.skinny_gemm_ar sum an [M, N] partial (row stride ld) through the fused
-        buffer?"""
-        return 1 <= M <= 64 and N % 16 == 0 and N // 16 <= 1024 and ld % 8 == 0 and \
+        buffer?  (A group wider than the kernel's FAR_MAX_RANKS takes the partial store +
+        one-shot path instead.)"""
+        return self.world <= FAR_MAX_RANKS and 1 <= M <= 64 and N % 16 == 0 and N // 16 <= 1024 and ld % 8 == 0 and \
             ((M - 1) * ld + N) * 4 <= self.far_max_bytes
 
     def close(self):

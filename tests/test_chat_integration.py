@@ -628,3 +628,41 @@ def test_inbox_cap_keeps_newest(procs):
                 break
             time.sleep(0.02)
     assert [m["content"] for m in inbox] == ["m2", "m3", "m4"]
+
+
+def test_stream_reset_mid_message_leaves_inbox_untouched(procs):
+    """SURVEY §5 fault injection "drop connection mid-stream": a sender that resets its
+    chat stream before EOF makes the receiver's read fail (the reference's io.ReadAll
+    error path, `go/cmd/node/main.go:160-164`): nothing is pushed.  A well-formed stream
+    from the same injector (FIN after the JSON) is delivered."""
+    d = start_directory(procs)
+    b = start_node(procs, "B", d)
+    addr = json.loads(http("GET", b + "/me")[1])["addrs"][0]
+    msg = {"id": "m-1", "from_user": "X", "to_user": "B", "content": "whole message",
+           "timestamp": "2025-09-02T21:11:32.154084+02:00"}
+    raw = json.dumps(msg).encode()
+    native().chat_inject(addr, raw[:len(raw) // 2], "reset")  # half a message, then RST
+    native().chat_inject(addr, raw, "reset")  # a whole JSON body but no EOF: still an error
+    time.sleep(0.5)
+    assert json.loads(http("GET", b + "/inbox")[1]) == []
+    native().chat_inject(addr, raw, "close")
+    inbox = _wait_inbox(b, 1)
+    assert [m["id"] for m in inbox] == ["m-1"] and inbox[0]["content"] == "whole message"
+
+
+def test_directory_killed_after_startup_send_is_404(procs):
+    """SURVEY §5 fault injection "kill directory": a node that registered and already
+    delivered messages answers /send with 404 user not found once the Directory is gone
+    (every send looks the recipient up again, `go/cmd/node/main.go:225-228`); its inbox
+    and /me keep working."""
+    d = start_directory(procs)
+    a = start_node(procs, "A", d)
+    b = start_node(procs, "B", d)
+    assert http("POST", a + "/send", {"to_username": "B", "content": "before"})[0] == 200
+    _wait_inbox(b, 1)
+    procs.procs[0].terminate()
+    procs.procs[0].wait()
+    assert http("POST", a + "/send", {"to_username": "B", "content": "after"})[:2] == \
+        (404, '{"error":"user not found"}')
+    assert len(json.loads(http("GET", b + "/inbox")[1])) == 1
+    assert http("GET", a + "/me")[0] == 200

@@ -199,3 +199,34 @@ def test_ep_a2a_cluster_dp_split_matches_single_engine():
         assert json.loads(cs.handle_json(REQS[2]))["response"] == ref[1]  # one sequence only
     finally:
         cs.close()
+
+
+def test_dp_split_homes_are_balanced():
+    """EP a2a (DP attention) homes are chosen at admission on the least-loaded
+    rank, not derived from the first page id (4-page requests at world 8 all landed on
+    ranks 1 and 5 before); a sequence keeps its home for its whole life."""
+    from p2p_llm_chat_go_amd.engine.cluster import LockstepEngine
+
+    le = LockstepEngine(None, [object()] * 7, dp_split=True)
+    bts = [[1 + 4 * i + j for j in range(4)] for i in range(8)]  # first pages 1, 5, 9, ...
+    parts = le._parts(bts, fresh=range(8))
+    assert sorted(len(p) for p in parts) == [1] * 8
+    home = {bt[0]: r for r, p in enumerate(parts) for bt in (bts[b] for b in p)}
+    # decode of the same sequences: same homes
+    again = le._parts(bts, decode=True)
+    assert {bts[b][0]: r for r, p in enumerate(again) for b in p} == home
+    # 16 more arrive while 8 run: every rank ends with 3
+    more = [[100 + 4 * i + j for j in range(4)] for i in range(16)]
+    parts = le._parts(more, fresh=range(16))
+    assert sorted(len(p) for p in parts) == [2] * 8
+    # half of the first batch retires; the next decode sees the live set, and 4 new
+    # sequences fill exactly the ranks that lost one
+    live = bts[:4] + more
+    le._parts(live, decode=True)
+    short = [r for r in range(8) if r not in [home[bt[0]] for bt in bts[:4]]]
+    new = [[300 + 4 * i + j for j in range(4)] for i in range(4)]
+    parts = le._parts(new, fresh=range(4))
+    assert sorted(r for r, p in enumerate(parts) if p) == sorted(short)
+    # a reused first page gets a fresh home (its old sequence is gone)
+    le._homes[new[0][0]] = 0
+    le._parts([new[0]], fresh=[0])

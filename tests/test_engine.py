@@ -206,3 +206,43 @@ def test_fp8_engine_cpu_matches_dequantized_weights():
     assert e8.weights.nbytes() < 0.75 * EngineWeights.random(TINY_LLAMA, "cpu", seed=5).nbytes()
     with pytest.raises(ValueError):
         Engine(TINY_LLAMA, device="cpu", kv_pages=8, weight_dtype="int3")
+
+
+@pytest.mark.parametrize("name", ["tiny-llama-gqa", "tiny-mixtral"])
+def test_lazy_safetensors_reads_shard_slices(tmp_path, name):
+    """A TP rank built from a LazySafetensors checkpoint reads only its slice of every
+    sharded tensor (get_slice) and gets the same weights as slicing the full tensors."""
+    from safetensors.torch import save_file
+
+    from p2p_llm_chat_go_amd.models.config import get_config
+    from p2p_llm_chat_go_amd.models.reference import random_state_dict
+    from p2p_llm_chat_go_amd.models.weights import EngineWeights, LazySafetensors
+
+    cfg = get_config(name)
+    sd = random_state_dict(cfg, seed=3)
+    half = sorted(sd)[:len(sd) // 2]
+    save_file({k: sd[k].contiguous() for k in half}, str(tmp_path / "a.safetensors"))
+    save_file({k: sd[k].contiguous() for k in sd if k not in half}, str(tmp_path / "b.safetensors"))
+    lazy = LazySafetensors(str(tmp_path))
+    reads = []
+    orig = lazy.get_rows_cols
+
+    def spy(n, rows=None, cols=None):
+        t = orig(n, rows, cols)
+        reads.append((n, tuple(t.shape), tuple(sd[n].shape)))
+        return t
+    lazy.get_rows_cols = spy
+    tp = 2 if cfg.n_kv_heads % 2 == 0 else 1
+    for r in range(tp):
+        a = EngineWeights.from_state_dict(sd, cfg, "cpu", tp_rank=r, tp_size=tp)
+        b = EngineWeights.from_state_dict(lazy, cfg, "cpu", tp_rank=r, tp_size=tp)
+        assert torch.equal(a.lm_head, b.lm_head) and torch.equal(a.embed, b.embed)
+        for la, lb in zip(a.layers, b.layers):
+            for f in ("qkv", "o", "gate_up", "down", "router", "w13", "w2"):
+                x, y = getattr(la, f), getattr(lb, f)
+                assert (x is None and y is None) or torch.equal(x, y), f
+    if tp > 1:  # projections came off the disk as shards, not whole tensors
+        q = [x for x in reads if x[0].endswith("q_proj.weight")]
+        assert q and all(got[0] * tp == full[0] for _n, got, full in q)
+        o = [x for x in reads if x[0].endswith("o_proj.weight")]
+        assert o and all(got[1] * tp == full[1] for _n, got, full in o)

@@ -326,3 +326,56 @@ def test_server_sampled_requests_reproducible_with_seed():
         assert len(outs) > 1  # different seeds draw different replies
     finally:
         srv.close()
+
+
+def test_stalled_engine_times_out_with_503(monkeypatch):
+    """SURVEY §5 fault injection "stall engine": with the engine loop stalled, the
+    co-pilot call fails within ENGINE_TIMEOUT (the reference UI's 60 s bound,
+    `web/streamlit_app.py:95`) -- /suggest answers 503 "LLM unavailable: ..." as the UI's
+    `(LLM unavailable: ...)` -- the request is cancelled, its KV pages come back, and the
+    engine serves again once the stall ends."""
+    from p2p_llm_chat_go_amd.engine.server import EngineTimeout
+
+    monkeypatch.setenv("ENGINE_TIMEOUT", "1.0")
+    srv, _, _ = make_server()
+    N = load()
+    N.set_log_quiet(True)
+    d = N.Directory()
+    durl = "http://127.0.0.1:%d" % d.start("127.0.0.1:0")
+    node = N.Node({"username": "B", "http_addr": "127.0.0.1:%d" % free_port(),
+                   "directory_url": durl, "key_type": "ed25519", "access_log": False,
+                   "listen": ["/ip4/127.0.0.1/tcp/0"]})
+    node.set_generate_hook(srv.handle_json)
+    node.set_generate_stream_hook(srv.handle_json_stream)
+    try:
+        node.start()
+        b = "http://127.0.0.1:%d" % node.http_port
+        wait_http(b + "/me")
+        free0 = srv.sched.free_pages
+        srv.stall(30.0)
+        t0 = time.perf_counter()
+        st, body, _ = http("POST", b + "/suggest", {"message": "Hey! How's it going?",
+                                                    "options": {"num_predict": 4}}, timeout=30)
+        dt = time.perf_counter() - t0
+        assert st == 503 and json.loads(body)["error"].startswith("LLM unavailable: ")
+        assert "within 1s" in json.loads(body)["error"]
+        assert 0.9 < dt < 5.0, dt
+        # the streaming path has the same deadline
+        t0 = time.perf_counter()
+        with pytest.raises(EngineTimeout):
+            srv.handle_json_stream(json.dumps({"prompt": "x", "options": {"num_predict": 4}}),
+                                   lambda c: True)
+        assert time.perf_counter() - t0 < 5.0
+        srv.stall(0.0)  # the GPU "recovers": cancelled requests drain, serving resumes
+        st, body, _ = http("POST", b + "/suggest", {"message": "again",
+                                                    "options": {"num_predict": 4}}, timeout=30)
+        assert st == 200 and "suggestion" in json.loads(body)
+        for _ in range(200):
+            if srv.sched.free_pages == free0 and srv.sched.n_running == 0:
+                break
+            time.sleep(0.02)
+        assert srv.sched.free_pages == free0 and srv.sched.n_running == 0
+    finally:
+        node.stop()
+        srv.close()
+        d.stop()

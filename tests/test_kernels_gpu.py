@@ -1,5 +1,6 @@
 """HIP kernel numerics vs plain PyTorch fp32 references (run on an MI355X)."""
 import math
+import os
 
 import pytest
 import torch
@@ -273,8 +274,18 @@ def test_paged_attention_spike_forces_rescale():
 
 
 # ------------------------------------------- fused decode attention + o_proj
+# measured-negative fusions kept for the record in the opt-in experimental library
+# (csrc/experimental, built with P2P_BUILD_EXPERIMENTAL=1 or `_build --only experimental`;
+# no engine default path uses them)
+needs_experimental = pytest.mark.skipif(
+    not os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "p2p_llm_chat_go_amd", "_lib", "libp2p_experimental.so")),
+    reason="experimental kernel library not built (P2P_BUILD_EXPERIMENTAL=1)")
+
+
 @pytest.mark.parametrize("R,Hkv,G,ctxs", [(1, 8, 4, [100]), (3, 2, 2, [1, 17, 256]),
                                           (16, 1, 4, list(range(5, 245, 15))), (2, 4, 1, [64, 65])])
+@needs_experimental
 def test_attn_oproj_fused(R, Hkv, G, ctxs):
     """One launch (attention blocks + o_proj blocks with a cross-workgroup hand-off)
     == paged_attention followed by the o_proj+residual GEMM; repeated launches and
@@ -331,6 +342,7 @@ def test_attn_oproj_fused(R, Hkv, G, ctxs):
 @pytest.mark.parametrize("R,Hkv,G,ctxs", [(1, 8, 4, [100]), (1, 8, 4, [1]), (1, 8, 4, [256]),
                                           (3, 2, 2, [1, 17, 256]), (2, 4, 1, [64, 65]),
                                           (16, 1, 4, list(range(5, 245, 15)))])
+@needs_experimental
 def test_attn_oproj_heads(R, Hkv, G, ctxs):
     """Head-split fused decode attention + o_proj (no hand-off; the last kv head of each
     column block sums the partials) == paged_attention followed by the o_proj+residual

@@ -224,3 +224,47 @@ def test_fault_bits_shared_across_group():
     for p in ps:
         p.join(30)
     assert res == [(0, 2), (1, 2)]
+
+
+def _local_timeout_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    import types
+
+    from p2p_llm_chat_go_amd.models.llama import LlamaModel
+    from p2p_llm_chat_go_amd.parallel.comm import TPComm
+    from p2p_llm_chat_go_amd.parallel.custom_ar import CollectiveTimeout
+
+    class Comm(TPComm):
+        def check(self):  # rank 1's one-shot spin timed out; rank 0's did not
+            if rank == 1:
+                raise CollectiveTimeout("local spin timeout")
+
+    fake = types.SimpleNamespace(device=torch.device("cpu"), comm=Comm())
+    try:
+        LlamaModel.check_faults(fake, None)
+        got = "no raise"
+    except CollectiveTimeout as e:
+        got = "raised: " + str(e)[:20]
+    dist.destroy_process_group()
+    _put_exit(q, (rank, got))
+
+
+def test_local_collective_timeout_raises_on_every_rank():
+    """a rank whose own one-shot wait timed out shares it (fault bit 4) through
+    the group MAX before raising, so its peers raise CollectiveTimeout at the same point
+    instead of blocking in the MAX collective until the process-group timeout."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_local_timeout_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(30)
+    assert res[0][1].startswith("raised: a one-shot") and res[1][1] == "raised: local spin timeout"
