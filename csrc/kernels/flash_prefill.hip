@@ -44,6 +44,7 @@ __global__ __launch_bounds__(64 * G) void flash_prefill_kernel(
   const int b = xcd_remap(blockIdx.x, nb);
   const int ti = b / Hkv, kvh = b % Hkv;  // consecutive ids: same tile, all heads
   const Tile T = tiles[ti];
+  if (T.n <= 0) return;  // padding tile of a graph-captured prefill (fixed grid)
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int g = lane >> 4, col = lane & 15;
   const int h = kvh * G + w;
@@ -236,6 +237,7 @@ __global__ __launch_bounds__(512) void flash_prefill2_kernel(
   const int b = xcd_remap(blockIdx.x, nb);
   const int kvh = b / n_tiles, ti = n_tiles - 1 - b % n_tiles;
   const Tile T = tiles[ti];
+  if (T.n <= 0) return;  // padding tile of a graph-captured prefill (fixed grid)
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int r32 = lane & 31, hh = lane >> 5;
   const int h = kvh * G + w / WPH;
@@ -444,6 +446,7 @@ P2P_API int p2p_flash_prefill2(const void* q, int ldq, const void* kc, const voi
 }
 
 // tiles: int32 [n_tiles, 4] = (first row, n tokens <= 16, sequence, first position);
+// n = 0 marks a padding tile (a captured prefill graph launches a fixed tile count);
 // a tile's rows are consecutive positions of one sequence whose K/V (positions
 // 0 .. pos0+n-1) are already in the paged cache.  head_dim must be 128.
 P2P_API int p2p_flash_prefill(const void* q, int ldq, const void* kc, const void* vc,

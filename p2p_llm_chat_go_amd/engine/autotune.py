@@ -7,8 +7,21 @@ layer once (cold weights, like the real decode step) and the fastest launch
 code is installed in ``ops.gemm._TUNE``.  Measured on MI355X the spread between
 configurations is up to ~2x at M=1 (e.g. down_proj 18.7 vs 42.9 us), and the
 best choice differs per shape, so a fixed heuristic leaves time on the table.
+
+Determinism.  Several candidates are often within run-to-run noise of each other, and a
+pick that flips between boxes moved the bench by a few percent.  So:
+  * near-ties are broken by a fixed rule: every candidate within ``TIE_FRAC`` of the
+    fastest counts as tied, and the tie goes to the first of them in the fixed candidate
+    order (``_configs``), not to whichever was faster on this box;
+  * a committed table (``tuned/<model>-<arch>.json``, written by
+    ``python -m p2p_llm_chat_go_amd.engine.autotune --model ... --save``) pins the picks:
+    with a table present (P2P_AUTOTUNE_TABLE, default on) the recorded code is installed
+    and only timed once for the report.  P2P_AUTOTUNE_TABLE=0 re-tunes from scratch.
 """
 from __future__ import annotations
+
+import json
+import os
 
 import torch
 
@@ -38,6 +51,44 @@ def _graph_time(fn, reps=3):
         best = min(best, e0.elapsed_time(e1))
     del g
     return best
+
+
+TIE_FRAC = float(os.environ.get("P2P_AUTOTUNE_TIE", "0.02"))
+TABLE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
+
+
+def _arch() -> str:
+    try:
+        return torch.cuda.get_device_properties(0).gcnArchName.split(":")[0]
+    except Exception:  # noqa: BLE001
+        return "gfx950"
+
+
+def table_path(model_name: str, arch: str | None = None) -> str:
+    return os.path.join(TABLE_DIR, "%s-%s.json" % (model_name, arch or _arch()))
+
+
+def load_table(model_name: str) -> dict:
+    if os.environ.get("P2P_AUTOTUNE_TABLE", "1") == "0":
+        return {}
+    p = table_path(model_name)
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        return json.load(f).get("codes", {})
+
+
+def pick(times: dict, order: list) -> int:
+    """Fastest candidate, near-ties (within TIE_FRAC) resolved by candidate order."""
+    t_min = min(times.values())
+    for code in order:
+        if code in times and times[code] <= t_min * (1.0 + TIE_FRAC):
+            return code
+    return min(times, key=times.get)
+
+
+def _job_key(name, N, K, M, fp8) -> str:
+    return "%s:N%d:K%d:M%d%s" % (name, N, K, M, ":fp8" if fp8 else "")
 
 
 def _configs(K, M=1, tiled=False, midm=False, wide=False):
@@ -75,9 +126,16 @@ def describe(code: int) -> str:
     return "w%d/U%d%s" % (code & 0xff, (code >> 8) & 0xff, "/NG%d" % ng if ng > 1 else "")
 
 
-def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
+def autotune_model(model, batch_sizes=(1,), verbose=False, table: dict | None = None,
+                   record: dict | None = None) -> dict:
+    """Tune (or, for keys in ``table``, install the recorded pick of) every projection at
+    every M of ``batch_sizes``.  ``record`` (if given) receives {job key: code} of every
+    pick, for ``--save``."""
     if model.device.type != "cuda":
         return {}
+    if table is None:
+        tp = getattr(model, "tp", 1)
+        table = load_table(model.cfg.name if tp == 1 else "%s-tp%d" % (model.cfg.name, tp))
     cfg, w = model.cfg, model.w
     dev = model.device
     H = cfg.hidden
@@ -122,9 +180,17 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
                 # pack the activations fragment-major first (one extra launch, timed with the
                 # GEMM): measured to pay on the qkv shape only (profiles/r3_afrag_probe.jsonl)
                 codes += [c | G.AFRAG_FLAG for c in _configs(K, M) if (c >> 16) & 0xff]
-            for code in codes:
-                times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
-            best = min(times, key=times.get)
+            jk = _job_key(name, N, K, M, not bf)
+            fixed = table.get(jk)
+            if fixed is not None and int(fixed) in codes:
+                times[int(fixed)] = _graph_time(lambda: [fn(wt, int(fixed)) for wt in wts])
+                best = int(fixed)
+            else:
+                for code in codes:
+                    times[code] = _graph_time(lambda: [fn(wt, code) for wt in wts])
+                best = pick(times, codes)
+            if record is not None:
+                record[jk] = best
             norm = epi in (G.EPI_QKV_ROPE, G.EPI_SILU, G.EPI_ARGMAX)
             G.set_tune(G.tune_key(wts[0], M, epi, norm), best)
             if epi == G.EPI_RESID:
@@ -139,3 +205,37 @@ def autotune_model(model, batch_sizes=(1,), verbose=False) -> dict:
         keys.zero_()
     torch.cuda.synchronize()
     return result
+
+
+def main(argv=None):
+    """Tune a model on this GPU and (``--save``) write the pinned table."""
+    import argparse
+
+    from ..models.config import get_config
+    from .engine import Engine
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3.1-8b")
+    ap.add_argument("--tp", type=int, default=1, help="tune one rank's shard of a TP group")
+    ap.add_argument("--batch", default="1,2,4,8,16,48,64")
+    ap.add_argument("--save", action="store_true")
+    a = ap.parse_args(argv)
+    os.environ["P2P_AUTOTUNE_TABLE"] = "0"
+    cfg = get_config(a.model)
+    kw = dict(tp_rank=0, tp_size=a.tp) if a.tp > 1 else {}
+    eng = Engine(cfg, device="cuda", kv_pages=64, max_batch=16, use_graph=False, **kw)
+    rec = {}
+    res = autotune_model(eng.model, tuple(int(b) for b in a.batch.split(",")), verbose=True,
+                         table={}, record=rec)
+    out = {"model": cfg.name, "arch": _arch(), "tp": a.tp, "tie_frac": TIE_FRAC, "codes": rec,
+           "us": {"%s@M%d" % k: round(v[1], 2) for k, v in res.items()}}
+    print(json.dumps(out), flush=True)
+    if a.save:
+        name = cfg.name if a.tp == 1 else "%s-tp%d" % (cfg.name, a.tp)
+        os.makedirs(TABLE_DIR, exist_ok=True)
+        with open(table_path(name), "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

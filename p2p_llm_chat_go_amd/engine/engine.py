@@ -28,7 +28,7 @@ from ..models.weights import EngineWeights
 from .. import ops
 from ..utils.trace import span
 from ..ops import PAGE
-from .graph import DecodeGraph, DecodeState
+from .graph import PREFILL_ROW_BUCKETS, DecodeGraph, DecodeState, PrefillGraph
 from .kv_cache import KVCache, pages_for
 
 BATCH_BUCKETS = (1, 2, 4, 8, 16, 32, 64)
@@ -97,6 +97,12 @@ class Engine:
         self.use_graph = use_graph
         self._prefill_ws = {}
         self._graphs = {}
+        # graph-captured prefill chunks (engine.graph.PrefillGraph): dense TP=1 engines on
+        # the GPU; P2P_PREFILL_GRAPH=0 keeps every prefill eager
+        self.prefill_graphs_enabled = (
+            use_graph and self.device.type == "cuda" and tp_size == 1 and not cfg.is_moe
+            and os.environ.get("P2P_PREFILL_GRAPH", "1") != "0")
+        self._pgraphs = {}
 
     # -------------------------------------------------------------- helpers
     def _sync(self):
@@ -119,6 +125,26 @@ class Engine:
             g = DecodeGraph(st, self.use_graph, greedy=greedy).capture()
             self._graphs[key] = g
         return g
+
+    def prefill_graph(self, rows: int, n_seq: int, max_ctx: int, greedy: bool = True) -> PrefillGraph:
+        """The captured prefill of a chunk of <= ``rows`` rows from <= ``n_seq`` sequences
+        (bucketed), contexts <= ``max_ctx``; captured on first use."""
+        rb = bucket(rows, PREFILL_ROW_BUCKETS)
+        sb = min(bucket(n_seq, BATCH_BUCKETS), self.max_batch)
+        cb = bucket(max_ctx, CTX_BUCKETS)
+        key = (rb, sb, cb, greedy)
+        g = self._pgraphs.get(key)
+        if g is None:
+            g = PrefillGraph(self.model, self.prefill_workspace(cb), rb, sb, cb // PAGE, cb,
+                             greedy=greedy).capture()
+            self._pgraphs[key] = g
+        return g
+
+    def _graph_prefill_ok(self, n_rows: int, B: int, max_ctx: int, n_dummy: int,
+                          return_logits: bool) -> bool:
+        return (self.prefill_graphs_enabled and not return_logits and not n_dummy
+                and n_rows <= min(self.max_prefill_tokens, PREFILL_ROW_BUCKETS[-1])
+                and B <= self.max_batch and max_ctx <= CTX_BUCKETS[-1])
 
     def autotune(self, batch_sizes=(1,), verbose=False):
         """Pick the fastest GEMM launch configs for this model (before graph capture)."""
@@ -191,6 +217,8 @@ class Engine:
             assert n_dummy >= 0, (pad_rows, len(rows))
             rows += [(B, i, 0) for i in range(n_dummy)]  # sequence B: the null page
         max_ctx = max([len(p) for p in prompts] + [n_dummy, 1])
+        if self._graph_prefill_ok(len(rows), B, max_ctx, n_dummy, return_logits):
+            return self._prefill_graphed(prompts, block_tables, rows, max_ctx, sampling, sampled)
         ws = self.prefill_workspace(max_ctx)
         max_pages = bucket(max_ctx, CTX_BUCKETS) // PAGE
         bt = torch.zeros(B + (1 if n_dummy else 0),
@@ -264,6 +292,22 @@ class Engine:
             if all_logits is not None:
                 all_logits.index_copy_(0, sel, res)
         return (first, all_logits) if return_logits else first
+
+    def _prefill_graphed(self, prompts, block_tables, rows, max_ctx, sampling, sampled):
+        """One chunk through its captured graph: one metadata copy + one graph launch."""
+        B = len(prompts)
+        g = self.prefill_graph(len(rows), B, max_ctx, greedy=not sampled)
+        last = [0] * B
+        for j, r in enumerate(rows):  # rows are grouped by sequence, in order
+            last[r[0]] = j
+        g.load(g.host_meta(rows, block_tables, last))
+        g.replay()
+        if not sampled:
+            return g.first[:B]
+        from .sampling import sample
+
+        res = g.ws.logits[:B]
+        return sample(res, list(sampling), [len(p) - 1 for p in prompts])
 
     # --------------------------------------------------------------- decode
     def decode_steps(self, last_ids: list, pos: list, block_tables: list, ctx: int, k: int,

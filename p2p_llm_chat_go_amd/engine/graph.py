@@ -14,6 +14,7 @@ replay.  Padding rows of a bucket stay on the null page.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -190,3 +191,130 @@ class DecodeGraph:
                 self.graph.replay()
             else:
                 self.state.body_sampled()
+
+
+# rows of a captured prefill (a chunk of <= max_prefill_tokens rows is padded up to the
+# next bucket with dummy rows on the KV null page)
+PREFILL_ROW_BUCKETS = (16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024)
+
+
+class PrefillGraph:
+    """A whole prefill chunk -- embedding gather, every layer (fused-epilogue GEMMs, flash
+    prefill attention on paged KV), last-row gather, LM head and the greedy argmax (or the
+    fp32 logits for sampled requests) -- captured as ONE hipGraph per (row bucket, sequence
+    bucket, context bucket).
+
+    Eager prefill issues ~170 launches from Python per chunk; on a slow host that, not the
+    GPU, sets the time to first token.  Replaying a graph costs one host->device copy of the
+    chunk's metadata (``load``) plus one ``hipGraphLaunch``.
+
+    Every launch parameter is static per bucket; what varies per chunk lives in one device
+    int32 buffer (``meta``): block tables (``n_seq`` + 1 rows; the last one is the dummy
+    sequence on the null page), per-row sequence / position / token / KV slot / context,
+    the output rows, and the flash-attention query tiles (padded to ``max_tiles`` with
+    zero-length tiles, which the kernel skips).  Dummy rows carry slot -1 (no KV write)."""
+
+    def __init__(self, model, ws, rows: int, n_seq: int, max_pages: int, max_ctx: int,
+                 greedy: bool = True):
+        dev = model.device
+        self.model, self.ws = model, ws
+        self.rows, self.n_seq, self.max_pages, self.max_ctx = rows, n_seq, max_pages, max_ctx
+        self.n_out = n_seq
+        self.greedy = greedy
+        self.qtile = ops.flash_tile(model.nq, model.nkv, rows)
+        # tiles never straddle sequences: <= rows / qtile + one partial tile per sequence
+        # (the dummy sequence included)
+        self.max_tiles = -(-rows // self.qtile) + n_seq + 1
+        R, S = rows, n_seq
+        sizes = [("bt", (S + 1) * max_pages), ("seq", R), ("pos", R), ("ids", R), ("slots", R),
+                 ("ctx", R), ("out", S), ("tiles", 4 * self.max_tiles)]
+        self.offsets = {}
+        o = 0
+        for name, n in sizes:
+            self.offsets[name] = (o, n)
+            o += n
+        self.meta = torch.zeros(o, device=dev, dtype=torch.int32)
+        v = {name: self.meta[a:a + n] for name, (a, n) in self.offsets.items()}
+        self.bt = v["bt"].view(S + 1, max_pages)
+        self.seq, self.pos, self.ids, self.slots, self.ctx = (v[k] for k in ("seq", "pos", "ids",
+                                                                               "slots", "ctx"))
+        self.out_rows = v["out"]
+        self.tiles = v["tiles"].view(self.max_tiles, 4)
+        self.first = torch.zeros(S, device=dev, dtype=torch.int32)
+        self.graph = None
+
+    # ------------------------------------------------------------------ host side
+    def host_meta(self, rows: list, block_tables: list, out_rows: list) -> torch.Tensor:
+        """The ``meta`` image of one chunk: rows = [(seq, pos, token)] (sequences
+        consecutive, in order), block_tables[s] = page list of sequence s, out_rows = the
+        row of each sequence whose logits are needed (its last).  numpy throughout: this
+        runs on the TTFT path, once per prefill."""
+        R, S, P = self.rows, self.n_seq, self.max_pages
+        n = len(rows)
+        assert n <= R and len(block_tables) <= S and len(out_rows) <= S, (n, len(block_tables))
+        host = np.zeros(self.meta.numel(), dtype=np.int32)
+        v = {name: host[a:a + k] for name, (a, k) in self.offsets.items()}
+        bt = v["bt"].reshape(S + 1, P)
+        for s, pages in enumerate(block_tables):
+            assert len(pages) <= P, (len(pages), P)
+            bt[s, :len(pages)] = pages
+        seq, pos = v["seq"], v["pos"]
+        if n:
+            a = np.asarray(rows, dtype=np.int32).reshape(n, 3)
+            seq[:n], pos[:n], v["ids"][:n] = a[:, 0], a[:, 1], a[:, 2]
+        seq[n:] = S  # dummy rows: sequence S (the null page), positions 0..
+        pos[n:] = np.arange(R - n, dtype=np.int32)
+        slots = bt[seq, pos // PAGE] * PAGE + pos % PAGE
+        slots[n:] = -1  # dummy rows write no KV
+        v["slots"][:] = slots
+        v["ctx"][:] = pos + 1
+        v["out"][:len(out_rows)] = out_rows
+        # query tiles: runs of consecutive positions of one sequence, cut at qtile rows
+        # (ops.prefill_tiles); the rest stay n = 0 padding tiles
+        brk = np.flatnonzero((seq[1:] != seq[:-1]) | (pos[1:] != pos[:-1] + 1)) + 1
+        bounds = np.concatenate(([0], brk, [R]))
+        tl = []
+        q = self.qtile
+        for r0, r1 in zip(bounds[:-1].tolist(), bounds[1:].tolist()):
+            for t0 in range(r0, r1, q):
+                tl.append((t0, min(q, r1 - t0), int(seq[t0]), int(pos[t0])))
+        assert len(tl) <= self.max_tiles, (len(tl), self.max_tiles)
+        v["tiles"][:4 * len(tl)] = np.asarray(tl, dtype=np.int32).reshape(-1)
+        return torch.from_numpy(host)
+
+    def load(self, host: torch.Tensor):
+        self.meta.copy_(host, non_blocking=True)
+
+    # ------------------------------------------------------------------ device side
+    def body(self):
+        m, ws = self.model, self.ws
+        res = m.forward(ws, self.ids, self.pos, self.slots, self.bt, self.seq, self.ctx,
+                        self.rows, self.max_ctx, out_rows=self.out_rows, n_out=self.n_out,
+                        greedy=self.greedy, tiles=self.tiles, qtile=self.qtile)
+        if self.greedy:
+            m.finalize_greedy(ws, self.n_out, out=self.first)
+        return res
+
+    def capture(self, warmup: int = 2):
+        dev = self.model.device
+        # a valid dummy chunk (every row on the null page) for the warmup runs and capture
+        self.load(self.host_meta([], [], []))
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):  # sizes lazily-grown workspaces before capture
+                self.body()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.body()
+        torch.cuda.synchronize(dev)
+        self.graph = g
+        return self
+
+    def replay(self):
+        """Runs the loaded chunk.  Greedy: the first tokens are in ``self.first[:n]``;
+        else the fp32 logits of the output rows in ``self.ws.logits[:n]`` (both are
+        overwritten by the next replay)."""
+        self.graph.replay()

@@ -20,7 +20,7 @@ step() {  # step <name> <timeout> <log> cmd...
 IFS=',' read -ra S <<< "$STEPS"
 for s in "${S[@]}"; do
   case "$s" in
-    tests) step tests ${TEST_TIMEOUT:-900} "${TAG}_pytest_gpu.log" python -u -m pytest tests -m gpu -x -q \
+    tests) step tests ${TEST_TIMEOUT:-900} "${TAG}_pytest_gpu.log" python -u -m pytest ${TEST_PATHS:-tests} -m gpu -x -q \
              --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke) step smoke 300 "${TAG}_smoke.log" python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 "${TAG}_bench.log" python bench.py ${BENCH_ARGS:---steps 20 --warmup 5} ;;

@@ -246,3 +246,52 @@ def test_lazy_safetensors_reads_shard_slices(tmp_path, name):
         assert q and all(got[0] * tp == full[0] for _n, got, full in q)
         o = [x for x in reads if x[0].endswith("o_proj.weight")]
         assert o and all(got[1] * tp == full[1] for _n, got, full in o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lens", [[44], [5, 37, 12], [60, 3], [130]])
+def test_prefill_graph_equals_eager_gpu(lens):
+    """A graph-captured prefill chunk (engine.graph.PrefillGraph: padded row bucket,
+    padding tiles, dummy rows on the null page) gives the eager prefill's first tokens,
+    logits and KV cache contents, and decoding continues identically."""
+    from p2p_llm_chat_go_amd.models import LLAMA31_8B
+
+    cfg = LLAMA31_8B.replace(n_layers=2)
+    w = EngineWeights.random(cfg, "cuda", seed=11)
+    prompts = [[(37 * b + 11 * i) % 5000 + 100 for i in range(L)] for b, L in enumerate(lens)]
+    out = {}
+    for graph in (False, True):
+        eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_batch=4)
+        assert eng.prefill_graphs_enabled
+        eng.prefill_graphs_enabled = graph
+        pages = [eng.kv.allocator.alloc(3) for _ in prompts]
+        first = eng.prefill(prompts, pages).cpu()
+        assert bool(eng._pgraphs) == graph
+        kv = []
+        for i in range(cfg.n_layers):
+            kc, vc = eng.kv.layer(i)
+            for b, p in enumerate(prompts):
+                pos = torch.arange(len(p))
+                pg = torch.tensor(pages[b])[pos // 64].cuda()
+                kv.append(kc[pg, :, (pos % 64).cuda()].float().cpu())
+                kv.append(vc[pg, :, (pos % 64).cuda()].float().cpu())
+        if graph:  # the sampled-request graph's logits vs the eager return_logits path
+            rows = [(b, i, t) for b, p in enumerate(prompts) for i, t in enumerate(p)]
+            last = [sum(lens[:b + 1]) - 1 for b in range(len(lens))]
+            g = eng.prefill_graph(len(rows), len(prompts), max(lens), greedy=False)
+            g.load(g.host_meta(rows, pages, last))
+            g.replay()
+            logits = g.ws.logits[:len(prompts)].float().cpu()
+        else:
+            _f, logits = eng.prefill(prompts, pages, return_logits=True)
+            logits = logits.float().cpu()
+        for p in pages:
+            eng.kv.allocator.free(p)
+        gen = [r.tokens for r in eng.generate(prompts, 12, stop_on_eos=False)]
+        out[graph] = (first, kv, logits, gen)
+    (f0, kv0, l0, g0), (f1, kv1, l1, g1) = out[False], out[True]
+    assert torch.equal(f0, f1)
+    for a, b in zip(kv0, kv1):
+        assert (a - b).abs().max() <= 1e-2 * max(1.0, float(a.abs().max()))
+    assert ((l0 - l1).norm() / l0.norm()) < 1e-2
+    assert g0 == g1
