@@ -191,6 +191,9 @@ def moe_forward_a2a(model, lw, ws, R):
     dummy_rows = buf.get("route_rows", 1, R, torch.int32)
     dummy_cnt = buf.get("route_cnt", 1, None, torch.int32)
     moe_ops.moe_route(logits, E, K, 0, 0, topk_ids, topk_w, dummy_cnt, dummy_rows)
+    ipc = getattr(comm, "ep_ipc", None)
+    if ipc is not None and dev.type == "cuda" and ipc.fits(n_slots):
+        return _a2a_ipc(model, lw, buf, ipc, h, topk_ids, topk_w, R)
     capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
     exact = (not capturing) and W * n_slots * H * 2 > A2A_STATIC_MAX_BYTES
     C = 0 if exact else n_slots
@@ -236,3 +239,36 @@ def moe_forward_a2a(model, lw, ws, R):
     else:
         comm.all_to_all_(back, o[:n])
     moe_ops.a2a_combine(back, send_map, R, K, h)
+
+
+def _a2a_ipc(model, lw, buf, ipc, h, topk_ids, topk_w, R):
+    """Decode-size exchanges of ``moe_forward_a2a`` on the IPC kernels
+    (``parallel.ep_a2a``): no host sync, no RCCL call, only routed rows on the wire --
+    the whole layer is captured in the decode hipGraph.  Same numbers as the RCCL path
+    (rows land in another order inside a destination; every row is computed on its own
+    and the combine sums a token's K returns in k order)."""
+    cfg = model.cfg
+    K, H = cfg.top_k, cfg.hidden
+    W = model.w.ep_size
+    El = cfg.n_experts // W
+    C = R * K
+    nb = ipc.blocks_per_pair(C, W)
+    send_map = buf.get("ipc_send_map", C, None, torch.int32)
+    ipc.dispatch(h, topk_ids, topk_w, K, El, send_map, R, nb)
+    n = W * C
+    recv_x = buf.get("recv_x", n, H)
+    recv_meta = buf.get("recv_meta", n, 2, torch.int32)
+    recv_w = buf.get("ipc_recv_w", n, None, torch.float32)
+    recv_cnt = buf.get("ipc_recv_cnt", W, None, torch.int32)
+    ipc.recv(C, recv_x, recv_meta, recv_w, recv_cnt, nb)
+    cnt = buf.get("cnt", El, None, torch.int32)
+    rows = buf.get("rows", El, n, torch.int32)
+    moe_ops.a2a_group(recv_meta, n, El, cnt, rows)
+    Fs = lw.w13.shape[1] * 16 // 2
+    act = buf.get("act", n, Fs)
+    o = buf.get("o", n, H)
+    moe_ops.grouped_gemm(lw.w13, cnt, rows, recv_x, 1, n, ops.EPI_SILU, act, norm=True,
+                         eps=cfg.eps)
+    moe_ops.grouped_gemm(lw.w2, cnt, rows, act, 1, n, ops.EPI_STORE, o, row_w=recv_w)
+    ipc.give_back(C, o, recv_cnt, nb)
+    ipc.combine(send_map, R, K, h, nb)

@@ -112,6 +112,16 @@ _SIGS = {
                               c_int, c_void_p],
     "p2p_moe_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p],
+    # expert-parallel all-to-all over IPC peer buffers (ep_a2a.hip)
+    "p2p_ep_set_timeout_ms": [c_int],
+    "p2p_ep_dispatch": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_ep_recv": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                    c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_ep_return": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                      c_int, c_void_p],
+    "p2p_ep_combine": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                       c_int, c_void_p, c_void_p, c_int, c_void_p],
 }
 
 
@@ -141,6 +151,10 @@ def lib():
             if fn is not None:
                 fn.argtypes = [ctypes.c_size_t]
                 fn.restype = ctypes.c_size_t
+        fn = getattr(L, "p2p_ep_buffer_bytes", None)
+        if fn is not None:
+            fn.argtypes = [c_int, c_int]
+            fn.restype = ctypes.c_size_t
         fn = getattr(L, "p2p_tiled_gemm_config", None)
         if fn is not None:
             fn.argtypes = [c_int, c_int, c_int]

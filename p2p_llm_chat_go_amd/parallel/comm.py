@@ -39,6 +39,7 @@ class TPComm:
             car_max_bytes = int(os.environ.get("P2P_CAR_MAX_BYTES", str(4 << 20)))
         self.car_max_bytes = car_max_bytes
         self.car = None
+        self.ep_ipc = None  # parallel.ep_a2a.IpcAllToAll (EP a2a decode exchanges)
         # world-1 groups normally skip the IPC kernels; the TP rank proxy
         # (bench/tp_rank_proxy.py) keeps them so one rank's launch structure is the real one
         self.car_at_world1 = False
@@ -53,7 +54,18 @@ class TPComm:
             self.car = CustomAllReduce(self.group, device, self.car_max_bytes)
         return self
 
+    def setup_ep_ipc(self, cmax: int, hidden: int):
+        """IPC all-to-all buffers of the DP-attention + EP MoE layer (call on every rank of
+        the group, before graph capture).  P2P_EP_IPC=0 keeps RCCL for every exchange."""
+        if (self.car is not None and self.ep_ipc is None
+                and os.environ.get("P2P_EP_IPC", "1") != "0"):
+            from .ep_a2a import IpcAllToAll
+
+            self.ep_ipc = IpcAllToAll(self.car, cmax, hidden)
+        return self.ep_ipc
+
     def close(self):
+        self.ep_ipc = None  # its buffers are the car's (freed below)
         if self.car is not None:
             self.car.close()
             self.car = None

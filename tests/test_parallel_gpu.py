@@ -24,8 +24,9 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q, moe, a2a=False, overlap=False, graphs=False):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, world, port, q, moe, a2a=False, overlap=False, graphs=False, ipc=True):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      P2P_EP_IPC="1" if ipc else "0")
     if overlap:  # prefill row-parallel sums chunked onto a communication stream
         os.environ["P2P_TP_OVERLAP_MIN_ROWS"] = "16"
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -91,15 +92,19 @@ def _sampled(eng, prompts, n=5):
     return out
 
 
-@pytest.mark.parametrize("moe,a2a,overlap,graphs", [
-    (False, False, False, False), (False, False, False, True), (False, False, True, False),
-    (True, False, False, False), (True, True, False, False)])
-def test_virtual_rank_parallel_gpu(moe, a2a, overlap, graphs):
+# a2a: EP decode exchanges on the IPC kernels (parallel.ep_a2a), eager and graph-captured,
+# and on the RCCL/gloo static-capacity path (ipc=False)
+@pytest.mark.parametrize("moe,a2a,overlap,graphs,ipc", [
+    (False, False, False, False, True), (False, False, False, True, True),
+    (False, False, True, False, True), (True, False, False, False, True),
+    (True, True, False, False, False), (True, True, False, False, True),
+    (True, True, False, True, True)])
+def test_virtual_rank_parallel_gpu(moe, a2a, overlap, graphs, ipc):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     world = 2
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a, overlap, graphs))
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, moe, a2a, overlap, graphs, ipc))
           for r in range(world)]
     [p.start() for p in ps]
     res = [q.get(timeout=600) for _ in range(world)]

@@ -15,7 +15,8 @@ is that the protocol, the sharding and the graphs are right at world 8.
   model's logits at that position.
 * MoE: Mixtral-8x7B full width (2 layers), EP=8 (one expert per rank), in the
   ``allreduce`` mode (replicated attention, partial expert sums all-reduced) and the
-  ``a2a`` mode (DP attention, token dispatch/combine all-to-all).
+  ``a2a`` mode (DP attention, token dispatch/combine all-to-all on the IPC kernels,
+  decode graph-captured).
 
 The reference has no parallelism; the call these engines serve is
 `web/streamlit_app.py:91-95` (BASELINE configs 3 and 5).
@@ -79,8 +80,9 @@ def _worker(rank, world, port, q, kind, mode, env):
         full_w = EngineWeights.from_state_dict(sd, cfg, "cuda") if rank == 0 else None
         del sd
         torch.cuda.empty_cache()
-        # a2a over gloo moves host memory (RCCL refuses 2+ ranks on one device): eager decode
-        graphs = mode != "a2a"
+        # every mode decodes through captured graphs; a2a's decode exchanges run on the IPC
+        # kernels (parallel.ep_a2a), its prefill (exact counts) over gloo
+        graphs = True
         eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_batch=2, comm=TPComm(),
                      tp_rank=w.tp_rank, tp_size=w.tp_size, use_graph=graphs,
                      ep_mode=mode if moe else "allreduce")
