@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1, help="serve through engine.cluster on N GPUs")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--ep", type=int, default=1)
+    ap.add_argument("--loop", choices=("native", "python"), default="native",
+                    help="native: the C++ step loop replaying captured graphs "
+                         "(engine.native_loop); python: engine.server's loop")
     a = ap.parse_args()
     if a.gpus > 1 or a.tp > 1 or a.ep > 1:
         return cluster_main(a)
@@ -55,9 +58,19 @@ def main():
     eng = Engine(cfg, device=dev, seed=7, max_batch=max(a.peers, 1),
                  max_prefill_tokens=a.max_prefill)
     eng.warmup(tuple(sorted({1, 2, 4, 8, a.peers} - {0})), ctx=256)
-    srv = EngineServer(eng, tok, max_batch=a.peers,
-                       decode_chunk=int(os.environ.get("ENGINE_DECODE_CHUNK", "8")),
-                       mixed=bool(a.mixed))
+    chunk = int(os.environ.get("ENGINE_DECODE_CHUNK", "8"))
+    if a.loop == "native":
+        from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
+
+        srv = NativeEngineServer(eng, tok, max_batch=a.peers, decode_chunk=chunk)
+
+        def stats():
+            return srv.metrics()
+    else:
+        srv = EngineServer(eng, tok, max_batch=a.peers, decode_chunk=chunk, mixed=bool(a.mixed))
+
+        def stats():
+            return dict(srv.stats)
     prompts = [tok.chat_ids(suggest_prompt(SAMPLE_MESSAGES[i % len(SAMPLE_MESSAGES)]))
                for i in range(a.peers)]
 
@@ -66,8 +79,10 @@ def main():
         return SamplingParams(max_tokens=max(1, n), stop_on_eos=False)
 
     # warm pass (graphs for every batch bucket the mix will hit)
-    futs = [srv.submit(prompts[p], params(p)) for p in range(a.peers)]
-    [f.result(600) for f in futs]
+    ths = [threading.Thread(target=srv.generate, args=(prompts[p], params(p), 600))
+           for p in range(a.peers)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
     results, lock = [], threading.Lock()
 
     def peer(p):
@@ -76,17 +91,18 @@ def main():
             with lock:
                 results.append(out)
 
-    occ0 = dict(srv.stats)
+    occ0 = stats()
     t0 = time.perf_counter()
     ths = [threading.Thread(target=peer, args=(p,)) for p in range(a.peers)]
     [t.start() for t in ths]
     [t.join() for t in ths]
     el = time.perf_counter() - t0
+    occ1 = stats()
     srv.close()
     toks = sum(r["eval_count"] for r in results)
     ttft = sorted(r["ttft_ns"] / 1e6 for r in results)
     queue = sorted((r["ttft_ns"] - r["prompt_eval_duration"]) / 1e6 for r in results)
-    steps = srv.stats["decode_steps"] - occ0["decode_steps"]
+    steps = occ1["decode_steps"] - occ0["decode_steps"]
     print(json.dumps({
         "metric": "suggest-reply tokens/sec (continuous batching)", "value": round(toks / el, 2),
         "unit": "tokens/s", "model": cfg.name, "peers": a.peers, "requests": len(results),
@@ -95,9 +111,9 @@ def main():
         "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
         "queue_p50_ms": round(statistics.median(queue), 3),
         "queue_p99_ms": round(queue[min(len(queue) - 1, int(0.99 * len(queue)))], 3),
-        "decode_chunk": srv.decode_chunk, "admit_wait_us": round(srv.admit_wait_s * 1e6),
+        "decode_chunk": srv.decode_chunk, "loop": a.loop,
         "mean_batch": round(toks / max(steps, 1), 2), "mixed": bool(a.mixed), "dtype": "bf16",
-        "engine_time_s": {k: round(srv.stats[k] - occ0[k], 4) for k in
+        "engine_time_s": {k: round(occ1[k] - occ0[k], 4) for k in
                           ("busy_s", "prefill_s", "decode_s", "prefill_calls", "decode_calls")},
         "data": "synthetic chat prompts, random-init weights"}), flush=True)
 

@@ -21,7 +21,8 @@
 namespace py = pybind11;
 using namespace p2p;
 
-void bind_runtime(py::module_& m);  // runtime_bind.cc
+void bind_runtime(py::module_& m);      // runtime_bind.cc
+void bind_engine_loop(py::module_& m);  // runtime_bind.cc
 
 namespace {
 
@@ -859,4 +860,5 @@ PYBIND11_MODULE(_native, m) {
       .def("stop", [](Relay& r) { r.h->close(); }, py::call_guard<py::gil_scoped_release>());
 
   bind_runtime(m);
+  bind_engine_loop(m);
 }

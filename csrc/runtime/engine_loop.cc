@@ -1,0 +1,720 @@
+#include "runtime/engine_loop.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+#include "runtime/hip_dyn.h"
+
+namespace p2p {
+
+namespace {
+
+// pinned staging slots
+enum Slot : int {
+  kDecodeMeta = 0,
+  kPrefillMeta = 1,
+  kHist0 = 2,  // kHist0, kHist0 + 1: double-buffered decode history
+  kFirst = 4,
+  kErr0 = 5,  // kErr0, kErr0 + 1: fault word per decode buffer; kErr0 + 2 prefill
+  kSampF = 8,
+  kSampI = 9,
+  kSampP = 10,
+  kSampS = 11,
+  kSlots = 12,
+};
+
+}  // namespace
+
+EngineLoop::EngineLoop(const LoopConfig& cfg)
+    : cfg_(cfg),
+      sched_(cfg.num_pages, cfg.page_size, cfg.max_batch, cfg.max_prefill_tokens, cfg.max_ctx) {
+  sched_.set_defer_free(true);
+  pinned_.assign(kSlots, {nullptr, 0});
+}
+
+// The thread only: HIP resources are released by shutdown() (a destructor running at
+// interpreter exit may find the HIP runtime already torn down).
+EngineLoop::~EngineLoop() { stop(); }
+
+void EngineLoop::shutdown() {
+  stop();
+  const HipApi& h = hip_api();
+  if (!h.ok) return;
+  for (auto& p : pinned_)
+    if (p.first) h.hostFree(p.first);
+  pinned_.assign(kSlots, {nullptr, 0});
+  for (void* e : events_)
+    if (e) h.eventDestroy(e);
+  events_.clear();
+  if (stream_) h.streamDestroy(stream_);
+  stream_ = nullptr;
+}
+
+int64_t EngineLoop::now_ns() const {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+int EngineLoop::bucket(int x, const std::vector<int>& b) {
+  for (int v : b)
+    if (x <= v) return v;
+  return -1;
+}
+
+void* EngineLoop::pinned(int slot, size_t bytes) {
+  auto& p = pinned_[slot];
+  if (p.second < bytes) {
+    const HipApi& h = hip_api();
+    if (p.first) h.hostFree(p.first);
+    size_t n = std::max(bytes, (size_t)4096);
+    hip_check(h.hostMalloc(&p.first, n, 0), "hipHostMalloc");
+    p.second = n;
+  }
+  return p.first;
+}
+
+// ------------------------------------------------------------------ registration
+void EngineLoop::add_decode_graph(const DecodeGraphDesc& d) {
+  std::lock_guard<std::mutex> lk(gmu_);
+  dgraphs_[std::make_tuple(d.B, d.ctx, d.greedy)] = std::make_unique<DecodeGraphDesc>(d);
+}
+
+void EngineLoop::add_prefill_graph(const PrefillGraphDesc& d) {
+  std::lock_guard<std::mutex> lk(gmu_);
+  pgraphs_[std::make_tuple(d.rows, d.n_seq, d.greedy)] = std::make_unique<PrefillGraphDesc>(d);
+}
+
+void EngineLoop::set_provider(GraphProvider p) { provider_ = std::move(p); }
+void EngineLoop::set_eager_prefill(EagerPrefill f) { eager_ = std::move(f); }
+
+const DecodeGraphDesc* EngineLoop::decode_graph(int B, int ctx, bool greedy) {
+  const auto key = std::make_tuple(B, ctx, greedy);
+  {
+    std::lock_guard<std::mutex> lk(gmu_);
+    auto it = dgraphs_.find(key);
+    if (it != dgraphs_.end()) return it->second.get();
+  }
+  if (!provider_) throw std::runtime_error("no decode graph for this batch / context bucket");
+  drain();  // the provider captures on the GPU: nothing of ours may be in flight
+  provider_("decode", B, ctx, greedy);
+  std::lock_guard<std::mutex> lk(gmu_);
+  auto it = dgraphs_.find(key);
+  if (it == dgraphs_.end()) throw std::runtime_error("graph provider registered no decode graph");
+  return it->second.get();
+}
+
+const PrefillGraphDesc* EngineLoop::prefill_graph(int rows, int nseq, bool greedy) {
+  const auto key = std::make_tuple(rows, nseq, greedy);
+  {
+    std::lock_guard<std::mutex> lk(gmu_);
+    auto it = pgraphs_.find(key);
+    if (it != pgraphs_.end()) return it->second.get();
+  }
+  if (!provider_) return nullptr;
+  drain();
+  provider_("prefill", rows, nseq, greedy);
+  std::lock_guard<std::mutex> lk(gmu_);
+  auto it = pgraphs_.find(key);
+  return it == pgraphs_.end() ? nullptr : it->second.get();
+}
+
+// ------------------------------------------------------------------ lifecycle
+void EngineLoop::start() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (started_) return;
+  const HipApi& h = hip_api();
+  if (!h.ok) throw std::runtime_error("native engine loop: " + h.error);
+  started_ = true;
+  th_ = std::thread([this] { run(); });
+}
+
+void EngineLoop::stop() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  done_cv_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+int64_t EngineLoop::submit(const std::vector<int>& prompt, int max_new, bool stop_on_eos,
+                           const LoopSampling& s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!dead_.empty()) throw std::runtime_error("engine replica is down: " + dead_);
+  const int64_t id = sched_.add((int)prompt.size(), max_new, stop_on_eos, cfg_.eos);
+  Req& r = reqs_[id];
+  r.prompt = prompt;
+  r.samp = s;
+  r.t_submit = now_ns();
+  cv_.notify_all();
+  return id;
+}
+
+void EngineLoop::cancel(int64_t id) {
+  std::lock_guard<std::mutex> lk(mu_);
+  cancels_.insert(id);
+  cv_.notify_all();
+}
+
+bool EngineLoop::wait(int64_t id, double timeout_s, LoopResult* out) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto it = reqs_.find(id);
+  if (it == reqs_.end()) throw std::runtime_error("unknown request " + std::to_string(id));
+  auto ready = [&] { return it->second.done || stop_ || !dead_.empty(); };
+  if (timeout_s < 0)
+    done_cv_.wait(lk, ready);
+  else
+    done_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), ready);
+  const Req& r = it->second;
+  const SchedRequest& s = sched_.get(id);
+  out->tokens = s.tokens;
+  out->done = r.done;
+  out->error = r.error;
+  out->done_reason = s.finish_reason.empty() ? (r.done ? "stop" : "") : s.finish_reason;
+  out->prompt_eval_count = s.prompt_len;
+  const int64_t t_first = r.t_first ? r.t_first : now_ns();
+  const int64_t t_end = r.t_done ? r.t_done : now_ns();
+  out->prompt_eval_ns = t_first - (r.t_admit ? r.t_admit : r.t_submit);
+  out->eval_ns = t_end - t_first;
+  out->total_ns = t_end - r.t_submit;
+  out->ttft_ns = t_first - r.t_submit;
+  return r.done;
+}
+
+std::vector<int> EngineLoop::wait_tokens(int64_t id, size_t have, double timeout_s, bool* done) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto it = reqs_.find(id);
+  if (it == reqs_.end()) throw std::runtime_error("unknown request " + std::to_string(id));
+  auto ready = [&] {
+    return it->second.done || stop_ || !dead_.empty() || sched_.get(id).tokens.size() > have;
+  };
+  done_cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.0, timeout_s)), ready);
+  const auto& toks = sched_.get(id).tokens;
+  *done = it->second.done;
+  if (toks.size() <= have) return {};
+  return std::vector<int>(toks.begin() + have, toks.end());
+}
+
+void EngineLoop::release(int64_t id) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = reqs_.find(id);
+  if (it == reqs_.end()) return;
+  if (it->second.done) {
+    sched_.release(id);
+    reqs_.erase(it);
+  } else {
+    it->second.released = true;  // dropped when it finishes
+    cancels_.insert(id);
+    cv_.notify_all();
+  }
+}
+
+void EngineLoop::stall(double seconds) {
+  std::lock_guard<std::mutex> lk(mu_);
+  stall_until_ = now_ns() + (int64_t)(seconds * 1e9);
+  cv_.notify_all();
+}
+
+std::string EngineLoop::dead() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return dead_;
+}
+
+std::map<std::string, double> EngineLoop::metrics() {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::map<std::string, double> m;
+  m["requests"] = n_requests_;
+  m["tokens"] = n_tokens_;
+  m["prefill_calls"] = n_prefill_calls_;
+  m["prefill_tokens"] = n_prefill_tokens_;
+  m["eager_prefill_calls"] = n_eager_prefill_;
+  m["decode_calls"] = n_decode_calls_;
+  m["decode_steps"] = n_decode_steps_;
+  m["speculated_chunks"] = n_speculated_;
+  m["state_loads"] = n_loads_;
+  m["errors"] = n_errors_;
+  m["busy_s"] = busy_ns_ * 1e-9;
+  m["prefill_s"] = prefill_ns_ * 1e-9;
+  m["decode_s"] = decode_ns_ * 1e-9;
+  m["running"] = sched_.n_running();
+  m["waiting"] = sched_.n_waiting();
+  m["free_kv_pages"] = sched_.free_pages();
+  m["native_loop"] = 1;
+  return m;
+}
+
+// ------------------------------------------------------------------ the loop
+void EngineLoop::run() {
+  const HipApi& h = hip_api();
+  try {
+    hip_check(h.setDevice(cfg_.device), "hipSetDevice");
+    hip_check(h.streamCreateWithFlags(&stream_, 1 /* hipStreamNonBlocking */), "hipStreamCreate");
+    for (int i = 0; i < 2; ++i) {
+      void* e = nullptr;
+      hip_check(h.eventCreateWithFlags(&e, 2 /* hipEventDisableTiming */), "hipEventCreate");
+      events_.push_back(e);
+    }
+  } catch (const std::exception& e) {
+    std::lock_guard<std::mutex> lk(mu_);
+    dead_ = e.what();
+    done_cv_.notify_all();
+    return;
+  }
+  while (true) {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      while (!stop_ && flight_.empty() && cancels_.empty() && sched_.n_running() == 0 &&
+             sched_.n_waiting() == 0)
+        cv_.wait_for(lk, std::chrono::milliseconds(500));
+      while (!stop_ && now_ns() < stall_until_)
+        cv_.wait_for(lk, std::chrono::nanoseconds(std::min<int64_t>(stall_until_ - now_ns(),
+                                                                     50000000)));
+      if (stop_) break;
+    }
+    const int64_t t0 = now_ns();
+    try {
+      step();
+    } catch (const std::exception& e) {
+      fail_all(e.what());
+    }
+    busy_ns_ += now_ns() - t0;
+  }
+  try {
+    drain();
+  } catch (...) {
+  }
+}
+
+void EngineLoop::fail_all(const std::string& why) {
+  try {
+    drain();
+  } catch (...) {
+    flight_.clear();
+  }
+  loaded_ = nullptr;
+  std::lock_guard<std::mutex> lk(mu_);
+  n_errors_++;
+  for (auto& kv : reqs_) {
+    if (kv.second.done) continue;
+    kv.second.error = why;
+    sched_.cancel(kv.first);
+  }
+  sched_.flush_deferred();
+  const int64_t t = now_ns();
+  for (int64_t id : sched_.take_finished()) {
+    auto it = reqs_.find(id);
+    if (it == reqs_.end()) continue;
+    it->second.done = true;
+    it->second.t_done = t;
+    if (it->second.released) {
+      sched_.release(id);
+      reqs_.erase(it);
+    }
+  }
+  done_cv_.notify_all();
+}
+
+void EngineLoop::step() {
+  std::vector<int64_t> admitted;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int64_t id : cancels_) sched_.cancel(id);
+    cancels_.clear();
+    SchedPlan plan = sched_.schedule();
+    admitted = plan.prefill;
+    const int64_t t = now_ns();
+    for (int64_t id : admitted) reqs_[id].t_admit = t;
+  }
+  if (!admitted.empty()) run_prefill(admitted);
+  std::vector<int64_t> running;
+  bool waiting;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    running = sched_.running();
+    waiting = sched_.n_waiting() > 0;
+  }
+  if (!admitted.empty() && cfg_.prefill_first && waiting) running.clear();
+  if (!running.empty()) {
+    decode(running, waiting);
+  } else if (!flight_.empty()) {
+    drain();
+  }
+  // retire
+  int done = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    const int64_t t = now_ns();
+    for (int64_t id : sched_.take_finished()) {
+      auto it = reqs_.find(id);
+      if (it == reqs_.end()) continue;
+      ++done;
+      Req& r = it->second;
+      r.done = true;
+      r.t_done = t;
+      if (!r.t_first) r.t_first = t;
+      n_requests_++;
+      n_tokens_ += (long)sched_.get(id).tokens.size();
+      if (r.released) {
+        sched_.release(id);
+        reqs_.erase(it);
+      }
+    }
+    if (done) done_cv_.notify_all();
+  }
+  if (done && cfg_.admit_wait_us > 0) {
+    // replies just went out: their peers usually send the next request within a fraction
+    // of a millisecond -- admit it at THIS step boundary (bounded wait; only while a batch
+    // slot is free, so a full batch never waits)
+    std::unique_lock<std::mutex> lk(mu_);
+    const int free = cfg_.max_batch - sched_.n_running() - sched_.n_waiting();
+    if (free > 0) {
+      const int want = std::min(done, free);
+      cv_.wait_for(lk, std::chrono::microseconds((int64_t)cfg_.admit_wait_us),
+                   [&] { return stop_ || sched_.n_waiting() >= want; });
+    }
+  }
+}
+
+// ------------------------------------------------------------------ prefill
+void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
+  const HipApi& h = hip_api();
+  drain();  // riders' last tokens must be current; nothing may write KV concurrently
+  loaded_ = nullptr;  // the decode state no longer matches (new rows; riders advance)
+  const int64_t t0 = now_ns();
+  struct Seq {
+    int64_t id;
+    const std::vector<int>* prompt;  // admitted: the prompt
+    int pos = 0, tok = 0;            // rider: one row
+    std::vector<int> pages;
+    LoopSampling samp;
+  };
+  std::vector<Seq> seqs;
+  std::vector<int64_t> riders;
+  int n_rows = 0, max_pages_needed = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int64_t id : admitted) {
+      Seq s;
+      s.id = id;
+      s.prompt = &reqs_[id].prompt;
+      s.pages = sched_.get(id).pages;
+      s.samp = reqs_[id].samp;
+      n_rows += (int)s.prompt->size();
+      max_pages_needed = std::max(max_pages_needed, (int)((s.prompt->size() + 63) / 64));
+      seqs.push_back(std::move(s));
+    }
+    if (cfg_.mixed) {
+      // running sequences fill the chunk's last 64-row tile, never start another one
+      int room = (n_rows + 63) / 64 * 64 - n_rows;
+      for (int64_t id : sched_.running()) {
+        if (room <= 0 || (int)seqs.size() >= cfg_.max_batch) break;
+        if (std::find(admitted.begin(), admitted.end(), id) != admitted.end()) continue;
+        const SchedRequest& r = sched_.get(id);
+        if (r.state != RUNNING || r.tokens.empty()) continue;
+        Seq s;
+        s.id = id;
+        s.prompt = nullptr;
+        s.pos = r.pos;
+        s.tok = r.tokens.back();
+        s.pages = r.pages;
+        s.samp = reqs_[id].samp;
+        max_pages_needed = std::max(max_pages_needed, r.pos / 64 + 1);
+        seqs.push_back(std::move(s));
+        riders.push_back(id);
+        --room;
+        ++n_rows;
+      }
+    }
+  }
+  const int nseq = (int)seqs.size();
+  bool greedy = true;
+  for (auto& s : seqs) greedy &= s.samp.greedy();
+  const int rb = bucket(n_rows, cfg_.row_buckets);
+  const int sb = std::min(bucket(nseq, cfg_.batch_buckets), cfg_.max_batch);
+  const PrefillGraphDesc* g = nullptr;
+  if (rb > 0 && sb >= nseq && max_pages_needed <= cfg_.prefill_max_pages)
+    g = prefill_graph(rb, sb, greedy);
+  std::vector<int> first(nseq, 0);
+  if (!g) {
+    // beyond every captured shape (a long prompt): Python's chunked eager prefill, without
+    // riders (they decode in the next step instead)
+    if (!eager_) throw std::runtime_error("prompt exceeds the captured prefill shapes");
+    std::vector<std::vector<int>> prompts, pages;
+    std::vector<int> starts;
+    std::vector<LoopSampling> samp;
+    for (auto& s : seqs) {
+      if (!s.prompt) continue;
+      prompts.push_back(*s.prompt);
+      pages.push_back(s.pages);
+      starts.push_back(0);
+      samp.push_back(s.samp);
+    }
+    riders.clear();
+    first = eager_(prompts, pages, starts, samp);
+    n_eager_prefill_++;
+  } else {
+    // chunk metadata (PrefillGraph.host_meta, engine/graph.py)
+    int32_t* m = (int32_t*)pinned(kPrefillMeta, g->meta_len * 4);
+    std::memset(m, 0, g->meta_len * 4);
+    const int P = g->max_pages, R = g->rows, S = g->n_seq;
+    int32_t* bt = m + g->off_bt;
+    int32_t* seq = m + g->off_seq;
+    int32_t* pos = m + g->off_pos;
+    int32_t* ids = m + g->off_ids;
+    int32_t* slots = m + g->off_slots;
+    int32_t* ctx = m + g->off_ctx;
+    int32_t* out = m + g->off_out;
+    int32_t* spos = m + g->off_spos;
+    int32_t* tiles = m + g->off_tiles;
+    int r = 0;
+    for (int b = 0; b < nseq; ++b) {
+      const Seq& s = seqs[b];
+      for (size_t i = 0; i < s.pages.size() && (int)i < P; ++i) bt[b * P + i] = s.pages[i];
+      if (s.prompt) {
+        for (size_t i = 0; i < s.prompt->size(); ++i, ++r) {
+          seq[r] = b;
+          pos[r] = (int)i;
+          ids[r] = (*s.prompt)[i];
+        }
+      } else {
+        seq[r] = b;
+        pos[r] = s.pos;
+        ids[r] = s.tok;
+        ++r;
+      }
+      out[b] = r - 1;
+      spos[b] = pos[r - 1];
+    }
+    const int n = r;
+    for (int i = n; i < R; ++i) {  // dummy rows: sequence S (the null page), no KV write
+      seq[i] = S;
+      pos[i] = i - n;
+    }
+    for (int i = 0; i < R; ++i) {
+      const int p = pos[i];
+      slots[i] = i < n ? bt[seq[i] * P + p / 64] * 64 + p % 64 : -1;
+      ctx[i] = p + 1;
+    }
+    int nt = 0;
+    for (int i = 0; i < R;) {  // runs of consecutive positions of one sequence, cut at qtile
+      int e = i + 1;
+      while (e < R && e - i < g->qtile && seq[e] == seq[i] && pos[e] == pos[e - 1] + 1) ++e;
+      if (nt >= g->max_tiles) throw std::runtime_error("prefill tiles exceed the graph's bound");
+      tiles[4 * nt] = i;
+      tiles[4 * nt + 1] = e - i;
+      tiles[4 * nt + 2] = seq[i];
+      tiles[4 * nt + 3] = pos[i];
+      ++nt;
+      i = e;
+    }
+    hip_check(h.memcpyAsync(g->meta, m, g->meta_len * 4, kH2D, stream_), "prefill meta H2D");
+    if (!g->greedy) {
+      float* tf = (float*)pinned(kSampF, S * 4);
+      int32_t* tk = (int32_t*)pinned(kSampI, S * 4);
+      float* tp = (float*)pinned(kSampP, S * 4);
+      int64_t* sd = (int64_t*)pinned(kSampS, S * 8);
+      for (int b = 0; b < S; ++b) {
+        const LoopSampling d = b < nseq ? seqs[b].samp : LoopSampling();
+        tf[b] = d.temperature;
+        tk[b] = d.top_k;
+        tp[b] = d.top_p;
+        sd[b] = d.seed;
+      }
+      hip_check(h.memcpyAsync(g->temp, tf, S * 4, kH2D, stream_), "samp H2D");
+      hip_check(h.memcpyAsync(g->topk, tk, S * 4, kH2D, stream_), "samp H2D");
+      hip_check(h.memcpyAsync(g->topp, tp, S * 4, kH2D, stream_), "samp H2D");
+      hip_check(h.memcpyAsync(g->seeds, sd, S * 8, kH2D, stream_), "samp H2D");
+    }
+    hip_check(h.graphLaunch(g->exec, stream_), "prefill graph launch");
+    int32_t* f = (int32_t*)pinned(kFirst, S * 4);
+    hip_check(h.memcpyAsync(f, g->first, nseq * 4, kD2H, stream_), "first tokens D2H");
+    int32_t* ew = (int32_t*)pinned(kErr0 + 2, 4);
+    if (g->err) hip_check(h.memcpyAsync(ew, g->err, 4, kD2H, stream_), "fault word D2H");
+    hip_check(h.streamSynchronize(stream_), "prefill sync");
+    if (g->err && *ew != 0) throw std::runtime_error("kernel fault word set during prefill");
+    for (int b = 0; b < nseq; ++b) first[b] = f[b];
+  }
+  const int64_t t1 = now_ns();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    int b = 0;
+    for (auto& s : seqs) {
+      if (!s.prompt) break;
+      auto it = reqs_.find(s.id);
+      if (it != reqs_.end()) it->second.t_first = t1;
+      sched_.on_first_token(s.id, first[b]);
+      n_prefill_tokens_ += (long)s.prompt->size();
+      ++b;
+    }
+    if (!riders.empty()) {
+      std::vector<std::vector<int>> toks;
+      for (size_t i = 0; i < riders.size(); ++i) toks.push_back({first[b + i]});
+      sched_.on_decode_tokens(riders, toks);
+      n_decode_steps_++;
+    }
+    n_prefill_calls_++;
+    prefill_ns_ += t1 - t0;
+  }
+  done_cv_.notify_all();
+}
+
+// ------------------------------------------------------------------ decode
+void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_t>& ids,
+                              bool load, int k) {
+  const HipApi& h = hip_api();
+  if (load) {
+    const int B = g->B, P = g->max_pages;
+    const size_t n = (size_t)B * (4 + P);
+    int32_t* m = (int32_t*)pinned(kDecodeMeta, n * 4);
+    std::memset(m, 0, n * 4);
+    int32_t *idv = m, *pos = m + B, *ctx = m + 2 * B, *slots = m + 3 * B, *bt = m + 4 * B;
+    std::vector<std::tuple<float, int, float, int64_t>> samp;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t b = 0; b < ids.size(); ++b) {
+        const SchedRequest& r = sched_.get(ids[b]);
+        for (size_t i = 0; i < r.pages.size() && (int)i < P; ++i) bt[b * P + i] = r.pages[i];
+        idv[b] = r.tokens.empty() ? 0 : r.tokens.back();
+        pos[b] = r.pos;
+        const LoopSampling& s = reqs_[ids[b]].samp;
+        samp.emplace_back(s.temperature, s.top_k, s.top_p, s.seed);
+      }
+    }
+    for (int b = 0; b < B; ++b) {  // rows >= n: dummies on the null page at position 0
+      ctx[b] = pos[b] + 1;
+      slots[b] = bt[b * P + pos[b] / 64] * 64 + pos[b] % 64;
+    }
+    hip_check(h.memcpyAsync(g->meta, m, n * 4, kH2D, stream_), "decode meta H2D");
+    hip_check(h.memsetAsync(g->step, 0, 4, stream_), "step reset");
+    if (g->keys && g->keys_bytes)
+      hip_check(h.memsetAsync(g->keys, 0, g->keys_bytes, stream_), "keys reset");
+    if (!g->greedy) {
+      float* tf = (float*)pinned(kSampF, B * 4);
+      int32_t* tk = (int32_t*)pinned(kSampI, B * 4);
+      float* tp = (float*)pinned(kSampP, B * 4);
+      int64_t* sd = (int64_t*)pinned(kSampS, B * 8);
+      for (int b = 0; b < B; ++b) {
+        if (b < (int)samp.size()) {
+          tf[b] = std::get<0>(samp[b]);
+          tk[b] = std::get<1>(samp[b]);
+          tp[b] = std::get<2>(samp[b]);
+          sd[b] = std::get<3>(samp[b]);
+        } else {
+          tf[b] = 0.f;
+          tk[b] = 40;
+          tp[b] = 0.9f;
+          sd[b] = 0;
+        }
+      }
+      hip_check(h.memcpyAsync(g->temp, tf, B * 4, kH2D, stream_), "samp H2D");
+      hip_check(h.memcpyAsync(g->topk, tk, B * 4, kH2D, stream_), "samp H2D");
+      hip_check(h.memcpyAsync(g->topp, tp, B * 4, kH2D, stream_), "samp H2D");
+      hip_check(h.memcpyAsync(g->seeds, sd, B * 8, kH2D, stream_), "samp H2D");
+    }
+    loaded_ = g;
+    loaded_ids_ = ids;
+    loaded_steps_ = 0;
+    n_loads_++;
+  }
+  for (int i = 0; i < k; ++i) hip_check(h.graphLaunch(g->exec, stream_), "decode graph launch");
+  Chunk c;
+  c.g = g;
+  c.ids = ids;
+  c.s0 = loaded_steps_;
+  c.k = k;
+  c.buf = hist_buf_;
+  hist_buf_ ^= 1;
+  // this chunk's k columns of every row: [B, k] packed
+  const size_t hb = (size_t)g->B * k * 4;
+  void* dst = pinned(kHist0 + c.buf, hb);
+  hip_check(h.memcpy2DAsync(dst, (size_t)k * 4, g->hist + c.s0, (size_t)g->max_steps * 4,
+                            (size_t)k * 4, g->B, kD2H, stream_),
+            "hist D2H");
+  if (g->err)
+    hip_check(h.memcpyAsync(pinned(kErr0 + c.buf, 4), g->err, 4, kD2H, stream_), "fault D2H");
+  c.ev = events_[c.buf];
+  hip_check(h.eventRecord(c.ev, stream_), "hipEventRecord");
+  loaded_steps_ += k;
+  flight_.push_back(std::move(c));
+  n_decode_calls_++;
+}
+
+void EngineLoop::collect() {
+  const HipApi& h = hip_api();
+  Chunk c = std::move(flight_.front());
+  flight_.pop_front();
+  hip_check(h.eventSynchronize(c.ev), "decode chunk sync");
+  if (c.g->err && *(int32_t*)pinned_[kErr0 + c.buf].first != 0)
+    throw std::runtime_error("kernel fault word set during decode (results invalid)");
+  const int32_t* hist = (const int32_t*)pinned_[kHist0 + c.buf].first;
+  std::vector<std::vector<int>> toks(c.ids.size());
+  for (size_t b = 0; b < c.ids.size(); ++b) {
+    const int32_t* row = hist + (size_t)b * c.k;
+    toks[b].assign(row, row + c.k);
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    sched_.on_decode_tokens(c.ids, toks);
+    n_decode_steps_ += c.k;
+    if (flight_.empty()) sched_.flush_deferred();  // nothing in flight can touch them now
+  }
+  done_cv_.notify_all();
+}
+
+void EngineLoop::drain() {
+  while (!flight_.empty()) collect();
+}
+
+void EngineLoop::decode(const std::vector<int64_t>& running_in, bool waiting) {
+  const int64_t t0 = now_ns();
+  std::vector<int64_t> running = running_in;
+  // chunk length: long chunks amortise the host round trip; a waiting request shortens it
+  // (it is admitted at the next chunk boundary)
+  const int k = waiting ? 2 : ((int)running.size() < cfg_.max_batch ? std::max(2, cfg_.decode_chunk / 2)
+                                                                    : cfg_.decode_chunk);
+  auto pick = [&](const std::vector<int64_t>& ids) {
+    int need = 1;
+    bool greedy = true;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int64_t id : ids) {
+      const SchedRequest& r = sched_.get(id);
+      // slack: a chunk may run past a request's end while the host reads the previous one
+      need = std::max(need, r.prompt_len + r.max_new + 2 * cfg_.decode_chunk + 2);
+      greedy &= reqs_[id].samp.greedy();
+    }
+    const int B = bucket((int)ids.size(), cfg_.batch_buckets);
+    const int C = bucket(need, cfg_.ctx_buckets);
+    if (B < 0 || C < 0) throw std::runtime_error("decode batch / context exceeds the buckets");
+    return std::make_tuple(B, C, greedy);
+  };
+  auto [B, C, greedy] = pick(running);
+  const DecodeGraphDesc* g = decode_graph(B, C, greedy);
+  if (cfg_.pipeline && !flight_.empty() && flight_.back().g == g && flight_.back().ids == running &&
+      loaded_ == g && loaded_steps_ + k <= g->max_steps) {
+    // the running set is unchanged as far as the host knows: enqueue the next chunk on the
+    // device-resident state, then read the previous one while it runs
+    launch_chunk(g, running, false, k);
+    n_speculated_++;
+    collect();
+    decode_ns_ += now_ns() - t0;
+    return;
+  }
+  drain();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    running = sched_.running();
+  }
+  if (running.empty()) return;
+  std::tie(B, C, greedy) = pick(running);
+  g = decode_graph(B, C, greedy);
+  const bool load = !(loaded_ == g && loaded_ids_ == running && loaded_steps_ + k <= g->max_steps);
+  launch_chunk(g, running, load, k);
+  if (!cfg_.pipeline) collect();
+  decode_ns_ += now_ns() - t0;
+}
+
+}  // namespace p2p

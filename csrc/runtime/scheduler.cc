@@ -101,7 +101,10 @@ void Scheduler::finish(SchedRequest& r, const char* reason) {
   if (r.state != RUNNING) return;
   r.state = FINISHED;
   r.finish_reason = reason;
-  alloc_.free(r.pages);
+  if (defer_free_)
+    deferred_.insert(deferred_.end(), r.pages.begin(), r.pages.end());
+  else
+    alloc_.free(r.pages);
   r.pages.clear();
   running_.erase(std::remove(running_.begin(), running_.end(), r.id), running_.end());
   finished_.push_back(r.id);
@@ -140,6 +143,12 @@ void Scheduler::on_decode_tokens(const std::vector<int64_t>& ids,
       if ((int)r.tokens.size() >= r.max_new) finish(r, "length");
     }
   }
+}
+
+void Scheduler::flush_deferred() {
+  if (deferred_.empty()) return;
+  alloc_.free(deferred_);
+  deferred_.clear();
 }
 
 std::vector<int64_t> Scheduler::take_finished() {

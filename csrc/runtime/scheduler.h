@@ -68,8 +68,15 @@ class Scheduler {
   void release(int64_t id);  // forget a finished request (frees nothing else)
   int n_waiting() const { return (int)waiting_.size(); }
   int n_running() const { return (int)running_.size(); }
+  const std::vector<int64_t>& running() const { return running_; }
   int free_pages() const { return alloc_.free_count(); }
   int page_size() const { return page_size_; }
+  // Deferred page release: a finished request's pages are held back until
+  // flush_deferred() -- the native loop keeps a decode chunk in flight while it reads
+  // the previous one, and that chunk may still write KV for a request that just hit EOS.
+  void set_defer_free(bool on) { defer_free_ = on; }
+  void flush_deferred();
+  int n_deferred_pages() const { return (int)deferred_.size(); }
 
  private:
   void finish(SchedRequest& r, const char* reason);
@@ -80,6 +87,8 @@ class Scheduler {
   std::deque<int64_t> waiting_;
   std::vector<int64_t> running_;
   std::vector<int64_t> finished_;
+  bool defer_free_ = false;
+  std::vector<int> deferred_;
 };
 
 }  // namespace p2p

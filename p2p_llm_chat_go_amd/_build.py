@@ -156,7 +156,7 @@ def build_native(force=False, jobs=8):
         pyinc = sysconfig.get_paths()["include"]
         if force or _stale(mod, bind + [ar] + hdrs):
             _run([CXX] + base + ["-shared", "-I", pybind11.get_include(), "-I", pyinc] + bind
-                 + [ar, "-o", mod] + libs)
+                 + [ar, "-o", mod] + libs + ["-ldl"])
         outs.append(mod)
     # engine C ABI (embeds the interpreter that drives the Python/HIP engine)
     eng_src = sorted(glob.glob(os.path.join(CSRC, "engine", "*.cc")))

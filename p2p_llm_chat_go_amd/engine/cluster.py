@@ -388,10 +388,15 @@ def _leader_main(spec, replica, eng, parent_conn, follower_conns):
     group = spec.get("tp", 1) * spec.get("ep", 1)
     split = spec.get("ep", 1) > 1 and spec.get("ep_mode", "allreduce") == "a2a"
     front = LockstepEngine(eng, follower_conns, dp_split=split) if group > 1 else eng
-    server = EngineServer(front, get_tokenizer(eng.cfg, spec.get("tokenizer")
-                                               or spec.get("checkpoint")),
-                          model_name=spec.get("model_name", "llama3.1"),
-                          default_max_tokens=spec.get("max_tokens", 128))
+    tok = get_tokenizer(eng.cfg, spec.get("tokenizer") or spec.get("checkpoint"))
+    kw = dict(model_name=spec.get("model_name", "llama3.1"),
+              default_max_tokens=spec.get("max_tokens", 128))
+    if group == 1:  # a single-GPU replica runs the native step loop when it can
+        from .native_loop import make_server
+
+        server = make_server(eng, tok, **kw)
+    else:  # TP/EP groups: the Python loop, whose calls the leader broadcasts
+        server = EngineServer(front, tok, **kw)
     send_lock = threading.Lock()
     cancelled = set()
 

@@ -307,13 +307,11 @@ class Engine:
         for j, r in enumerate(rows):  # rows are grouped by sequence, in order
             last[r[0]] = j
         g.load(g.host_meta(rows, block_tables, last))
+        if sampled:
+            g.samp._key = None  # the native loop may have written these slots directly
+            g.samp.load(list(sampling))
         g.replay()
-        if not sampled:
-            return g.first[:B]
-        from .sampling import sample
-
-        res = g.ws.logits[:B]
-        return sample(res, list(sampling), [len(p) - 1 for p in prompts])
+        return g.first[:B]
 
     # --------------------------------------------------------------- decode
     def decode_steps(self, last_ids: list, pos: list, block_tables: list, ctx: int, k: int,

@@ -180,6 +180,20 @@ class DecodeGraph:
             else:
                 self.state.body()
 
+    def describe(self) -> dict:
+        """Addresses and layout for the native loop (runtime/engine_loop.h DecodeGraphDesc)."""
+        st = self.state
+        d = {"B": st.B, "max_pages": st.max_pages, "ctx": st.max_ctx, "greedy": self.greedy,
+             "exec": self.graph.raw_cuda_graph_exec(), "meta": st.meta.data_ptr(),
+             "hist": st.hist.data_ptr(), "max_steps": st.max_steps, "step": st.step.data_ptr(),
+             "keys": st.ws.keys.data_ptr(), "keys_bytes": st.ws.keys.numel() * 8,
+             "err": st.ws.err.data_ptr()}
+        if not self.greedy:
+            sp = st.samp
+            d.update(temp=sp.temp.data_ptr(), topk=sp.topk.data_ptr(), topp=sp.topp.data_ptr(),
+                     seeds=sp.seeds.data_ptr())
+        return d
+
     def step_sampled(self, params: list, n: int = 1):
         """n decode steps with per-row SamplingParams (temperature <= 0 rows stay greedy):
         the parameters are loaded into device slots (only when they change), then each
@@ -227,7 +241,7 @@ class PrefillGraph:
         self.max_tiles = -(-rows // self.qtile) + n_seq + 1
         R, S = rows, n_seq
         sizes = [("bt", (S + 1) * max_pages), ("seq", R), ("pos", R), ("ids", R), ("slots", R),
-                 ("ctx", R), ("out", S), ("tiles", 4 * self.max_tiles)]
+                 ("ctx", R), ("out", S), ("spos", S), ("tiles", 4 * self.max_tiles)]
         self.offsets = {}
         o = 0
         for name, n in sizes:
@@ -239,8 +253,14 @@ class PrefillGraph:
         self.seq, self.pos, self.ids, self.slots, self.ctx = (v[k] for k in ("seq", "pos", "ids",
                                                                                "slots", "ctx"))
         self.out_rows = v["out"]
+        self.spos = v["spos"]  # position each output row's token is drawn for (sampling)
         self.tiles = v["tiles"].view(self.max_tiles, 4)
         self.first = torch.zeros(S, device=dev, dtype=torch.int32)
+        self.samp = None
+        if not greedy:  # per-sequence sampling parameters, read by the captured ops.sample
+            from .sampling import SamplerSlots
+
+            self.samp = SamplerSlots(S, dev)
         self.graph = None
 
     # ------------------------------------------------------------------ host side
@@ -269,6 +289,7 @@ class PrefillGraph:
         v["slots"][:] = slots
         v["ctx"][:] = pos + 1
         v["out"][:len(out_rows)] = out_rows
+        v["spos"][:] = pos[v["out"]]
         # query tiles: runs of consecutive positions of one sequence, cut at qtile rows
         # (ops.prefill_tiles); the rest stay n = 0 padding tiles
         brk = np.flatnonzero((seq[1:] != seq[:-1]) | (pos[1:] != pos[:-1] + 1)) + 1
@@ -293,6 +314,10 @@ class PrefillGraph:
                         greedy=self.greedy, tiles=self.tiles, qtile=self.qtile)
         if self.greedy:
             m.finalize_greedy(ws, self.n_out, out=self.first)
+        else:
+            sp = self.samp
+            ops.sample(ws.logits[:self.n_out], sp.temp, sp.topk, sp.topp, sp.seeds, self.spos,
+                       out=self.first)
         return res
 
     def capture(self, warmup: int = 2):
@@ -314,7 +339,22 @@ class PrefillGraph:
         return self
 
     def replay(self):
-        """Runs the loaded chunk.  Greedy: the first tokens are in ``self.first[:n]``;
-        else the fp32 logits of the output rows in ``self.ws.logits[:n]`` (both are
-        overwritten by the next replay)."""
+        """Runs the loaded chunk: the first token of every sequence lands in
+        ``self.first[:n]`` (greedy argmax, or drawn with the parameters loaded into
+        ``self.samp``); the sampled graph also leaves the fp32 logits of the output rows in
+        ``self.ws.logits[:n]``.  Both are overwritten by the next replay."""
         self.graph.replay()
+
+    def describe(self) -> dict:
+        """Addresses and layout for the native loop (runtime/engine_loop.h PrefillGraphDesc)."""
+        d = {"rows": self.rows, "n_seq": self.n_seq, "max_pages": self.max_pages,
+             "qtile": self.qtile, "max_tiles": self.max_tiles, "greedy": self.greedy,
+             "exec": self.graph.raw_cuda_graph_exec(), "meta": self.meta.data_ptr(),
+             "meta_len": self.meta.numel(), "first": self.first.data_ptr(),
+             "err": self.ws.err.data_ptr()}
+        for name, (a, _n) in self.offsets.items():
+            d["off_" + name] = a
+        if self.samp is not None:
+            d.update(temp=self.samp.temp.data_ptr(), topk=self.samp.topk.data_ptr(),
+                     topp=self.samp.topp.data_ptr(), seeds=self.samp.seeds.data_ptr())
+        return d

@@ -1,0 +1,216 @@
+"""The suggest-reply server on the native engine loop (``csrc/runtime/engine_loop.cc``).
+
+Same interface as :class:`engine.server.EngineServer` (the node's generate hooks), but
+the continuous-batching step loop runs in a C++ thread: admission, prefill launches,
+decode-chunk control, finish detection and KV-page release never enter Python.  Python
+only tokenises / formats at the HTTP boundary and, once per new shape, captures a graph
+for the loop (``provider``).  The loop replays:
+
+  * prefill chunks: ``engine.graph.PrefillGraph`` (row bucket x sequence bucket, greedy
+    argmax or in-graph sampling), with running sequences riding along as one row each;
+  * decode steps: ``engine.graph.DecodeGraph`` per (batch bucket, context bucket),
+    chunk i+1 enqueued before chunk i is read, the batch state reloaded only when the
+    running set changes.
+
+Prompts longer than the largest prefill bucket fall back to Python's chunked prefill
+(``eager``).  Used for single-GPU replicas (TP = EP = 1) when the engine runs its graphs
+on a GPU (``ENGINE_NATIVE_LOOP``, default on); TP/EP groups keep the Python loop, whose
+calls the cluster broadcasts to the follower ranks.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+from ..native import load as load_native
+from .engine import BATCH_BUCKETS, CTX_BUCKETS, Engine
+from .graph import PREFILL_ROW_BUCKETS
+from .sampling import SamplingParams
+from .server import EngineServer, EngineTimeout
+from .tokenizer import get_tokenizer
+
+# context bucket (block-table width) of the loop's prefill graphs: prompts up to this many
+# tokens prefill through a captured graph; longer ones through the eager chunked path
+PREFILL_CTX = int(os.environ.get("ENGINE_PREFILL_GRAPH_CTX", "4096"))
+
+
+def native_loop_ok(engine: Engine) -> bool:
+    return (engine.device.type == "cuda" and engine.use_graph and engine.model.tp == 1
+            and engine.prefill_graphs_enabled
+            and os.environ.get("ENGINE_NATIVE_LOOP", "1") != "0")
+
+
+class NativeEngineServer(EngineServer):
+    def __init__(self, engine: Engine, tokenizer=None, model_name: str = "llama3.1",
+                 max_batch: int | None = None, decode_chunk: int = 8,
+                 default_max_tokens: int = 128, max_ctx: int | None = None,
+                 prewarm: bool = True, prefill_ctx: int | None = None):
+        # no Python engine thread: the EngineServer state this class uses is set here
+        self.engine = engine
+        self.tok = tokenizer or get_tokenizer(engine.cfg)
+        self.model_name = model_name
+        self.max_batch = max_batch or engine.max_batch
+        self.decode_chunk = decode_chunk
+        self.default_max_tokens = default_max_tokens
+        self.request_timeout_s = float(os.environ.get("ENGINE_TIMEOUT", "60"))
+        self.max_ctx = max_ctx or min(engine.cfg.max_pos, CTX_BUCKETS[-1],
+                                      engine.kv.num_pages * 64)
+        self.errors = 0
+        self.prefill_ctx = min(prefill_ctx or PREFILL_CTX, CTX_BUCKETS[-1])
+        N = load_native()
+        dev = engine.device
+        self.loop = N.EngineLoop({
+            "num_pages": engine.kv.num_pages, "page_size": 64, "max_batch": self.max_batch,
+            "max_prefill_tokens": engine.max_prefill_tokens, "max_ctx": self.max_ctx,
+            "eos": [int(e) for e in engine.cfg.eos_ids], "decode_chunk": decode_chunk,
+            "admit_wait_us": float(os.environ.get("ENGINE_ADMIT_WAIT_US", "500")),
+            "prefill_first": os.environ.get("ENGINE_PREFILL_FIRST", "1") != "0",
+            "mixed": True, "pipeline": os.environ.get("ENGINE_PIPELINE", "1") != "0",
+            "device": dev.index or 0, "batch_buckets": list(BATCH_BUCKETS),
+            "ctx_buckets": list(CTX_BUCKETS),
+            "row_buckets": [r for r in PREFILL_ROW_BUCKETS if r <= engine.max_prefill_tokens],
+            "prefill_max_pages": self.prefill_ctx // 64})
+        self.loop.set_provider(self._provide)
+        self.loop.set_eager_prefill(self._eager_prefill)
+        self._registered = set()
+        if prewarm:
+            self.prewarm()
+        self.loop.start()
+
+    # --------------------------------------------------------------- graphs
+    def _provide(self, kind: str, a: int, b: int, greedy: bool):
+        """Capture (once) and register the graph the loop asked for (loop thread, GIL)."""
+        eng = self.engine
+        key = (kind, a, b, greedy)
+        if key in self._registered:
+            return
+        if kind == "decode":
+            g = eng.decode_graph(a, b, greedy=greedy)
+            self.loop.add_decode_graph(g.describe())
+        else:
+            g = eng.prefill_graph(a, b, self.prefill_ctx, greedy=greedy)
+            self.loop.add_prefill_graph(g.describe())
+        self._registered.add(key)
+
+    def prewarm(self, batches=None, rows=(16, 32, 48, 64, 96, 128)):
+        """Capture the chat-typical shapes before the first request: decode graphs of every
+        batch bucket at the 256-token context, prefill chunks of one prompt."""
+        for B in batches or [b for b in BATCH_BUCKETS if b <= self.max_batch]:
+            self._provide("decode", B, 256, True)
+        for r in rows:
+            if r <= self.engine.max_prefill_tokens:
+                self._provide("prefill", r, 1, True)
+
+    def _eager_prefill(self, prompts, pages, starts, samp):
+        params = [SamplingParams(temperature=t, top_k=k, top_p=p, seed=s) for t, k, p, s in samp]
+        first = self.engine.prefill(prompts, pages, sampling=params,
+                                    starts=starts if any(starts) else None)
+        return [int(x) for x in first.cpu().tolist()]
+
+    # --------------------------------------------------------------- API
+    @property
+    def dead(self):
+        d = self.loop.dead()
+        return d or None
+
+    def _submit(self, prompt_ids, params: SamplingParams) -> int:
+        return self.loop.submit(list(prompt_ids), int(params.max_tokens), bool(params.stop_on_eos),
+                                float(params.temperature), int(params.top_k), float(params.top_p),
+                                int(params.resolved_seed()) if not params.greedy else 0)
+
+    def generate(self, prompt_ids, params: SamplingParams, timeout: float | None = None) -> dict:
+        t = self.request_timeout_s if timeout is None else float(timeout)
+        rid = self._submit(prompt_ids, params)
+        r = self.loop.wait(rid, t if t > 0 else -1.0)
+        self.loop.release(rid)  # done: forgotten; else cancelled, dropped when it ends
+        if r["error"]:
+            self.errors += 1
+            raise RuntimeError(r["error"])
+        if not r["done"]:
+            raise EngineTimeout("engine did not answer within %gs (request cancelled)" % t)
+        return r
+
+    def stall(self, seconds: float):
+        self.loop.stall(float(seconds))
+
+    def close(self):
+        self.loop.shutdown()
+
+    def metrics(self) -> dict:
+        return {k: (int(v) if float(v).is_integer() else v) for k, v in self.loop.metrics().items()}
+
+    def handle_json_stream(self, req_text: str, emit) -> str:
+        """Ollama streaming (NDJSON) on the loop: token batches as they are decoded."""
+        req = json.loads(req_text)
+        params = SamplingParams.from_ollama(req.get("options"), self.default_max_tokens)
+        chat = req.get("endpoint") == "chat"
+        if chat:
+            ids = self.tok.chat_messages_ids(req.get("messages") or [])
+        elif req.get("raw"):
+            ids = self.tok.encode(req.get("prompt", ""), bos=True)
+        else:
+            ids = self.tok.chat_ids(req.get("prompt", ""))
+        rid = self._submit(ids, params)
+        model = req.get("model", self.model_name)
+        t_lim = self.request_timeout_s
+        deadline = time.perf_counter() + t_lim if t_lim > 0 else None
+        toks, text_sent, alive = [], "", True
+
+        def now():
+            return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime()) + ".000000Z"
+
+        def flush(final=False):
+            nonlocal text_sent, alive
+            text = self.tok.decode(toks)
+            if not final and text.endswith("\ufffd"):
+                return
+            delta = text[len(text_sent):] if text.startswith(text_sent) else text
+            text_sent = text
+            if not delta or not alive:
+                return
+            chunk = {"model": model, "created_at": now(), "done": False}
+            if chat:
+                chunk["message"] = {"role": "assistant", "content": delta}
+            else:
+                chunk["response"] = delta
+            alive = bool(emit(json.dumps(chunk)))
+            if not alive:  # client went away: stop generating for it
+                self.loop.cancel(rid)
+
+        try:
+            while True:
+                new, done = self.loop.wait_tokens(rid, len(toks), 0.05)
+                if new:
+                    toks += new
+                    flush()
+                if done:
+                    break
+                if deadline is not None and time.perf_counter() > deadline:
+                    raise EngineTimeout("engine did not answer within %gs (request cancelled)"
+                                        % t_lim)
+            r = self.loop.wait(rid, 0.0)
+        finally:
+            self.loop.release(rid)
+        if r["error"]:
+            raise RuntimeError(r["error"])
+        toks = r["tokens"]
+        flush(final=True)
+        out = {"model": model, "created_at": now(), "done": True,
+               "done_reason": r["done_reason"], "total_duration": r["total_duration"],
+               "load_duration": 0, "prompt_eval_count": r["prompt_eval_count"],
+               "prompt_eval_duration": r["prompt_eval_duration"], "eval_count": r["eval_count"],
+               "eval_duration": r["eval_duration"]}
+        if chat:
+            out["message"] = {"role": "assistant", "content": ""}
+        else:
+            out["response"] = ""
+            out["context"] = []
+        return json.dumps(out)
+
+
+def make_server(engine: Engine, tokenizer=None, **kw) -> EngineServer:
+    """The native-loop server when the engine supports it, else the Python loop."""
+    if native_loop_ok(engine):
+        return NativeEngineServer(engine, tokenizer, **kw)
+    return EngineServer(engine, tokenizer, **kw)

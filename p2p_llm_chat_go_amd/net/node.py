@@ -20,6 +20,9 @@ STRICT_SENDER, UI_FILE) and the engine knobs:
   ENGINE_TP       tensor-parallel ranks per replica (default 1; 8 for 70B over xGMI)
   ENGINE_EP       expert-parallel ranks per replica (MoE models, default 1)
   ENGINE_WEIGHTS  bf16 (default) / fp8 (weight-only e4m3 projections)
+  ENGINE_NATIVE_LOOP  1 (default) / 0: single-GPU replicas run the C++ step loop
+                  (engine.native_loop) instead of the Python one
+  ENGINE_TIMEOUT  per-request deadline in seconds (default 60, the reference UI's bound)
 
 The libp2p host, HTTP API and Directory client are the C++ ``Node``; this
 process only adds the GPU engine behind the node's /api/generate, /api/chat
@@ -47,7 +50,7 @@ def build_engine_server(model: str | None = None, device: str | None = None):
     import torch
 
     from ..engine import Engine
-    from ..engine.server import EngineServer
+    from ..engine.native_loop import make_server
     from ..engine.tokenizer import get_tokenizer
     from ..models.config import get_config
     from ..models.weights import (EngineWeights, config_from_hf, load_safetensors_dir)
@@ -71,8 +74,10 @@ def build_engine_server(model: str | None = None, device: str | None = None):
         # the first request (ENGINE_WARMUP=0 skips: faster start, untuned first replies)
         eng.warmup(tuple(b for b in (1, 2, 4, 8, 16) if b <= max_batch), ctx=256)
     tok = get_tokenizer(cfg, os.environ.get("TOKENIZER_PATH") or (ckpt or None))
-    return EngineServer(eng, tok, model_name=os.environ.get("LLM_MODEL", "llama3.1"),
-                        default_max_tokens=int(os.environ.get("ENGINE_MAX_TOKENS", "128")))
+    # single-GPU replica: the continuous-batching loop runs natively (engine.native_loop);
+    # CPU engines keep the Python loop
+    return make_server(eng, tok, model_name=os.environ.get("LLM_MODEL", "llama3.1"),
+                       default_max_tokens=int(os.environ.get("ENGINE_MAX_TOKENS", "128")))
 
 
 # CLI flags mirror the environment (SURVEY §5 "Config / flag system"): a flag wins

@@ -1,0 +1,154 @@
+"""The native engine step loop (csrc/runtime/engine_loop.cc via engine.native_loop):
+continuous batching from a C++ thread that replays the captured prefill / decode graphs.
+
+Its replies must equal the static-batch engine's (greedy), concurrent requests of
+different lengths exercise riders in prefill chunks, pipelined decode chunks with lagged
+finish detection and deferred page release; sampled requests must reproduce with their
+seed and equal the Python loop's draws; streaming, the request deadline, cancellation and
+the eager long-prompt path are covered too.  (The reference serves one blocking Ollama
+call per click, `web/streamlit_app.py:89-101,163-165`.)"""
+import json
+import threading
+import time
+
+import pytest
+import torch
+
+from p2p_llm_chat_go_amd.engine import Engine
+from p2p_llm_chat_go_amd.engine.sampling import SamplingParams
+from p2p_llm_chat_go_amd.models import TINY_LLAMA
+from p2p_llm_chat_go_amd.models.weights import EngineWeights
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(max_batch=4, layers=3, seed=5):
+    cfg = TINY_LLAMA.replace(n_layers=layers, n_heads=8, n_kv_heads=2)
+    w = EngineWeights.random(cfg, "cuda", seed=seed)
+    return Engine(cfg, weights=w, device="cuda", kv_pages=128, max_batch=max_batch,
+                  max_prefill_tokens=256), w, cfg
+
+
+def _prompts(n):
+    return [[(13 * b + 7 * i) % 250 + 3 for i in range(5 + 11 * b)] for b in range(n)]
+
+
+def test_native_loop_matches_static_greedy():
+    from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
+
+    eng, w, cfg = _engine()
+    prompts = _prompts(6)
+    lens = [9, 17, 4, 23, 12, 30]
+    ref = []
+    for p, n in zip(prompts, lens):  # one request at a time through the static engine
+        ref.append(eng.generate([p], n, stop_on_eos=False)[0].tokens)
+    srv = NativeEngineServer(eng, max_batch=4, decode_chunk=4)
+    try:
+        outs = [None] * len(prompts)
+
+        def run(i):
+            outs[i] = srv.generate(prompts[i], SamplingParams(max_tokens=lens[i],
+                                                              stop_on_eos=False))
+
+        ths = [threading.Thread(target=run, args=(i,)) for i in range(len(prompts))]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        for i, o in enumerate(outs):
+            assert o["done"] and o["tokens"] == ref[i], (i, o["tokens"], ref[i])
+            assert o["eval_count"] == lens[i] and o["prompt_eval_count"] == len(prompts[i])
+        m = srv.metrics()
+        assert m["requests"] == len(prompts) and m["native_loop"] == 1
+        assert m["speculated_chunks"] > 0 and m["decode_calls"] > 0, m
+        for _ in range(100):
+            if srv.metrics()["free_kv_pages"] == 127:
+                break
+            time.sleep(0.02)
+        assert srv.metrics()["free_kv_pages"] == 127  # every page back (null page reserved)
+    finally:
+        srv.close()
+
+
+def test_native_loop_sampled_matches_python_loop():
+    from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
+    from p2p_llm_chat_go_amd.engine.server import EngineServer
+
+    prompts = _prompts(3)
+    params = [SamplingParams(temperature=0.9, top_k=20, top_p=0.9, seed=100 + i, max_tokens=10,
+                             stop_on_eos=False) for i in range(3)]
+    got = {}
+    for kind in ("python", "native"):
+        eng, _w, _cfg = _engine(seed=9)
+        srv = (NativeEngineServer(eng, max_batch=4) if kind == "native"
+               else EngineServer(eng, max_batch=4))
+        try:  # one at a time: identical (prompt, position, seed) keys in both loops
+            got[kind] = [srv.generate(p, params[i])["tokens"] for i, p in enumerate(prompts)]
+            again = srv.generate(prompts[0], params[0])["tokens"]
+            assert again == got[kind][0]
+        finally:
+            srv.close()
+    assert got["native"] == got["python"]
+
+
+def test_native_loop_stream_deadline_cancel_and_eager():
+    from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
+    from p2p_llm_chat_go_amd.engine.server import EngineTimeout
+
+    eng, _w, _cfg = _engine()
+    ref = eng.generate([_prompts(2)[1]], 12, stop_on_eos=False)[0].tokens
+    long_prompt = [(5 * i) % 250 + 3 for i in range(300)]  # > prefill_ctx: the eager path
+    ref_long = eng.generate([long_prompt], 6, stop_on_eos=False)[0].tokens
+    srv = NativeEngineServer(eng, max_batch=4, prefill_ctx=256)
+    try:
+        chunks = []
+        out = json.loads(srv.handle_json_stream(json.dumps(
+            {"raw": False, "prompt": "hello there", "options": {"num_predict": 12,
+                                                                "ignore_eos": True}}),
+            lambda c: chunks.append(json.loads(c)) or True))
+        assert out["done"] and out["eval_count"] == 12 and len(chunks) >= 1
+        r = srv.generate(_prompts(2)[1], SamplingParams(max_tokens=12, stop_on_eos=False))
+        assert r["tokens"] == ref
+        r = srv.generate(long_prompt, SamplingParams(max_tokens=6, stop_on_eos=False))
+        assert r["tokens"] == ref_long and srv.metrics()["eager_prefill_calls"] >= 1
+        # stalled loop: the deadline fires, the request is cancelled and its pages return
+        srv.request_timeout_s = 0.5
+        free0 = srv.metrics()["free_kv_pages"]
+        srv.stall(3.0)
+        t0 = time.perf_counter()
+        with pytest.raises(EngineTimeout):
+            srv.generate(_prompts(1)[0], SamplingParams(max_tokens=50, stop_on_eos=False))
+        assert time.perf_counter() - t0 < 2.5
+        srv.stall(0.0)
+        srv.request_timeout_s = 60
+        r = srv.generate(_prompts(2)[1], SamplingParams(max_tokens=12, stop_on_eos=False))
+        assert r["tokens"] == ref
+        for _ in range(200):
+            m = srv.metrics()
+            if m["free_kv_pages"] == free0 and m["running"] == 0:
+                break
+            time.sleep(0.02)
+        assert m["free_kv_pages"] == free0 and m["running"] == 0, m
+    finally:
+        srv.close()
+
+
+def test_native_loop_8b_width_graphs():
+    """Full-width 8B layers: the loop's prefill + decode graphs equal the static engine."""
+    from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
+    from p2p_llm_chat_go_amd.models import LLAMA31_8B
+
+    cfg = LLAMA31_8B.replace(n_layers=2)
+    w = EngineWeights.random(cfg, "cuda", seed=3)
+    eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_batch=8)
+    prompts = [[(97 * b + 31 * i) % 9000 + 200 for i in range(44 - 7 * b)] for b in range(4)]
+    ref = [eng.generate([p], 16, stop_on_eos=False)[0].tokens for p in prompts]
+    srv = NativeEngineServer(eng, max_batch=8)
+    try:
+        outs = [None] * 4
+        ths = [threading.Thread(target=lambda i=i: outs.__setitem__(i, srv.generate(
+            prompts[i], SamplingParams(max_tokens=16, stop_on_eos=False)))) for i in range(4)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        assert [o["tokens"] for o in outs] == ref
+        torch.cuda.synchronize()
+    finally:
+        srv.close()
