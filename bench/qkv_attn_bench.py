@@ -49,7 +49,24 @@ def run(name, Hq, Hkv, K, M, ctx_len, L=32):
         ops.qkv_attn(wts[i % L], x, pos, slots, cs, Hq, Hkv, kc, vc, bt, ctx, out, ws, err,
                      waves=waves)
 
+    No = Hq * 128 * (4 if Hkv > 1 else 8)  # o_proj output width: 8B 4096, 70B TP=8 rank 8192
+    wos = [torch.randn(No // 16, Hq * 128 // 32, 64, 8, device=dev).mul_(0.02).to(torch.bfloat16)
+           for _ in range(L)]
+    h = torch.zeros(M, No, device=dev, dtype=torch.bfloat16)
+
+    def fused_then_oproj(i):
+        ops.qkv_attn(wts[i % L], x, pos, slots, cs, Hq, Hkv, kc, vc, bt, ctx, out, ws, err)
+        ops.skinny_gemm(wos[i % L], out, ops.EPI_RESID, out=h)
+
+    def fused_oproj(i, waves=None):
+        ops.qkv_attn(wts[i % L], x, pos, slots, cs, Hq, Hkv, kc, vc, bt, ctx, None, ws, err,
+                     waves=waves, oproj=(wos[i % L], h))
+
     res = {}
+    res["qkv_attn+o_proj_2launch"] = graph_time(fused_then_oproj, n_inner=L)
+    for wv in (4, 8):
+        if ops.qkv_attn_oproj_ok(wos[0], Hq, wv):
+            res["qkv_attn_oproj_w%d" % wv] = graph_time(lambda i: fused_oproj(i, wv), n_inner=L)
     for wv in (4, 8):
         res["fused_w%d" % wv] = graph_time(lambda i: fused(i, wv), n_inner=L)
     res["two_kernels"] = graph_time(two, n_inner=L)

@@ -54,6 +54,14 @@ struct QAArgs {
   int* err;
   int n_cons;         // consumer blocks = M * Hkv
   int probe;          // bench probe: 2 = consumers stop after the granule sweep
+  // o_proj role (p2p_qkv_attn_oproj; null Wo = the attention output goes to `out`)
+  const bf16x8* Wo;   // o_proj weight, fragment-major [No / 16][Ko / 32][64][8]
+  bf16* h;            // residual [M][ldh]: h += attention @ Wo^T
+  int ldh, No, Ko;    // Ko = Hq * 128
+  u64* gran2;         // [M][Ko / 2] attention-output granules {epoch, two bf16}
+  unsigned* epoch;    // [2]: launch epoch, o_proj arrival ticket
+  int n_prod;         // producer blocks
+  int n_o;            // o_proj blocks = No / 16
 };
 
 __device__ __forceinline__ unsigned bits16(float x) {
@@ -256,6 +264,8 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
   }
   // 2. the current token's q (G heads), k and v from the producers' granules
   const unsigned tag = a.counters[r * Hkv + h] + 1;
+  const unsigned o_epoch =
+      a.gran2 ? __hip_atomic_load(&a.epoch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 : 0;
   const u64* gb = a.gran + ((size_t)r * Hkv + h) * (G + 2) * 64;
   const int failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long t0 = wall_clock64();
@@ -376,8 +386,7 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
     sl[w][kk] = lg;
   }
   __syncthreads();
-  for (int i = tid; i < G * HD; i += W * 64) {
-    const int hd = i / HD, dd = i % HD;
+  auto merged = [&](int hd, int dd) {
     float M = -INFINITY;
 #pragma unroll
     for (int ww = 0; ww < KW; ++ww) M = fmaxf(M, sm[ww][hd]);
@@ -390,9 +399,117 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
         den = fmaf(e, sl[ww][hd], den);
       }
     }
-    a.out[(size_t)r * a.ldo + (size_t)(h * G + hd) * HD + dd] = f2bf(den > 0.f ? num / den : 0.f);
+    return den > 0.f ? num / den : 0.f;
+  };
+  if (a.gran2 != nullptr) {
+    // o_proj role in this launch: publish the attention output as {epoch, two bf16}
+    // granules (R2: the data is the flag) for the o_proj workgroups to sweep
+    for (int i = tid; i < G * HD / 2; i += W * 64) {
+      const int hd = i / (HD / 2), dd = 2 * (i % (HD / 2));
+      const u64 gr = ((u64)o_epoch << 32) | ((u64)bits16(merged(hd, dd + 1)) << 16) |
+                     bits16(merged(hd, dd));
+      __hip_atomic_store(a.gran2 + (size_t)r * (a.Ko >> 1) + (((h * G + hd) * HD + dd) >> 1), gr,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else {
+    for (int i = tid; i < G * HD; i += W * 64) {
+      const int hd = i / HD, dd = i % HD;
+      a.out[(size_t)r * a.ldo + (size_t)(h * G + hd) * HD + dd] = f2bf(merged(hd, dd));
+    }
   }
   if (tid == 0) a.counters[r * Hkv + h] = tag;  // every granule of this call was consumed
+}
+
+// ---------------------------------------------------------------- o_proj
+// One workgroup per 16 output columns of o_proj (p2p_qkv_attn_oproj).  At kernel start
+// its waves load their k-range of the o_proj weight into registers (nt loads: the stream
+// runs beside the qkv producers' and during the attention phase, when the weight stream
+// would otherwise be idle); then they sweep the attention-output granules of their
+// k-range (the A fragments, rows = batch rows), run the MFMAs, reduce over the waves and
+// add the result to the residual h -- the unfused path's o_proj launch (skinny GEMM,
+// EPI_RESID) without its launch, weight-stream ramp and boundary.  The launch epoch
+// (epoch[0] + 1, read by every consumer and o_proj block at its start) tags the
+// granules; the last o_proj block to finish advances it.
+constexpr int OQ = 32;  // max k-steps per wave held in registers (Ko / 32 / W)
+
+template <int W>
+__device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int S = a.Ko >> 5;
+  const int s0 = (S * w) / W, n = (S * (w + 1)) / W - s0;
+  const bf16x8* wp = a.Wo + ((size_t)g * S + s0) * 64 + lane;
+  bf16x8 wr[OQ];
+#pragma unroll
+  for (int i = 0; i < OQ; ++i)
+    if (i < n) wr[i] = __builtin_nontemporal_load(wp + (size_t)i * 64);
+  const unsigned e = __hip_atomic_load(&a.epoch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const int r = lane & 15, q = lane >> 4;
+  const bool rv = r < a.M;
+  // A fragment of k-step s: row r, dims 32 s + 8 q .. + 7 = granules 16 s + 4 q .. + 3
+  const u64* gp = a.gran2 + (size_t)(rv ? r : 0) * (a.Ko >> 1) + (size_t)s0 * 16 + q * 4;
+  const int failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long t0 = wall_clock64();
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < OQ; ++i) {
+    if (i < n) {
+      bf16x8 af = zero_bf16x8();
+      if (rv) {
+        u64 x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          x[j] = __hip_atomic_load(gp + (size_t)i * 16 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ok &= (unsigned)(x[j] >> 32) == e;
+        while (!ok && !failed) {
+          if (wall_clock64() - t0 > QA_SPIN_TICKS) {
+            atomicOr(a.err, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          ok = true;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if ((unsigned)(x[j] >> 32) != e)
+              x[j] = __hip_atomic_load(gp + (size_t)i * 16 + j, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            ok &= (unsigned)(x[j] >> 32) == e;
+          }
+        }
+        unsigned lo[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lo[j] = (unsigned)x[j];
+        __builtin_memcpy(&af, lo, 16);
+      }
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wr[i], acc, 0, 0, 0);
+    }
+  }
+  float* red = reinterpret_cast<float*>(smem);  // [W - 1][4][64]
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[((w - 1) * 4 + j) * 64 + lane] = acc[j];
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int ww = 0; ww < W - 1; ++ww)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += red[(ww * 4 + j) * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // acc[j]: row 4 q + j, column 16 g + r
+      const int m = 4 * q + j;
+      if (m < a.M) {
+        bf16* hp = a.h + (size_t)m * a.ldh + 16 * g + r;
+        *hp = f2bf((float)*hp + acc[j]);
+      }
+    }
+    if (lane == 0 &&
+        atomicAdd(&a.epoch[1], 1u) == (unsigned)a.n_o - 1) {  // every block swept: next epoch
+      a.epoch[1] = 0;
+      __hip_atomic_store(&a.epoch[0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 template <int G>
@@ -402,25 +519,28 @@ constexpr size_t consumer_lds() {
   return (v > o ? v : o) + sizeof(unsigned) * (G + 2) * 64 + 2 * sizeof(float) * KW * G;
 }
 
-template <int G, int W>
+// FO: the launch also holds the o_proj workgroups (blocks after the producers)
+template <int G, int W, bool FO>
 __global__ __launch_bounds__(W * 64) void qkv_attn_kernel(QAArgs a) {
   constexpr size_t kProd = sizeof(float) * ((W - 1) * 4 * 64 + W * 16);
   constexpr size_t kCons = consumer_lds<G>();
   __shared__ __attribute__((aligned(16))) char smem[kCons > kProd ? kCons : kProd];
   if ((int)blockIdx.x < a.n_cons)
     consumer<G, W>(a, blockIdx.x, smem);
-  else
+  else if (!FO || (int)blockIdx.x < a.n_cons + a.n_prod)
     producer<G, W>(a, blockIdx.x - a.n_cons, smem);
+  else if constexpr (FO)
+    oproj<W>(a, blockIdx.x - a.n_cons - a.n_prod, smem);
 }
 
-template <int W>
+template <int W, bool FO>
 int launch_qa(const QAArgs& a, int G, int groups, hipStream_t stream) {
-  const dim3 grid(a.n_cons + groups), block(W * 64);
+  const dim3 grid(a.n_cons + groups + (FO ? a.n_o : 0)), block(W * 64);
   switch (G) {
-    case 1: hipLaunchKernelGGL((qkv_attn_kernel<1, W>), grid, block, 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((qkv_attn_kernel<2, W>), grid, block, 0, stream, a); break;
-    case 4: hipLaunchKernelGGL((qkv_attn_kernel<4, W>), grid, block, 0, stream, a); break;
-    case 8: hipLaunchKernelGGL((qkv_attn_kernel<8, W>), grid, block, 0, stream, a); break;
+    case 1: hipLaunchKernelGGL((qkv_attn_kernel<1, W, FO>), grid, block, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((qkv_attn_kernel<2, W, FO>), grid, block, 0, stream, a); break;
+    case 4: hipLaunchKernelGGL((qkv_attn_kernel<4, W, FO>), grid, block, 0, stream, a); break;
+    case 8: hipLaunchKernelGGL((qkv_attn_kernel<8, W, FO>), grid, block, 0, stream, a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -440,14 +560,16 @@ P2P_API void p2p_qkv_attn_probe(int mode) { g_qa_probe = mode; }
 // keys (this step's token at position ctx - 1, its slot in slots[r]).  gran: u64
 // [M][Hkv][Hq / Hkv + 2][64], counters: u32 [M][Hkv] (zeroed once, private to this call
 // site's buffers), err: device int (fault word).
-P2P_API int p2p_qkv_attn(const void* Wt, const void* X, int ldx, int M, int K, int Hq, int Hkv,
+static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, int Hq, int Hkv,
                          const int* pos, const int* slots, const void* cos_sin, void* k_cache,
                          void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float scale, void* out, int ldo, float eps,
-                         void* gran, unsigned* counters, int* err, int waves, hipStream_t stream) {
+                         void* gran, unsigned* counters, int* err, int waves, const void* Wo,
+                         int No, void* h, int ldh, void* gran2, unsigned* epoch,
+                         hipStream_t stream) {
   if (M < 1 || M > 16 || K % 32 || Hkv <= 0 || Hq % Hkv || bt_stride * PAGE < 1)
     return (int)hipErrorInvalidValue;
-  QAArgs a;
+  QAArgs a = {};
   a.Wt = (const bf16x8*)Wt;
   a.X = (const bf16*)X;
   a.ldx = ldx;
@@ -473,9 +595,54 @@ P2P_API int p2p_qkv_attn(const void* Wt, const void* X, int ldx, int M, int K, i
   a.n_cons = (g_qa_probe & 1) ? 0 : M * Hkv;  // probe 1: producers only
   a.probe = g_qa_probe;
   const int groups = (Hq + 2 * Hkv) * (HD / 16);
+  a.n_prod = groups;
   // producer waves per block (split-K): 8 when the projection has few column groups (the
   // 70B TP=8 shard: 80), as the skinny kernel's heuristic would pick; else 4
   int W = waves;
   if (W != 4 && W != 8) W = (groups * 8 * 2 <= 4096 && (K / 32) / 8 >= 8) ? 8 : 4;
-  return W == 8 ? launch_qa<8>(a, Hq / Hkv, groups, stream) : launch_qa<4>(a, Hq / Hkv, groups, stream);
+  if (Wo != nullptr) {
+    a.Wo = (const bf16x8*)Wo;
+    a.h = (bf16*)h;
+    a.ldh = ldh;
+    a.No = No;
+    a.Ko = Hq * HD;
+    a.gran2 = (u64*)gran2;
+    a.epoch = epoch;
+    a.n_o = No / 16;
+    // the o_proj weights live in registers: at most OQ k-steps per wave
+    if (No % 16 || No <= 0 || !h || !gran2 || !epoch || (a.Ko / 32 + W - 1) / W > OQ ||
+        (g_qa_probe & 1))
+      return (int)hipErrorInvalidValue;
+    return W == 8 ? launch_qa<8, true>(a, Hq / Hkv, groups, stream)
+                  : launch_qa<4, true>(a, Hq / Hkv, groups, stream);
+  }
+  return W == 8 ? launch_qa<8, false>(a, Hq / Hkv, groups, stream)
+                : launch_qa<4, false>(a, Hq / Hkv, groups, stream);
+}
+
+P2P_API int p2p_qkv_attn(const void* Wt, const void* X, int ldx, int M, int K, int Hq, int Hkv,
+                         const int* pos, const int* slots, const void* cos_sin, void* k_cache,
+                         void* v_cache, const int* block_tables, int bt_stride,
+                         const int* ctx_lens, float scale, void* out, int ldo, float eps,
+                         void* gran, unsigned* counters, int* err, int waves, hipStream_t stream) {
+  return qkv_attn_impl(Wt, X, ldx, M, K, Hq, Hkv, pos, slots, cos_sin, k_cache, v_cache,
+                       block_tables, bt_stride, ctx_lens, scale, out, ldo, eps, gran, counters, err,
+                       waves, nullptr, 0, nullptr, 0, nullptr, nullptr, stream);
+}
+
+// p2p_qkv_attn with the o_proj projection + residual in the same launch (TP = 1 decode):
+// h[M][ldh] += attention @ Wo^T, Wo fragment-major [No / 16][Hq * 128 / 32][64][8] (bf16),
+// Hq * 128 / 32 / waves <= 32.  gran2: u64 [M][Hq * 64], epoch: u32 [2] (zeroed once,
+// private to this call site's buffers).  `out` is not written.
+P2P_API int p2p_qkv_attn_oproj(const void* Wt, const void* X, int ldx, int M, int K, int Hq,
+                               int Hkv, const int* pos, const int* slots, const void* cos_sin,
+                               void* k_cache, void* v_cache, const int* block_tables,
+                               int bt_stride, const int* ctx_lens, float scale, float eps,
+                               void* gran, unsigned* counters, int* err, int waves,
+                               const void* Wo, int No, void* h, int ldh, void* gran2,
+                               unsigned* epoch, hipStream_t stream) {
+  if (!Wo) return (int)hipErrorInvalidValue;
+  return qkv_attn_impl(Wt, X, ldx, M, K, Hq, Hkv, pos, slots, cos_sin, k_cache, v_cache,
+                       block_tables, bt_stride, ctx_lens, scale, nullptr, 0, eps, gran, counters,
+                       err, waves, Wo, No, h, ldh, gran2, epoch, stream);
 }

@@ -103,6 +103,12 @@ class LlamaModel:
         # as ONE launch (ops.qkv_attn): the attention's block-table -> K/V load chain runs
         # behind the qkv weight stream.  P2P_QKV_ATTN=0: the two kernels.
         self.fuse_qkv_attn = os.environ.get("P2P_QKV_ATTN", "1") == "1"
+        # ... and, at TP = 1, the o_proj projection + residual in that same launch (its
+        # workgroups stream their weight slice into registers while the qkv weights and the
+        # attention run, then sweep the attention output as tagged granules): one launch
+        # boundary and one short weight-stream ramp less per layer.  P2P_QKV_ATTN_OPROJ=0:
+        # o_proj stays its own launch
+        self.fuse_qkv_attn_oproj = os.environ.get("P2P_QKV_ATTN_OPROJ", "1") == "1"
         self.heads_max_rows = int(os.environ.get("P2P_HEADS_MAX_ROWS", "4"))
         # TP prefill: row-parallel GEMMs of >= this many rows overlap their all-reduce
         # (chunked, separate communication stream); decode-size sums use the one-shot AR
@@ -198,12 +204,16 @@ class LlamaModel:
         qa = (self.fuse_qkv_attn and not fused and not heads and tiles is None
               and row_bt is None and ws.qa is not None and isinstance(self.w.layers[0].qkv, torch.Tensor)
               and ops.qkv_attn_ok(R, self.nq, self.nkv, max_ctx))
+        qa_o = (qa and self.fuse_qkv_attn_oproj and self.tp == 1
+                and ops.qkv_attn_oproj_ok(self.w.layers[0].o, self.nq))
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)
             if qa:
                 ops.qkv_attn(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, kc, vc,
-                             block_tables, ctx_lens[:R], attn, ws.qa, ws.err, eps=cfg.eps)
-                self._row_parallel(lw.o, attn, h, ws, R)
+                             block_tables, ctx_lens[:R], attn, ws.qa, ws.err, eps=cfg.eps,
+                             oproj=(lw.o, h) if qa_o else None)
+                if not qa_o:
+                    self._row_parallel(lw.o, attn, h, ws, R)
                 self._mlp(lw, ws, R)
                 continue
             ops.qkv_rope_gemm(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, q, kc,

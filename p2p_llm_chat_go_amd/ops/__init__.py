@@ -13,7 +13,7 @@ from .gemm import (EPI_AR, EPI_F32, EPI_RESID, EPI_SILU, EPI_STORE, Fp8Weight, s
 from .attention import (PAGE, HEAD_DIM, attn_oproj, attn_oproj_ok, attn_oproj_heads,
                         attn_oproj_heads_ok, attn_oproj_heads_workspace, attn_workspace,
                         flash_prefill, flash_tile, paged_attention, prefill_tiles, rope_cache,
-                        qkv_attn, qkv_attn_ok, qkv_attn_workspace)
+                        qkv_attn, qkv_attn_ok, qkv_attn_oproj_ok, qkv_attn_workspace)
 from .elementwise import advance, argmax, gather_rows, l3_prefetch
 from .sampling import sample, sample_candidates, topk_candidates
 from ._lib import available as kernels_available, lib as kernel_lib, lib_path as kernel_lib_path
@@ -24,6 +24,6 @@ __all__ = [
     "rope_row_perm", "PAGE", "HEAD_DIM", "attn_workspace", "paged_attention", "flash_prefill", "flash_tile", "prefill_tiles",
     "attn_oproj", "attn_oproj_ok", "attn_oproj_heads", "attn_oproj_heads_ok",
     "attn_oproj_heads_workspace", "tiled_split_fault", "tiled_split_parallel", "l3_prefetch",
-    "rope_cache", "qkv_attn", "qkv_attn_ok", "qkv_attn_workspace", "sample", "sample_candidates", "topk_candidates", "advance", "argmax", "gather_rows", "kernels_available", "kernel_lib",
+    "rope_cache", "qkv_attn", "qkv_attn_ok", "qkv_attn_oproj_ok", "qkv_attn_workspace", "sample", "sample_candidates", "topk_candidates", "advance", "argmax", "gather_rows", "kernels_available", "kernel_lib",
     "kernel_lib_path",
 ]

@@ -96,22 +96,42 @@ def qkv_attn_ok(R: int, n_heads: int, n_kv: int, max_ctx: int) -> bool:
 
 
 def qkv_attn_workspace(rows: int, n_heads: int, n_kv: int, device) -> tuple:
-    """(granules u64 [rows][n_kv][G + 2][64], tag counters u32 [rows][n_kv]), zeroed."""
+    """(granules u64 [rows][n_kv][G + 2][64], tag counters u32 [rows][n_kv],
+    attention-output granules u64 [rows][n_heads * 64] + launch epoch u32 [2] for the
+    fused o_proj role), zeroed."""
     G = n_heads // n_kv
     gran = torch.zeros(rows * n_kv * (G + 2) * 64, dtype=torch.int64, device=device)
     cnt = torch.zeros(rows * n_kv, dtype=torch.int32, device=device)
-    return gran, cnt
+    gran2 = torch.zeros(rows * n_heads * 64, dtype=torch.int64, device=device)
+    epoch = torch.zeros(2, dtype=torch.int32, device=device)
+    return gran, cnt, gran2, epoch
+
+
+# o_proj in the qkv+attention launch: the weights of a wave's k-range sit in registers
+QKV_ATTN_OPROJ_MAX_KSTEPS = 32
+
+
+def qkv_attn_oproj_ok(wo, n_heads: int, waves: int = 4) -> bool:
+    """Can ops.qkv_attn run this o_proj (bf16, fragment-major) in its own launch?"""
+    if not isinstance(wo, torch.Tensor) or wo.dtype != torch.bfloat16:
+        return False
+    K = n_heads * HEAD_DIM
+    return wo.shape[1] * 32 == K and -(-(K // 32) // waves) <= QKV_ATTN_OPROJ_MAX_KSTEPS
 
 
 QKV_ATTN_WAVES = int(os.environ.get("P2P_QA_WAVES", "0"))  # 0: heuristic (4 or 8)
 
 
 def qkv_attn(wt, x, pos, slots, cos_sin, n_heads, n_kv, k_cache, v_cache, block_tables,
-             ctx_lens, out, workspace, err, eps=1e-5, scale=None, waves=None):
+             ctx_lens, out, workspace, err, eps=1e-5, scale=None, waves=None, oproj=None):
     """Decode step's qkv projection (RMSNorm folded, rope_row_perm rows) + RoPE + paged-KV
     write + attention in one launch (csrc/kernels/qkv_attn.hip): out[r] = attention of
     row r's q over its ctx_lens[r] keys (this step's token last), block-table row r.
-    Same numbers as qkv_rope_gemm followed by paged_attention (up to summation order)."""
+    Same numbers as qkv_rope_gemm followed by paged_attention (up to summation order).
+
+    oproj=(wo, h): the o_proj projection runs in the same launch (its workgroups hold their
+    weight slice in registers from the start and sweep the attention output as tagged
+    granules): h += attention @ wo^T, and ``out`` is not written."""
     from .gemm import tiled_shape
 
     R = x.shape[0]
@@ -119,9 +139,24 @@ def qkv_attn(wt, x, pos, slots, cos_sin, n_heads, n_kv, k_cache, v_cache, block_
     assert N == (n_heads + 2 * n_kv) * HEAD_DIM and x.stride(1) == 1
     if scale is None:
         scale = 1.0 / math.sqrt(HEAD_DIM)
-    gran, cnt = workspace
+    gran, cnt = workspace[0], workspace[1]
     assert gran.numel() >= R * n_kv * (n_heads // n_kv + 2) * 64 and cnt.numel() >= R * n_kv
     L = _lib.lib()
+    if oproj is not None:
+        wo, h = oproj
+        No, Ko = tiled_shape(wo)
+        gran2, epoch = workspace[2], workspace[3]
+        assert Ko == n_heads * HEAD_DIM and h.shape[1] == No and h.stride(1) == 1
+        assert gran2.numel() >= R * n_heads * 64 and h.shape[0] >= R
+        _lib.check(L.p2p_qkv_attn_oproj(
+            wt.data_ptr(), x.data_ptr(), x.stride(0), R, K, n_heads, n_kv, pos.data_ptr(),
+            slots.data_ptr(), cos_sin.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+            block_tables.data_ptr(), block_tables.stride(0), ctx_lens.data_ptr(), float(scale),
+            float(eps), gran.data_ptr(), cnt.data_ptr(), err.data_ptr(),
+            QKV_ATTN_WAVES if waves is None else int(waves), wo.data_ptr(), No, h.data_ptr(),
+            h.stride(0), gran2.data_ptr(), epoch.data_ptr(), _lib.stream_ptr(x.device)),
+            "qkv_attn_oproj")
+        return h
     _lib.check(L.p2p_qkv_attn(
         wt.data_ptr(), x.data_ptr(), x.stride(0), R, K, n_heads, n_kv, pos.data_ptr(),
         slots.data_ptr(), cos_sin.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),

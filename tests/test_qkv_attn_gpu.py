@@ -107,3 +107,65 @@ def test_qkv_attn_graph_replay():
         assert int(err.item()) == 0
         rel = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
         assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("M,Hq,Hkv,K,No", [(1, 32, 8, 4096, 4096), (3, 32, 8, 1024, 512),
+                                           (16, 32, 8, 1024, 256), (1, 8, 1, 8192, 8192),
+                                           (5, 8, 2, 1024, 1024), (2, 4, 4, 512, 256)])
+def test_qkv_attn_oproj_matches_unfused(M, Hq, Hkv, K, No):
+    """o_proj (+ residual) inside the qkv+attention launch == qkv_attn followed by the
+    o_proj GEMM (skinny, EPI_RESID), and == the fp32 reference of attention @ Wo^T + h;
+    repeated calls and graph replays advance the granule epoch on the same buffers."""
+    d = _setup(M, Hq, Hkv, K, seed=M * 31 + Hq + No)
+    g = torch.Generator().manual_seed(M + No)
+    wo32 = torch.randn(No, Hq * 128, generator=g) * 0.03
+    wo = ops.tile_weight(wo32.to(torch.bfloat16)).to(DEV)
+    h0 = torch.randn(M, No, generator=g).to(torch.bfloat16).to(DEV)
+    ws = ops.qkv_attn_workspace(M, Hq, Hkv, DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    # unfused reference on the same kernels
+    kc1, vc1 = d["kc"].clone(), d["vc"].clone()
+    attn = torch.zeros(M, Hq * 128, dtype=torch.bfloat16, device=DEV)
+    ops.qkv_attn(d["wt"], d["x"], d["pos"], d["slots"], d["cs"], Hq, Hkv, kc1, vc1, d["bt"],
+                 d["ctx"], attn, ws, err)
+    h_ref = h0.clone()
+    ops.skinny_gemm(wo, attn, ops.EPI_RESID, out=h_ref)
+    ref32 = h0.float().cpu() + attn.float().cpu() @ wo32.to(torch.bfloat16).float().t()
+    torch.cuda.synchronize()
+    for rep in range(3):
+        kc2, vc2 = d["kc"].clone(), d["vc"].clone()
+        h = h0.clone()
+        ops.qkv_attn(d["wt"], d["x"], d["pos"], d["slots"], d["cs"], Hq, Hkv, kc2, vc2, d["bt"],
+                     d["ctx"], None, ws, err, oproj=(wo, h))
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0, "granule sweep timed out"
+        for a_, b_ in ((kc2, kc1), (vc2, vc1)):
+            assert int((a_ != b_).sum()) <= 8
+        rel = ((h.float() - h_ref.float()).abs().max() / h_ref.float().abs().max()).item()
+        assert rel < 1e-2, (rep, rel)
+        rel32 = ((h.float().cpu() - ref32).abs().max() / ref32.abs().max()).item()
+        assert rel32 < 2e-2, (rep, rel32)
+    # graph capture + replays (the epoch advances inside the graph)
+    hg = h0.clone()
+    kc3, vc3 = d["kc"].clone(), d["vc"].clone()
+
+    def body():
+        hg.copy_(h0)
+        ops.qkv_attn(d["wt"], d["x"], d["pos"], d["slots"], d["cs"], Hq, Hkv, kc3, vc3, d["bt"],
+                     d["ctx"], None, ws, err, oproj=(wo, hg))
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            body()
+            body()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        gr.replay()
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        rel = ((hg.float() - h_ref.float()).abs().max() / h_ref.float().abs().max()).item()
+        assert rel < 1e-2, rel
