@@ -18,7 +18,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from kernel_bench import graph_time  # noqa: E402
 
 
-def run(name, Hq, Hkv, K, M, ctx_len, L=32):
+def run(name, Hq, Hkv, K, M, ctx_len, L=32, hidden=None):
+    hidden = hidden or K
     dev = "cuda"
     N = (Hq + 2 * Hkv) * 128
     wts = [torch.randn(N // 16, K // 32, 64, 8, device=dev).mul_(0.02).to(torch.bfloat16)
@@ -49,23 +50,29 @@ def run(name, Hq, Hkv, K, M, ctx_len, L=32):
         ops.qkv_attn(wts[i % L], x, pos, slots, cs, Hq, Hkv, kc, vc, bt, ctx, out, ws, err,
                      waves=waves)
 
-    No = Hq * 128 * (4 if Hkv > 1 else 8)  # o_proj output width: 8B 4096, 70B TP=8 rank 8192
+    No = hidden  # o_proj output width: the model's hidden size
     wos = [torch.randn(No // 16, Hq * 128 // 32, 64, 8, device=dev).mul_(0.02).to(torch.bfloat16)
            for _ in range(L)]
     h = torch.zeros(M, No, device=dev, dtype=torch.bfloat16)
 
+    # the unfused o_proj at its best skinny launch code (what the engine's autotuner picks)
+    best_o = min(((graph_time(lambda i, c=c: ops.skinny_gemm(wos[i % L], out, ops.EPI_RESID,
+                                                               out=h, waves=c), n_inner=L), c)
+                  for c in [w | (u << 8) for w in (1, 2, 4, 8) for u in (4, 8)]))
+    res_o = {"o_proj_alone": best_o[0]}
+
     def fused_then_oproj(i):
         ops.qkv_attn(wts[i % L], x, pos, slots, cs, Hq, Hkv, kc, vc, bt, ctx, out, ws, err)
-        ops.skinny_gemm(wos[i % L], out, ops.EPI_RESID, out=h)
+        ops.skinny_gemm(wos[i % L], out, ops.EPI_RESID, out=h, waves=best_o[1])
 
     def fused_oproj(i, waves=None):
         ops.qkv_attn(wts[i % L], x, pos, slots, cs, Hq, Hkv, kc, vc, bt, ctx, None, ws, err,
                      waves=waves, oproj=(wos[i % L], h))
 
-    res = {}
+    res = dict(res_o)
     res["qkv_attn+o_proj_2launch"] = graph_time(fused_then_oproj, n_inner=L)
     for wv in (4, 8):
-        if ops.qkv_attn_oproj_ok(wos[0], Hq, wv):
+        if ops.qkv_attn_oproj_ok(wos[0], Hq, Hkv, wv):
             res["qkv_attn_oproj_w%d" % wv] = graph_time(lambda i: fused_oproj(i, wv), n_inner=L)
     for wv in (4, 8):
         res["fused_w%d" % wv] = graph_time(lambda i: fused(i, wv), n_inner=L)

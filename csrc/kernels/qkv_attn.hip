@@ -153,7 +153,7 @@ __device__ __forceinline__ void producer(const QAArgs& a, int g, char* smem) {
   }
   if (q == 0) red_ss[w * 16 + r] = ss;
   __syncthreads();
-  if (w != 0) return;
+  if (w != 0) return;  // (every wave returns together to the o_proj phase, if any)
 #pragma unroll
   for (int ww = 0; ww < W - 1; ++ww)
 #pragma unroll
@@ -421,19 +421,24 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
 }
 
 // ---------------------------------------------------------------- o_proj
-// One workgroup per 16 output columns of o_proj (p2p_qkv_attn_oproj).  At kernel start
-// its waves load their k-range of the o_proj weight into registers (nt loads: the stream
-// runs beside the qkv producers' and during the attention phase, when the weight stream
-// would otherwise be idle); then they sweep the attention-output granules of their
-// k-range (the A fragments, rows = batch rows), run the MFMAs, reduce over the waves and
-// add the result to the residual h -- the unfused path's o_proj launch (skinny GEMM,
-// EPI_RESID) without its launch, weight-stream ramp and boundary.  The launch epoch
-// (epoch[0] + 1, read by every consumer and o_proj block at its start) tags the
-// granules; the last o_proj block to finish advances it.
-constexpr int OQ = 32;  // max k-steps per wave held in registers (Ko / 32 / W)
+// 16 output columns of o_proj per workgroup (p2p_qkv_attn_oproj): producer workgroup
+// g < No / 16 continues with column group g once its qkv slice is published.  Its waves
+// load their k-range of the o_proj weight into the registers the qkv stream just freed (nt
+// loads: this stream runs while the attention does, when the weight stream would
+// otherwise idle).  Then the whole workgroup sweeps the attention-output granules of
+// up to OROWS batch rows into LDS -- every thread's loads issued at once, one round trip
+// once the consumers have published -- and each wave runs its k-range of MFMAs from LDS,
+// the waves' partial tiles are summed and added to the residual h: the unfused path's
+// o_proj launch (skinny GEMM, EPI_RESID) without its launch, weight-stream ramp and
+// boundary.  The launch epoch (epoch[0] + 1, read by every consumer and o_proj block at its
+// start) tags the granules; the last o_proj block to finish advances it.
+constexpr int OQ = 32;     // max k-steps per wave held in registers (Ko / 32 / W)
+constexpr int OROWS = 8;   // batch rows staged in LDS per sweep pass
+constexpr int OGPT = 8;    // granules in flight per thread per sweep round
 
 template <int W>
-__device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem) {
+__device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem, size_t smem_bytes) {
+  constexpr int NT = W * 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int S = a.Ko >> 5;
   const int s0 = (S * w) / W, n = (S * (w + 1)) / W - s0;
@@ -443,48 +448,64 @@ __device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem) {
   for (int i = 0; i < OQ; ++i)
     if (i < n) wr[i] = __builtin_nontemporal_load(wp + (size_t)i * 64);
   const unsigned e = __hip_atomic_load(&a.epoch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  const int r = lane & 15, q = lane >> 4;
-  const bool rv = r < a.M;
-  // A fragment of k-step s: row r, dims 32 s + 8 q .. + 7 = granules 16 s + 4 q .. + 3
-  const u64* gp = a.gran2 + (size_t)(rv ? r : 0) * (a.Ko >> 1) + (size_t)s0 * 16 + q * 4;
   const int failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int r = lane & 15, q = lane >> 4;
+  const int KG = a.Ko >> 1;        // granules per row
+  const int LDR = a.Ko + 8;        // LDS row stride (bf16): 16 B pad, rows on distinct banks
+  unsigned* st = reinterpret_cast<unsigned*>(smem);  // [OROWS][LDR / 2] bf16 pairs
   const long long t0 = wall_clock64();
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int m0 = 0; m0 < a.M; m0 += OROWS) {
+    const int mb = min(OROWS, a.M - m0);
+    const int total = mb * KG;
+    __syncthreads();  // the previous pass's LDS reads are done
+    for (int base = 0; base < total; base += NT * OGPT) {
+      u64 x[OGPT];
 #pragma unroll
-  for (int i = 0; i < OQ; ++i) {
-    if (i < n) {
-      bf16x8 af = zero_bf16x8();
-      if (rv) {
-        u64 x[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          x[j] = __hip_atomic_load(gp + (size_t)i * 16 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ok &= (unsigned)(x[j] >> 32) == e;
-        while (!ok && !failed) {
-          if (wall_clock64() - t0 > QA_SPIN_TICKS) {
-            atomicOr(a.err, 1);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          ok = true;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if ((unsigned)(x[j] >> 32) != e)
-              x[j] = __hip_atomic_load(gp + (size_t)i * 16 + j, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            ok &= (unsigned)(x[j] >> 32) == e;
-          }
-        }
-        unsigned lo[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) lo[j] = (unsigned)x[j];
-        __builtin_memcpy(&af, lo, 16);
+      for (int j = 0; j < OGPT; ++j) {  // independent loads: one round trip
+        const int i = base + j * NT + (int)threadIdx.x;
+        x[j] = i < total ? __hip_atomic_load(a.gran2 + (size_t)m0 * KG + i, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+                         : ((u64)e << 32);
       }
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wr[i], acc, 0, 0, 0);
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < OGPT; ++j) ok &= (unsigned)(x[j] >> 32) == e;
+      while (!ok && !failed) {  // the consumers have not published yet: re-poll the missing
+        if (wall_clock64() - t0 > QA_SPIN_TICKS) {
+          atomicOr(a.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        ok = true;
+#pragma unroll
+        for (int j = 0; j < OGPT; ++j) {
+          const int i = base + j * NT + (int)threadIdx.x;
+          if ((unsigned)(x[j] >> 32) != e && i < total)
+            x[j] = __hip_atomic_load(a.gran2 + (size_t)m0 * KG + i, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+          ok &= (unsigned)(x[j] >> 32) == e;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < OGPT; ++j) {
+        const int i = base + j * NT + (int)threadIdx.x;
+        if (i < total) st[(i / KG) * (LDR >> 1) + i % KG] = (unsigned)x[j];
+      }
+    }
+    __syncthreads();
+    // this wave's k-range: A fragment of k-step s = row r, dims 32 s + 8 q .. + 7
+    const bool rv = r >= m0 && r < m0 + mb;
+    const bf16* arow = reinterpret_cast<const bf16*>(st) + (size_t)(rv ? r - m0 : 0) * LDR + 8 * q;
+#pragma unroll
+    for (int i = 0; i < OQ; ++i) {
+      if (i < n) {
+        const bf16x8 af = rv ? *reinterpret_cast<const bf16x8*>(arow + 32 * (s0 + i)) : zero_bf16x8();
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wr[i], acc, 0, 0, 0);
+      }
     }
   }
+  __syncthreads();  // the staging area becomes the reduction buffer
   float* red = reinterpret_cast<float*>(smem);  // [W - 1][4][64]
   if (w > 0) {
 #pragma unroll
@@ -510,6 +531,7 @@ __device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem) {
       __hip_atomic_store(&a.epoch[0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  (void)smem_bytes;
 }
 
 template <int G>
@@ -520,22 +542,37 @@ constexpr size_t consumer_lds() {
 }
 
 // FO: the launch also holds the o_proj workgroups (blocks after the producers)
+size_t consumer_lds_for(int G) {
+  switch (G) {
+    case 1: return consumer_lds<1>();
+    case 2: return consumer_lds<2>();
+    case 4: return consumer_lds<4>();
+    case 8: return consumer_lds<8>();
+  }
+  return 0;
+}
+
 template <int G, int W, bool FO>
 __global__ __launch_bounds__(W * 64) void qkv_attn_kernel(QAArgs a) {
   constexpr size_t kProd = sizeof(float) * ((W - 1) * 4 * 64 + W * 16);
   constexpr size_t kCons = consumer_lds<G>();
   __shared__ __attribute__((aligned(16))) char smem[kCons > kProd ? kCons : kProd];
-  if ((int)blockIdx.x < a.n_cons)
+  if ((int)blockIdx.x < a.n_cons) {
     consumer<G, W>(a, blockIdx.x, smem);
-  else if (!FO || (int)blockIdx.x < a.n_cons + a.n_prod)
-    producer<G, W>(a, blockIdx.x - a.n_cons, smem);
-  else if constexpr (FO)
-    oproj<W>(a, blockIdx.x - a.n_cons - a.n_prod, smem);
+  } else {
+    const int pg = blockIdx.x - a.n_cons;
+    producer<G, W>(a, pg, smem);
+    // FO: the first n_o producers go on to an o_proj column group, their registers free
+    // once the qkv stream is done (no extra workgroups competing for residency)
+    if constexpr (FO) {
+      if (pg < a.n_o) oproj<W>(a, pg, smem, sizeof(smem));
+    }
+  }
 }
 
 template <int W, bool FO>
 int launch_qa(const QAArgs& a, int G, int groups, hipStream_t stream) {
-  const dim3 grid(a.n_cons + groups + (FO ? a.n_o : 0)), block(W * 64);
+  const dim3 grid(a.n_cons + groups), block(W * 64);
   switch (G) {
     case 1: hipLaunchKernelGGL((qkv_attn_kernel<1, W, FO>), grid, block, 0, stream, a); break;
     case 2: hipLaunchKernelGGL((qkv_attn_kernel<2, W, FO>), grid, block, 0, stream, a); break;
@@ -610,8 +647,10 @@ static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, i
     a.epoch = epoch;
     a.n_o = No / 16;
     // the o_proj weights live in registers: at most OQ k-steps per wave
+    const size_t stage = (size_t)OROWS * (a.Ko + 8) * sizeof(bf16);
+    const size_t lds = consumer_lds_for(Hq / Hkv);
     if (No % 16 || No <= 0 || !h || !gran2 || !epoch || (a.Ko / 32 + W - 1) / W > OQ ||
-        (g_qa_probe & 1))
+        stage > lds || a.n_o > groups || (g_qa_probe & 1))
       return (int)hipErrorInvalidValue;
     return W == 8 ? launch_qa<8, true>(a, Hq / Hkv, groups, stream)
                   : launch_qa<4, true>(a, Hq / Hkv, groups, stream);

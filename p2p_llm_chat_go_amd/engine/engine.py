@@ -85,8 +85,8 @@ class Engine:
             self.kv = KVCache(cfg, kv_pages, self.device, tp_size)
         if comm is not None and hasattr(comm, "setup"):
             comm.setup(self.device)
-            if (cfg.is_moe and ep_size > 1 and ep_mode == "a2a" and self.device.type == "cuda"
-                    and hasattr(comm, "setup_ep_ipc")):
+            if (cfg.is_moe and max(ep_size, weights.ep_size) > 1 and ep_mode == "a2a"
+                    and self.device.type == "cuda" and hasattr(comm, "setup_ep_ipc")):
                 # decode-size expert exchanges on the IPC kernels: up to the largest decode
                 # bucket's rows x top_k slots per call (larger calls: RCCL exact counts)
                 comm.setup_ep_ipc(cfg.top_k * bucket(max(1, min(max_batch, BATCH_BUCKETS[-1])),

@@ -151,18 +151,25 @@ class DecodeGraph:
         st.reset_dummy()
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g):
+            # thread_local: HIP calls other threads make meanwhile (a serving loop's host
+            # copies, a collective's helper threads) are not this capture's business
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._body()
         except Exception as e:  # e.g. a collective backend that cannot be captured
             import os
+            import traceback
             import warnings
 
-            if st.model.tp > 1 and os.environ.get("P2P_ALLOW_EAGER", "0") != "1":
-                # a TP group must not silently lose its graphs (eager TP decode is several
-                # times slower); P2P_ALLOW_EAGER=1 accepts it
-                raise RuntimeError("TP decode graph capture failed: %s (set P2P_ALLOW_EAGER=1 to "
-                                   "run the step eagerly)" % e) from e
-            warnings.warn("decode graph capture failed (%s); running the step eagerly" % e)
+            comm = st.model.comm
+            if (getattr(comm, "world", 1) > 1 and st.model.device.type == "cuda"
+                    and os.environ.get("P2P_ALLOW_EAGER", "0") != "1"):
+                # a TP / EP group must not silently lose its graphs (eager group decode is
+                # several times slower); P2P_ALLOW_EAGER=1 accepts it
+                raise RuntimeError("group decode graph capture failed: %s (set "
+                                   "P2P_ALLOW_EAGER=1 to run the step eagerly)\n%s"
+                                   % (e, traceback.format_exc())) from e
+            warnings.warn("decode graph capture failed (%s); running the step eagerly\n%s"
+                          % (e, traceback.format_exc()))
             torch.cuda.synchronize(st.model.device)
             st.reset_dummy()
             self.graph = None
@@ -332,7 +339,7 @@ class PrefillGraph:
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.body()
         torch.cuda.synchronize(dev)
         self.graph = g

@@ -205,7 +205,7 @@ class LlamaModel:
               and row_bt is None and ws.qa is not None and isinstance(self.w.layers[0].qkv, torch.Tensor)
               and ops.qkv_attn_ok(R, self.nq, self.nkv, max_ctx))
         qa_o = (qa and self.fuse_qkv_attn_oproj and self.tp == 1
-                and ops.qkv_attn_oproj_ok(self.w.layers[0].o, self.nq))
+                and ops.qkv_attn_oproj_ok(self.w.layers[0].o, self.nq, self.nkv))
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)
             if qa:

@@ -111,12 +111,15 @@ def qkv_attn_workspace(rows: int, n_heads: int, n_kv: int, device) -> tuple:
 QKV_ATTN_OPROJ_MAX_KSTEPS = 32
 
 
-def qkv_attn_oproj_ok(wo, n_heads: int, waves: int = 4) -> bool:
-    """Can ops.qkv_attn run this o_proj (bf16, fragment-major) in its own launch?"""
+def qkv_attn_oproj_ok(wo, n_heads: int, n_kv: int, waves: int = 4) -> bool:
+    """Can ops.qkv_attn run this o_proj (bf16, fragment-major) in its own launch?  Each
+    16-column group of o_proj is taken by one of the (n_heads + 2 n_kv) * 8 producer
+    workgroups after its qkv slice, so o_proj may not have more groups than that."""
     if not isinstance(wo, torch.Tensor) or wo.dtype != torch.bfloat16:
         return False
     K = n_heads * HEAD_DIM
-    return wo.shape[1] * 32 == K and -(-(K // 32) // waves) <= QKV_ATTN_OPROJ_MAX_KSTEPS
+    return (wo.shape[1] * 32 == K and -(-(K // 32) // waves) <= QKV_ATTN_OPROJ_MAX_KSTEPS
+            and wo.shape[0] <= (n_heads + 2 * n_kv) * (HEAD_DIM // 16))
 
 
 QKV_ATTN_WAVES = int(os.environ.get("P2P_QA_WAVES", "0"))  # 0: heuristic (4 or 8)

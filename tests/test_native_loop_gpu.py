@@ -121,12 +121,13 @@ def test_native_loop_stream_deadline_cancel_and_eager():
         srv.request_timeout_s = 60
         r = srv.generate(_prompts(2)[1], SamplingParams(max_tokens=12, stop_on_eos=False))
         assert r["tokens"] == ref
-        for _ in range(200):
-            m = srv.metrics()
-            if m["free_kv_pages"] == free0 and m["running"] == 0:
+        for _ in range(200):  # every page back (pages of finished requests are released
+            m = srv.metrics()  # once no decode chunk is in flight; the null page stays)
+            if m["free_kv_pages"] == 127 and m["running"] == 0:
                 break
             time.sleep(0.02)
-        assert m["free_kv_pages"] == free0 and m["running"] == 0, m
+        assert m["free_kv_pages"] == 127 and m["running"] == 0, m
+        assert free0 <= 127
     finally:
         srv.close()
 

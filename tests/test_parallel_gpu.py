@@ -110,6 +110,8 @@ def test_virtual_rank_parallel_gpu(moe, a2a, overlap, graphs, ipc):
     res = [q.get(timeout=600) for _ in range(world)]
     [p.join(timeout=60) for p in ps]
     for rank, ok, got, ref in res:
+        if not ok and isinstance(got, str):
+            print("rank %d failed:\n%s" % (rank, got))  # the whole traceback
         assert ok, (rank, got, ref)
 
 

@@ -110,7 +110,7 @@ def test_qkv_attn_graph_replay():
 
 
 @pytest.mark.parametrize("M,Hq,Hkv,K,No", [(1, 32, 8, 4096, 4096), (3, 32, 8, 1024, 512),
-                                           (16, 32, 8, 1024, 256), (1, 8, 1, 8192, 8192),
+                                           (16, 32, 8, 1024, 256), (9, 32, 8, 4096, 4096),
                                            (5, 8, 2, 1024, 1024), (2, 4, 4, 512, 256)])
 def test_qkv_attn_oproj_matches_unfused(M, Hq, Hkv, K, No):
     """o_proj (+ residual) inside the qkv+attention launch == qkv_attn followed by the
@@ -120,6 +120,9 @@ def test_qkv_attn_oproj_matches_unfused(M, Hq, Hkv, K, No):
     g = torch.Generator().manual_seed(M + No)
     wo32 = torch.randn(No, Hq * 128, generator=g) * 0.03
     wo = ops.tile_weight(wo32.to(torch.bfloat16)).to(DEV)
+    assert ops.qkv_attn_oproj_ok(wo, Hq, Hkv)
+    # a 70B TP=8 rank's o_proj (512 column groups) has more groups than producers (80)
+    assert not ops.qkv_attn_oproj_ok(torch.empty(512, 32, 64, 8, dtype=torch.bfloat16), 8, 1)
     h0 = torch.randn(M, No, generator=g).to(torch.bfloat16).to(DEV)
     ws = ops.qkv_attn_workspace(M, Hq, Hkv, DEV)
     err = torch.zeros(1, dtype=torch.int32, device=DEV)
