@@ -72,7 +72,7 @@ def run(name, Hq, Hkv, K, M, ctx_len, L=32, hidden=None):
     res = dict(res_o)
     res["qkv_attn+o_proj_2launch"] = graph_time(fused_then_oproj, n_inner=L)
     for wv in (4, 8):
-        if ops.qkv_attn_oproj_ok(wos[0], Hq, Hkv, wv):
+        if ops.qkv_attn_oproj_ok(wos[0], Hq, Hkv, wv, rows=M, hidden=K):
             res["qkv_attn_oproj_w%d" % wv] = graph_time(lambda i: fused_oproj(i, wv), n_inner=L)
     for wv in (4, 8):
         res["fused_w%d" % wv] = graph_time(lambda i: fused(i, wv), n_inner=L)

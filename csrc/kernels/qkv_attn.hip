@@ -437,16 +437,22 @@ constexpr int OROWS = 8;   // batch rows staged in LDS per sweep pass
 constexpr int OGPT = 8;    // granules in flight per thread per sweep round
 
 template <int W>
-__device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem, size_t smem_bytes) {
-  constexpr int NT = W * 64;
+__device__ __forceinline__ void oproj_load(const QAArgs& a, int g, bf16x8 (&wr)[OQ]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int S = a.Ko >> 5;
   const int s0 = (S * w) / W, n = (S * (w + 1)) / W - s0;
   const bf16x8* wp = a.Wo + ((size_t)g * S + s0) * 64 + lane;
-  bf16x8 wr[OQ];
 #pragma unroll
   for (int i = 0; i < OQ; ++i)
     if (i < n) wr[i] = __builtin_nontemporal_load(wp + (size_t)i * 64);
+}
+
+template <int W>
+__device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem, const bf16x8 (&wr)[OQ]) {
+  constexpr int NT = W * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int S = a.Ko >> 5;
+  const int s0 = (S * w) / W, n = (S * (w + 1)) / W - s0;
   const unsigned e = __hip_atomic_load(&a.epoch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   const int failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int r = lane & 15, q = lane >> 4;
@@ -531,7 +537,6 @@ __device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem, size_t
       __hip_atomic_store(&a.epoch[0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  (void)smem_bytes;
 }
 
 template <int G>
@@ -563,9 +568,15 @@ __global__ __launch_bounds__(W * 64) void qkv_attn_kernel(QAArgs a) {
     const int pg = blockIdx.x - a.n_cons;
     producer<G, W>(a, pg, smem);
     // FO: the first n_o producers go on to an o_proj column group, their registers free
-    // once the qkv stream is done (no extra workgroups competing for residency)
+    // once the qkv stream is done (no extra workgroups competing for residency).  Loading
+    // the o_proj slice before the qkv stream instead needs ~250 VGPRs + spills: one wave
+    // per SIMD, and the grid no longer fits the device at once
     if constexpr (FO) {
-      if (pg < a.n_o) oproj<W>(a, pg, smem, sizeof(smem));
+      if (pg < a.n_o) {
+        bf16x8 wr[OQ];
+        oproj_load<W>(a, pg, wr);
+        oproj<W>(a, pg, smem, wr);
+      }
     }
   }
 }
@@ -597,6 +608,30 @@ P2P_API void p2p_qkv_attn_probe(int mode) { g_qa_probe = mode; }
 // keys (this step's token at position ctx - 1, its slot in slots[r]).  gran: u64
 // [M][Hkv][Hq / Hkv + 2][64], counters: u32 [M][Hkv] (zeroed once, private to this call
 // site's buffers), err: device int (fault word).
+// workgroups of the fused-o_proj kernel the device holds at once (occupancy x CUs)
+static int oproj_capacity(int W, int G) {
+  static int cache[2][9] = {};
+  int& c = cache[W == 8][G];
+  if (c) return c;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const void* k = nullptr;
+#define P2P_QA_K(WW, GG) (const void*)qkv_attn_kernel<GG, WW, true>
+  switch (G) {
+    case 1: k = W == 8 ? P2P_QA_K(8, 1) : P2P_QA_K(4, 1); break;
+    case 2: k = W == 8 ? P2P_QA_K(8, 2) : P2P_QA_K(4, 2); break;
+    case 4: k = W == 8 ? P2P_QA_K(8, 4) : P2P_QA_K(4, 4); break;
+    case 8: k = W == 8 ? P2P_QA_K(8, 8) : P2P_QA_K(4, 8); break;
+    default: return 0;
+  }
+#undef P2P_QA_K
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, W * 64, 0) != hipSuccess) return 0;
+  c = per * cus;
+  return c;
+}
+
 static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, int Hq, int Hkv,
                          const int* pos, const int* slots, const void* cos_sin, void* k_cache,
                          void* v_cache, const int* block_tables, int bt_stride,
@@ -652,6 +687,9 @@ static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, i
     if (No % 16 || No <= 0 || !h || !gran2 || !epoch || (a.Ko / 32 + W - 1) / W > OQ ||
         stage > lds || a.n_o > groups || (g_qa_probe & 1))
       return (int)hipErrorInvalidValue;
+    // producers that went on to o_proj wait for the consumers, which wait for EVERY
+    // producer: the whole grid must be resident at once or it only ends at the spin bound
+    if (a.n_cons + groups > oproj_capacity(W, Hq / Hkv)) return (int)hipErrorInvalidConfiguration;
     return W == 8 ? launch_qa<8, true>(a, Hq / Hkv, groups, stream)
                   : launch_qa<4, true>(a, Hq / Hkv, groups, stream);
   }
@@ -667,6 +705,15 @@ P2P_API int p2p_qkv_attn(const void* Wt, const void* X, int ldx, int M, int K, i
   return qkv_attn_impl(Wt, X, ldx, M, K, Hq, Hkv, pos, slots, cos_sin, k_cache, v_cache,
                        block_tables, bt_stride, ctx_lens, scale, out, ldo, eps, gran, counters, err,
                        waves, nullptr, 0, nullptr, 0, nullptr, nullptr, stream);
+}
+
+// 1 if p2p_qkv_attn_oproj can run M rows of this shape (every workgroup resident at once).
+P2P_API int p2p_qkv_attn_oproj_fits(int M, int K, int Hq, int Hkv, int waves) {
+  if (M < 1 || M > 16 || Hkv <= 0 || Hq % Hkv) return 0;
+  const int groups = (Hq + 2 * Hkv) * (HD / 16);
+  int W = waves;
+  if (W != 4 && W != 8) W = (groups * 8 * 2 <= 4096 && (K / 32) / 8 >= 8) ? 8 : 4;
+  return M * Hkv + groups <= oproj_capacity(W, Hq / Hkv) ? 1 : 0;
 }
 
 // p2p_qkv_attn with the o_proj projection + residual in the same launch (TP = 1 decode):

@@ -103,12 +103,14 @@ class LlamaModel:
         # as ONE launch (ops.qkv_attn): the attention's block-table -> K/V load chain runs
         # behind the qkv weight stream.  P2P_QKV_ATTN=0: the two kernels.
         self.fuse_qkv_attn = os.environ.get("P2P_QKV_ATTN", "1") == "1"
-        # ... and, at TP = 1, the o_proj projection + residual in that same launch (its
-        # workgroups stream their weight slice into registers while the qkv weights and the
-        # attention run, then sweep the attention output as tagged granules): one launch
-        # boundary and one short weight-stream ramp less per layer.  P2P_QKV_ATTN_OPROJ=0:
-        # o_proj stays its own launch
-        self.fuse_qkv_attn_oproj = os.environ.get("P2P_QKV_ATTN_OPROJ", "1") == "1"
+        # ... and, at TP = 1, the o_proj projection + residual in that same launch (the
+        # producer workgroups take an o_proj column group after their qkv slice, weights in
+        # registers, the attention output swept from tagged granules).  Opt-in
+        # (P2P_QKV_ATTN_OPROJ=1): measured SLOWER than the separate o_proj launch at 8B --
+        # 24.1 vs 21.5 us per layer at batch 1, 33.0 vs 25.1 at 8 rows
+        # (profiles/r4_qkv_attn_oproj_negative.jsonl): the o_proj stream starts only when
+        # a producer's qkv slice is done, so it does not hide behind the attention
+        self.fuse_qkv_attn_oproj = os.environ.get("P2P_QKV_ATTN_OPROJ", "0") == "1"
         self.heads_max_rows = int(os.environ.get("P2P_HEADS_MAX_ROWS", "4"))
         # TP prefill: row-parallel GEMMs of >= this many rows overlap their all-reduce
         # (chunked, separate communication stream); decode-size sums use the one-shot AR
@@ -205,7 +207,8 @@ class LlamaModel:
               and row_bt is None and ws.qa is not None and isinstance(self.w.layers[0].qkv, torch.Tensor)
               and ops.qkv_attn_ok(R, self.nq, self.nkv, max_ctx))
         qa_o = (qa and self.fuse_qkv_attn_oproj and self.tp == 1
-                and ops.qkv_attn_oproj_ok(self.w.layers[0].o, self.nq, self.nkv))
+                and ops.qkv_attn_oproj_ok(self.w.layers[0].o, self.nq, self.nkv, rows=R,
+                                          hidden=cfg.hidden))
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)
             if qa:

@@ -59,6 +59,7 @@ _SIGS = {
     "p2p_qkv_attn": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_float, c_void_p,
                      c_int, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "p2p_qkv_attn_oproj_fits": [c_int, c_int, c_int, c_int, c_int],
     "p2p_qkv_attn_oproj": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                            c_float, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,

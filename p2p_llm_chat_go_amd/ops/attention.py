@@ -111,15 +111,31 @@ def qkv_attn_workspace(rows: int, n_heads: int, n_kv: int, device) -> tuple:
 QKV_ATTN_OPROJ_MAX_KSTEPS = 32
 
 
-def qkv_attn_oproj_ok(wo, n_heads: int, n_kv: int, waves: int = 4) -> bool:
-    """Can ops.qkv_attn run this o_proj (bf16, fragment-major) in its own launch?  Each
-    16-column group of o_proj is taken by one of the (n_heads + 2 n_kv) * 8 producer
-    workgroups after its qkv slice, so o_proj may not have more groups than that."""
+_OPROJ_FITS: dict = {}
+
+
+def qkv_attn_oproj_ok(wo, n_heads: int, n_kv: int, waves: int | None = None, rows: int = 1,
+                      hidden: int | None = None) -> bool:
+    """Can ops.qkv_attn run this o_proj (bf16, fragment-major) in its own launch for
+    ``rows`` batch rows?  Each 16-column group of o_proj is taken by one of the
+    (n_heads + 2 n_kv) * 8 producer workgroups after its qkv slice (so o_proj may not have
+    more groups than that), and the producers that wait for the attention need the whole
+    grid resident at once (checked against the device's occupancy, GPU only)."""
     if not isinstance(wo, torch.Tensor) or wo.dtype != torch.bfloat16:
         return False
     K = n_heads * HEAD_DIM
-    return (wo.shape[1] * 32 == K and -(-(K // 32) // waves) <= QKV_ATTN_OPROJ_MAX_KSTEPS
-            and wo.shape[0] <= (n_heads + 2 * n_kv) * (HEAD_DIM // 16))
+    w = QKV_ATTN_WAVES if waves is None else int(waves)
+    if not (wo.shape[1] * 32 == K and -(-(K // 32) // (w or 4)) <= QKV_ATTN_OPROJ_MAX_KSTEPS
+            and wo.shape[0] <= (n_heads + 2 * n_kv) * (HEAD_DIM // 16)):
+        return False
+    if wo.device.type != "cuda":
+        return True
+    key = (rows, hidden or wo.shape[0] * 16, n_heads, n_kv, w)
+    ok = _OPROJ_FITS.get(key)
+    if ok is None:
+        ok = bool(_lib.lib().p2p_qkv_attn_oproj_fits(rows, key[1], n_heads, n_kv, w))
+        _OPROJ_FITS[key] = ok
+    return ok
 
 
 QKV_ATTN_WAVES = int(os.environ.get("P2P_QA_WAVES", "0"))  # 0: heuristic (4 or 8)

@@ -120,7 +120,7 @@ def test_qkv_attn_oproj_matches_unfused(M, Hq, Hkv, K, No):
     g = torch.Generator().manual_seed(M + No)
     wo32 = torch.randn(No, Hq * 128, generator=g) * 0.03
     wo = ops.tile_weight(wo32.to(torch.bfloat16)).to(DEV)
-    assert ops.qkv_attn_oproj_ok(wo, Hq, Hkv)
+    assert ops.qkv_attn_oproj_ok(wo, Hq, Hkv, rows=M, hidden=K)
     # a 70B TP=8 rank's o_proj (512 column groups) has more groups than producers (80)
     assert not ops.qkv_attn_oproj_ok(torch.empty(512, 32, 64, 8, dtype=torch.bfloat16), 8, 1)
     h0 = torch.randn(M, No, generator=g).to(torch.bfloat16).to(DEV)
