@@ -52,6 +52,7 @@ void bind_runtime(py::module_& m) {
 #include <pybind11/functional.h>
 
 #include "runtime/engine_loop.h"
+#include "runtime/hip_dyn.h"
 
 namespace {
 
@@ -89,6 +90,8 @@ LoopConfig loop_cfg(const py::dict& d) {
 }  // namespace
 
 void bind_engine_loop(py::module_& m) {
+  m.def("loop_use_host_fake_hip", &hip_api_use_host_fake,
+        "tests: run the native engine loop on host memory with host-function 'graphs'");
   py::class_<EngineLoop>(m, "EngineLoop")
       .def(py::init([](py::dict d) { return new EngineLoop(loop_cfg(d)); }))
       .def("add_decode_graph",

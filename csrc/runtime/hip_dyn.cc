@@ -2,6 +2,8 @@
 
 #include <dlfcn.h>
 
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 
@@ -52,13 +54,77 @@ HipApi load() {
   return a;
 }
 
+HipApi& api_storage() {
+  static HipApi api;
+  return api;
+}
+
+std::once_flag g_once;
+
+// ---- host-only stand-in (hip_api_use_host_fake) ----
+int f_graph_launch(void* exec, void*) { return reinterpret_cast<int (*)()>(exec)(); }
+int f_memcpy(void* d, const void* s, size_t n, int, void*) {
+  std::memcpy(d, s, n);
+  return 0;
+}
+int f_memset(void* d, int v, size_t n, void*) {
+  std::memset(d, v, n);
+  return 0;
+}
+int f_memcpy2d(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t h, int, void*) {
+  for (size_t r = 0; r < h; ++r)
+    std::memcpy(static_cast<char*>(d) + r * dp, static_cast<const char*>(s) + r * sp, w);
+  return 0;
+}
+int f_stream_create(void** s, unsigned) {
+  *s = reinterpret_cast<void*>(1);
+  return 0;
+}
+int f_ok1(void*) { return 0; }
+int f_host_malloc(void** p, size_t n, unsigned) {
+  *p = std::malloc(n);
+  return *p ? 0 : 2;
+}
+int f_host_free(void* p) {
+  std::free(p);
+  return 0;
+}
+int f_set_device(int) { return 0; }
+int f_event_create(void** e, unsigned) {
+  *e = reinterpret_cast<void*>(1);
+  return 0;
+}
+int f_event_record(void*, void*) { return 0; }
+const char* f_err(int) { return "host fake HIP error"; }
+
 }  // namespace
 
 const HipApi& hip_api() {
-  static std::once_flag once;
-  static HipApi api;
-  std::call_once(once, [] { api = load(); });
-  return api;
+  std::call_once(g_once, [] { api_storage() = load(); });
+  return api_storage();
+}
+
+void hip_api_use_host_fake() {
+  std::call_once(g_once, [] {});
+  HipApi& a = api_storage();
+  a = HipApi();
+  a.ok = true;
+  a.graphLaunch = f_graph_launch;
+  a.memcpyAsync = f_memcpy;
+  a.memsetAsync = f_memset;
+  a.memcpy2DAsync = f_memcpy2d;
+  a.streamCreateWithFlags = f_stream_create;
+  a.streamDestroy = f_ok1;
+  a.streamSynchronize = f_ok1;
+  a.hostMalloc = f_host_malloc;
+  a.hostFree = f_host_free;
+  a.setDevice = f_set_device;
+  a.eventCreateWithFlags = f_event_create;
+  a.eventRecord = f_event_record;
+  a.eventSynchronize = f_ok1;
+  a.eventQuery = f_ok1;
+  a.eventDestroy = f_ok1;
+  a.getErrorString = f_err;
 }
 
 void hip_check(int rc, const char* what) {

@@ -42,4 +42,10 @@ const HipApi& hip_api();
 // Throws std::runtime_error("<what>: <hip error string>") when rc != 0.
 void hip_check(int rc, const char* what);
 
+// Tests without a GPU: replace the resolved API with a host-only stand-in (copies are
+// memcpy, streams and events are no-ops, pinned memory is malloc, and a "graph exec" is a
+// host function pointer `int (*)(void)` that hipGraphLaunch calls).  Lets the CPU tier run
+// the native engine loop against a simulated model.
+void hip_api_use_host_fake();
+
 }  // namespace p2p
