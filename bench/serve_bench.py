@@ -114,7 +114,10 @@ def main():
         "decode_chunk": srv.decode_chunk, "loop": a.loop,
         "mean_batch": round(toks / max(steps, 1), 2), "mixed": bool(a.mixed), "dtype": "bf16",
         "engine_time_s": {k: round(occ1[k] - occ0[k], 4) for k in
-                          ("busy_s", "prefill_s", "decode_s", "prefill_calls", "decode_calls")},
+                          ("busy_s", "prefill_s", "decode_s", "prefill_calls", "decode_calls",
+                           "capture_s", "captures", "eager_prefill_s", "eager_prefill_calls",
+                           "prefill_wait_s", "prefill_waits", "admit_wait_hits",
+                           "admit_wait_misses") if k in occ1},
         "data": "synthetic chat prompts, random-init weights"}), flush=True)
 
 

@@ -84,6 +84,8 @@ LoopConfig loop_cfg(const py::dict& d) {
   if (d.contains("ctx_buckets")) c.ctx_buckets = py::cast<std::vector<int>>(d["ctx_buckets"]);
   if (d.contains("row_buckets")) c.row_buckets = py::cast<std::vector<int>>(d["row_buckets"]);
   c.prefill_max_pages = val_of<int>(d, "prefill_max_pages", 64);
+  c.prefill_graph_after = val_of<int>(d, "prefill_graph_after", 2);
+  c.pipeline_free_slots = val_of<bool>(d, "pipeline_free_slots", false);
   return c;
 }
 

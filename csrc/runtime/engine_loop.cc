@@ -99,7 +99,10 @@ const DecodeGraphDesc* EngineLoop::decode_graph(int B, int ctx, bool greedy) {
   }
   if (!provider_) throw std::runtime_error("no decode graph for this batch / context bucket");
   drain();  // the provider captures on the GPU: nothing of ours may be in flight
+  const int64_t t0 = now_ns();
   provider_("decode", B, ctx, greedy);
+  capture_ns_ += now_ns() - t0;
+  n_captures_++;
   std::lock_guard<std::mutex> lk(gmu_);
   auto it = dgraphs_.find(key);
   if (it == dgraphs_.end()) throw std::runtime_error("graph provider registered no decode graph");
@@ -114,8 +117,14 @@ const PrefillGraphDesc* EngineLoop::prefill_graph(int rows, int nseq, bool greed
     if (it != pgraphs_.end()) return it->second.get();
   }
   if (!provider_) return nullptr;
+  // capturing costs a few forwards and a drained pipeline: a shape seen once (a rare mix of
+  // riders and new prompts) runs eagerly, one that recurs is captured
+  if (++puses_[key] < cfg_.prefill_graph_after) return nullptr;
   drain();
+  const int64_t t0 = now_ns();
   provider_("prefill", rows, nseq, greedy);
+  capture_ns_ += now_ns() - t0;
+  n_captures_++;
   std::lock_guard<std::mutex> lk(gmu_);
   auto it = pgraphs_.find(key);
   return it == pgraphs_.end() ? nullptr : it->second.get();
@@ -240,6 +249,13 @@ std::map<std::string, double> EngineLoop::metrics() {
   m["busy_s"] = busy_ns_ * 1e-9;
   m["prefill_s"] = prefill_ns_ * 1e-9;
   m["decode_s"] = decode_ns_ * 1e-9;
+  m["capture_s"] = capture_ns_ * 1e-9;  // inside the graph provider (captures)
+  m["captures"] = n_captures_;
+  m["eager_prefill_s"] = eager_ns_ * 1e-9;
+  m["prefill_wait_s"] = prefill_wait_ns_ * 1e-9;  // draining decode work before a prefill
+  m["prefill_waits"] = n_prefill_waits_;  // prefills that found decode work in flight
+  m["admit_wait_hits"] = n_admit_hits_;   // the admit wait saw the expected arrivals
+  m["admit_wait_misses"] = n_admit_misses_;
   m["running"] = sched_.n_running();
   m["waiting"] = sched_.n_waiting();
   m["free_kv_pages"] = sched_.free_pages();
@@ -373,8 +389,9 @@ void EngineLoop::step() {
     const int free = cfg_.max_batch - sched_.n_running() - sched_.n_waiting();
     if (free > 0) {
       const int want = std::min(done, free);
-      cv_.wait_for(lk, std::chrono::microseconds((int64_t)cfg_.admit_wait_us),
-                   [&] { return stop_ || sched_.n_waiting() >= want; });
+      const bool hit = cv_.wait_for(lk, std::chrono::microseconds((int64_t)cfg_.admit_wait_us),
+                                    [&] { return stop_ || sched_.n_waiting() >= want; });
+      (hit ? n_admit_hits_ : n_admit_misses_)++;
     }
   }
 }
@@ -382,9 +399,12 @@ void EngineLoop::step() {
 // ------------------------------------------------------------------ prefill
 void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
   const HipApi& h = hip_api();
+  const int64_t tw = now_ns();
+  if (!flight_.empty()) n_prefill_waits_++;
   drain();  // riders' last tokens must be current; nothing may write KV concurrently
   loaded_ = nullptr;  // the decode state no longer matches (new rows; riders advance)
   const int64_t t0 = now_ns();
+  prefill_wait_ns_ += t0 - tw;
   struct Seq {
     int64_t id;
     const std::vector<int>* prompt;  // admitted: the prompt
@@ -454,7 +474,9 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
       samp.push_back(s.samp);
     }
     riders.clear();
+    const int64_t te = now_ns();
     first = eager_(prompts, pages, starts, samp);
+    eager_ns_ += now_ns() - te;
     n_eager_prefill_++;
   } else {
     // chunk metadata (PrefillGraph.host_meta, engine/graph.py)
@@ -490,9 +512,9 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
       spos[b] = pos[r - 1];
     }
     const int n = r;
-    for (int i = n; i < R; ++i) {  // dummy rows: sequence S (the null page), no KV write
-      seq[i] = S;
-      pos[i] = i - n;
+    for (int i = n; i < R; ++i) {  // dummy rows: sequence S (the null page), no KV write,
+      seq[i] = S;                    // positions wrapped inside its block-table row
+      pos[i] = (i - n) % (P * 64);
     }
     for (int i = 0; i < R; ++i) {
       const int p = pos[i];
@@ -674,8 +696,19 @@ void EngineLoop::decode(const std::vector<int64_t>& running_in, bool waiting) {
   std::vector<int64_t> running = running_in;
   // chunk length: long chunks amortise the host round trip; a waiting request shortens it
   // (it is admitted at the next chunk boundary)
-  const int k = waiting ? 2 : ((int)running.size() < cfg_.max_batch ? std::max(2, cfg_.decode_chunk / 2)
-                                                                    : cfg_.decode_chunk);
+  int k = waiting ? 2 : ((int)running.size() < cfg_.max_batch ? std::max(2, cfg_.decode_chunk / 2)
+                                                              : cfg_.decode_chunk);
+  // steps until the first length stop among ids (minus what is already in flight): a chunk
+  // ends there, so that reply goes out and its slot is refilled without waiting for more
+  auto steps_left = [&](const std::vector<int64_t>& ids, int inflight) {
+    int left = 1 << 30;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int64_t id : ids) {
+      const SchedRequest& r = sched_.get(id);
+      left = std::min(left, r.max_new - (int)r.tokens.size());
+    }
+    return left - inflight;
+  };
   auto pick = [&](const std::vector<int64_t>& ids) {
     int need = 1;
     bool greedy = true;
@@ -693,11 +726,19 @@ void EngineLoop::decode(const std::vector<int64_t>& running_in, bool waiting) {
   };
   auto [B, C, greedy] = pick(running);
   const DecodeGraphDesc* g = decode_graph(B, C, greedy);
-  if (cfg_.pipeline && !flight_.empty() && flight_.back().g == g && flight_.back().ids == running &&
-      loaded_ == g && loaded_steps_ + k <= g->max_steps) {
-    // the running set is unchanged as far as the host knows: enqueue the next chunk on the
-    // device-resident state, then read the previous one while it runs
-    launch_chunk(g, running, false, k);
+  // speculating a chunk behind the running one doubles what a newly arriving request waits
+  // for before its prefill: only while no batch slot is free (nobody could be admitted)
+  const bool spec = cfg_.pipeline && !waiting &&
+                    (cfg_.pipeline_free_slots || (int)running.size() >= cfg_.max_batch);
+  int inflight = 0;
+  for (const Chunk& c : flight_) inflight += c.k;
+  const int spec_k = spec && !flight_.empty() ? std::min(k, steps_left(running, inflight)) : 0;
+  if (spec_k > 0 && flight_.back().g == g && flight_.back().ids == running &&
+      loaded_ == g && loaded_steps_ + spec_k <= g->max_steps) {
+    // the running set is unchanged as far as the host knows (and no length stop falls inside
+    // the chunk in flight): enqueue the next chunk on the device-resident state, then read
+    // the previous one while it runs
+    launch_chunk(g, running, false, spec_k);
     n_speculated_++;
     collect();
     decode_ns_ += now_ns() - t0;
@@ -706,9 +747,18 @@ void EngineLoop::decode(const std::vector<int64_t>& running_in, bool waiting) {
   drain();
   {
     std::lock_guard<std::mutex> lk(mu_);
+    // a request just finished: its reply goes out at this step's retire and its peer's next
+    // request (or one already waiting for the slot) would otherwise wait a whole chunk
+    // before its prefill.  Return to the step boundary instead (the next step decodes if
+    // nobody came).
+    if (sched_.n_finished() > 0) {
+      decode_ns_ += now_ns() - t0;
+      return;
+    }
     running = sched_.running();
   }
   if (running.empty()) return;
+  k = std::max(1, std::min(k, steps_left(running, 0)));
   std::tie(B, C, greedy) = pick(running);
   g = decode_graph(B, C, greedy);
   const bool load = !(loaded_ == g && loaded_ids_ == running && loaded_steps_ + k <= g->max_steps);

@@ -95,6 +95,8 @@ struct LoopConfig {
   std::vector<int> ctx_buckets{256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 131072};
   std::vector<int> row_buckets{16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024};
   int prefill_max_pages = 64;  // block-table width of the prefill graphs (their context bucket / 64)
+  bool pipeline_free_slots = false;  // speculate decode chunks even while a batch slot is free
+  int prefill_graph_after = 2;  // a chunk shape is captured on its n-th use (eager before)
 };
 
 struct LoopResult {
@@ -188,6 +190,7 @@ class EngineLoop {
   std::mutex gmu_;
   std::map<std::tuple<int, int, bool>, std::unique_ptr<DecodeGraphDesc>> dgraphs_;
   std::map<std::tuple<int, int, bool>, std::unique_ptr<PrefillGraphDesc>> pgraphs_;
+  std::map<std::tuple<int, int, bool>, int> puses_;  // uses of not-yet-captured chunk shapes
   GraphProvider provider_;
   EagerPrefill eager_;
 
@@ -205,7 +208,9 @@ class EngineLoop {
   std::atomic<long> n_requests_{0}, n_tokens_{0}, n_prefill_calls_{0}, n_decode_calls_{0},
       n_decode_steps_{0}, n_prefill_tokens_{0}, n_speculated_{0}, n_loads_{0}, n_errors_{0},
       n_eager_prefill_{0};
-  std::atomic<int64_t> busy_ns_{0}, prefill_ns_{0}, decode_ns_{0};
+  std::atomic<int64_t> busy_ns_{0}, prefill_ns_{0}, decode_ns_{0}, capture_ns_{0}, eager_ns_{0},
+      prefill_wait_ns_{0}, n_captures_{0}, n_prefill_waits_{0}, n_admit_hits_{0},
+      n_admit_misses_{0};
 };
 
 }  // namespace p2p

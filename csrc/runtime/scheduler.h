@@ -64,6 +64,7 @@ class Scheduler {
   // toks[i] are the tokens produced for ids[i] by consecutive decode steps.
   void on_decode_tokens(const std::vector<int64_t>& ids, const std::vector<std::vector<int>>& toks);
   std::vector<int64_t> take_finished();
+  size_t n_finished() const { return finished_.size(); }  // not yet taken
   const SchedRequest& get(int64_t id) const;
   void release(int64_t id);  // forget a finished request (frees nothing else)
   int n_waiting() const { return (int)waiting_.size(); }

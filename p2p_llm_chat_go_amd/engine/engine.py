@@ -109,6 +109,11 @@ class Engine:
             use_graph and self.device.type == "cuda" and tp_size == 1 and not cfg.is_moe
             and os.environ.get("P2P_PREFILL_GRAPH", "1") != "0")
         self._pgraphs = {}
+        # a chunk shape is captured once it has been seen this many times (eager before):
+        # capturing costs ~3 forwards, so a shape seen once (a rare rider / batch mix) is
+        # not worth it.  P2P_PREFILL_GRAPH_AFTER
+        self.prefill_graph_after = int(os.environ.get("P2P_PREFILL_GRAPH_AFTER", "2"))
+        self._pgraph_uses = {}
 
     # -------------------------------------------------------------- helpers
     def _sync(self):
@@ -132,13 +137,23 @@ class Engine:
             self._graphs[key] = g
         return g
 
+    def prefill_graph_key(self, rows: int, n_seq: int, max_ctx: int, greedy: bool = True):
+        return (bucket(rows, PREFILL_ROW_BUCKETS), min(bucket(n_seq, BATCH_BUCKETS), self.max_batch),
+                bucket(max_ctx, CTX_BUCKETS), greedy)
+
+    def prefill_graph_wanted(self, key) -> bool:
+        """Count a use of this chunk shape; True once it is (or should now be) captured."""
+        if key in self._pgraphs:
+            return True
+        n = self._pgraph_uses.get(key, 0) + 1
+        self._pgraph_uses[key] = n
+        return n >= self.prefill_graph_after
+
     def prefill_graph(self, rows: int, n_seq: int, max_ctx: int, greedy: bool = True) -> PrefillGraph:
         """The captured prefill of a chunk of <= ``rows`` rows from <= ``n_seq`` sequences
-        (bucketed), contexts <= ``max_ctx``; captured on first use."""
-        rb = bucket(rows, PREFILL_ROW_BUCKETS)
-        sb = min(bucket(n_seq, BATCH_BUCKETS), self.max_batch)
-        cb = bucket(max_ctx, CTX_BUCKETS)
-        key = (rb, sb, cb, greedy)
+        (bucketed), contexts <= ``max_ctx``; captured on first call."""
+        key = self.prefill_graph_key(rows, n_seq, max_ctx, greedy)
+        rb, sb, cb, _ = key
         g = self._pgraphs.get(key)
         if g is None:
             g = PrefillGraph(self.model, self.prefill_workspace(cb), rb, sb, cb // PAGE, cb,
@@ -196,8 +211,9 @@ class Engine:
     # -------------------------------------------------------------- prefill
     def prefill(self, prompts: list, block_tables: list, return_logits: bool = False,
                 sampling: list | None = None, starts: list | None = None,
-                pad_rows: int | None = None):
-        """Run all prompts (flat rows, chunked at max_prefill_tokens).
+                pad_rows: int | None = None, graph: bool = True):
+        """Run all prompts (flat rows, chunked at max_prefill_tokens); ``graph=False``
+        keeps it off the captured-chunk path (the native loop owns that policy).
 
         Returns int32 first tokens [B] on the device (and, with return_logits,
         the fp32 last-position logits [B, V_local] of every sequence).
@@ -223,7 +239,9 @@ class Engine:
             assert n_dummy >= 0, (pad_rows, len(rows))
             rows += [(B, i, 0) for i in range(n_dummy)]  # sequence B: the null page
         max_ctx = max([len(p) for p in prompts] + [n_dummy, 1])
-        if self._graph_prefill_ok(len(rows), B, max_ctx, n_dummy, return_logits):
+        if (graph and self._graph_prefill_ok(len(rows), B, max_ctx, n_dummy, return_logits) and
+                self.prefill_graph_wanted(self.prefill_graph_key(len(rows), B, max_ctx,
+                                                                 not sampled))):
             return self._prefill_graphed(prompts, block_tables, rows, max_ctx, sampling, sampled)
         ws = self.prefill_workspace(max_ctx)
         max_pages = bucket(max_ctx, CTX_BUCKETS) // PAGE

@@ -244,8 +244,8 @@ class PrefillGraph:
         self.greedy = greedy
         self.qtile = ops.flash_tile(model.nq, model.nkv, rows)
         # tiles never straddle sequences: <= rows / qtile + one partial tile per sequence
-        # (the dummy sequence included)
-        self.max_tiles = -(-rows // self.qtile) + n_seq + 1
+        # (the dummy sequence included) + one per wrap of the dummy rows' positions
+        self.max_tiles = -(-rows // self.qtile) + n_seq + 1 + rows // (max_pages * PAGE) + 1
         R, S = rows, n_seq
         sizes = [("bt", (S + 1) * max_pages), ("seq", R), ("pos", R), ("ids", R), ("slots", R),
                  ("ctx", R), ("out", S), ("spos", S), ("tiles", 4 * self.max_tiles)]
@@ -289,8 +289,8 @@ class PrefillGraph:
         if n:
             a = np.asarray(rows, dtype=np.int32).reshape(n, 3)
             seq[:n], pos[:n], v["ids"][:n] = a[:, 0], a[:, 1], a[:, 2]
-        seq[n:] = S  # dummy rows: sequence S (the null page), positions 0..
-        pos[n:] = np.arange(R - n, dtype=np.int32)
+        seq[n:] = S  # dummy rows: sequence S (the null page), positions 0.. wrapped inside
+        pos[n:] = np.arange(R - n, dtype=np.int32) % (P * PAGE)  # its block-table row
         slots = bt[seq, pos // PAGE] * PAGE + pos % PAGE
         slots[n:] = -1  # dummy rows write no KV
         v["slots"][:] = slots

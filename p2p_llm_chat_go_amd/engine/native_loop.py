@@ -70,7 +70,8 @@ class NativeEngineServer(EngineServer):
             "device": dev.index or 0, "batch_buckets": list(BATCH_BUCKETS),
             "ctx_buckets": list(CTX_BUCKETS),
             "row_buckets": [r for r in PREFILL_ROW_BUCKETS if r <= engine.max_prefill_tokens],
-            "prefill_max_pages": self.prefill_ctx // 64})
+            "prefill_max_pages": self.prefill_ctx // 64,
+            "prefill_graph_after": engine.prefill_graph_after})
         self.loop.set_provider(self._provide)
         self.loop.set_eager_prefill(self._eager_prefill)
         self._registered = set()
@@ -89,6 +90,7 @@ class NativeEngineServer(EngineServer):
             g = eng.decode_graph(a, b, greedy=greedy)
             self.loop.add_decode_graph(g.describe())
         else:
+            # (the loop asks only for shapes that recur: prefill_graph_after)
             g = eng.prefill_graph(a, b, self.prefill_ctx, greedy=greedy)
             self.loop.add_prefill_graph(g.describe())
         self._registered.add(key)
@@ -105,7 +107,7 @@ class NativeEngineServer(EngineServer):
     def _eager_prefill(self, prompts, pages, starts, samp):
         params = [SamplingParams(temperature=t, top_k=k, top_p=p, seed=s) for t, k, p, s in samp]
         first = self.engine.prefill(prompts, pages, sampling=params,
-                                    starts=starts if any(starts) else None)
+                                    starts=starts if any(starts) else None, graph=False)
         return [int(x) for x in first.cpu().tolist()]
 
     # --------------------------------------------------------------- API

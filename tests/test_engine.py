@@ -5,6 +5,7 @@ token stream must match the fp32 oracle within bf16 tolerance, and the engine's
 argmax must equal the oracle's wherever the oracle's top-2 margin is not a
 near-tie (random-init models have many near-ties).
 """
+import numpy as np
 import pytest
 import torch
 
@@ -248,8 +249,44 @@ def test_lazy_safetensors_reads_shard_slices(tmp_path, name):
         assert o and all(got[1] * tp == full[1] for _n, got, full in o)
 
 
+@pytest.mark.parametrize("rows,n_seq,pages,real", [(384, 8, 4, []), (1024, 8, 4, []),
+                                                     (384, 8, 4, [(0, 40), (1, 250)]),
+                                                     (64, 2, 1, [(0, 5)])])
+def test_prefill_graph_host_meta(rows, n_seq, pages, real):
+    """PrefillGraph.host_meta on the host: dummy rows (slot -1, the null-page sequence) keep
+    positions inside their block-table row even when the row bucket holds more rows than
+    the context bucket has positions (the capture-time image has no real rows at all), and
+    the query tiles cover every row, never straddle sequences and fit the bound."""
+    import types
+
+    from p2p_llm_chat_go_amd.engine.graph import PAGE, PrefillGraph
+
+    g = PrefillGraph(types.SimpleNamespace(device="cpu", nq=32, nkv=8), None, rows, n_seq,
+                     pages, pages * PAGE)
+    rws, bts, outs = [], [], []
+    for s, L in real:
+        bts.append([3 + s * pages + i for i in range(-(-L // PAGE))])
+        rws += [(s, i, 7) for i in range(L)]
+        outs.append(len(rws) - 1)
+    host = g.host_meta(rws, bts, outs).numpy()
+    v = {k: host[a:a + n] for k, (a, n) in g.offsets.items()}
+    n = len(rws)
+    assert (v["pos"] < pages * PAGE).all() and (v["pos"] >= 0).all()
+    assert (v["slots"][n:] == -1).all() and (v["seq"][n:] == n_seq).all()
+    for r, (s, i, _t) in enumerate(rws):
+        assert v["slots"][r] == bts[s][i // PAGE] * PAGE + i % PAGE
+    assert (v["ctx"] == v["pos"] + 1).all()
+    covered = np.zeros(rows, int)
+    for r0, k, sq, p0 in v["tiles"].reshape(-1, 4):
+        if k:
+            assert (v["seq"][r0:r0 + k] == sq).all()
+            assert (v["pos"][r0:r0 + k] == p0 + np.arange(k)).all()
+            covered[r0:r0 + k] += 1
+    assert (covered == 1).all()
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("lens", [[44], [5, 37, 12], [60, 3], [130]])
+@pytest.mark.parametrize("lens", [[44], [5, 37, 12], [60, 3], [130], [44] * 7])
 def test_prefill_graph_equals_eager_gpu(lens):
     """A graph-captured prefill chunk (engine.graph.PrefillGraph: padded row bucket,
     padding tiles, dummy rows on the null page) gives the eager prefill's first tokens,
@@ -261,9 +298,10 @@ def test_prefill_graph_equals_eager_gpu(lens):
     prompts = [[(37 * b + 11 * i) % 5000 + 100 for i in range(L)] for b, L in enumerate(lens)]
     out = {}
     for graph in (False, True):
-        eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_batch=4)
+        eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_batch=8)
         assert eng.prefill_graphs_enabled
         eng.prefill_graphs_enabled = graph
+        eng.prefill_graph_after = 1  # capture on first use
         pages = [eng.kv.allocator.alloc(3) for _ in prompts]
         first = eng.prefill(prompts, pages).cpu()
         assert bool(eng._pgraphs) == graph
@@ -288,10 +326,21 @@ def test_prefill_graph_equals_eager_gpu(lens):
         for p in pages:
             eng.kv.allocator.free(p)
         gen = [r.tokens for r in eng.generate(prompts, 12, stop_on_eos=False)]
-        out[graph] = (first, kv, logits, gen)
-    (f0, kv0, l0, g0), (f1, kv1, l1, g1) = out[False], out[True]
+        out[graph] = (first, kv, logits, gen, eng)
+    (f0, kv0, l0, g0, eager), (f1, kv1, l1, g1, _) = out[False], out[True]
     assert torch.equal(f0, f1)
     for a, b in zip(kv0, kv1):
         assert (a - b).abs().max() <= 1e-2 * max(1.0, float(a.abs().max()))
     assert ((l0 - l1).norm() / l0.norm()) < 1e-2
-    assert g0 == g1
+    # decoding continues identically -- up to a near-tie of the random model, which the
+    # padded chunk's different GEMM shape may round the other way: check its margin
+    for p, a, b in zip(prompts, g0, g1):
+        if a == b:
+            continue
+        j = next(i for i, (x, y) in enumerate(zip(a, b)) if x != y)
+        toks = p + a[:j]
+        pages = eager.kv.allocator.alloc(-(-len(toks) // 64))
+        _f, lg = eager.prefill([toks], [pages], return_logits=True)
+        eager.kv.allocator.free(pages)
+        lg = lg[0].float().cpu()
+        assert abs(float(lg[a[j]] - lg[b[j]])) < 2e-2 * float(lg.abs().max()), (j, a, b)

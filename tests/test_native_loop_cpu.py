@@ -99,7 +99,7 @@ class FakeModel:
 
     def prefill(self, rows, nseq, greedy, qtile=16):
         R, S, P = rows, nseq, self.P
-        max_tiles = -(-R // qtile) + S + 1
+        max_tiles = -(-R // qtile) + S + 1 + R // (P * PAGE) + 1  # as PrefillGraph
         sizes = [("bt", (S + 1) * P), ("seq", R), ("pos", R), ("ids", R), ("slots", R),
                  ("ctx", R), ("out", S), ("spos", S), ("tiles", 4 * max_tiles)]
         off, o = {}, 0
@@ -161,13 +161,14 @@ class FakeModel:
         return [nxt(p[-1], len(p) - 1, 0 if t <= 0 else s) for p, (t, _k, _p, s) in zip(prompts, samp)]
 
 
-def make_loop(pipeline=True, max_batch=8, chunk=4):
+def make_loop(pipeline=True, max_batch=8, chunk=4, free_slots=True):
     N = load()
     N.loop_use_host_fake_hip()
     model = FakeModel(prefill_pages=4)
     loop = N.EngineLoop({"num_pages": 256, "max_batch": max_batch, "max_prefill_tokens": 256,
                          "max_ctx": 2048, "eos": [EOS], "decode_chunk": chunk,
                          "admit_wait_us": 200.0, "pipeline": pipeline,
+                         "pipeline_free_slots": free_slots,
                          "row_buckets": [16, 32, 48, 64, 96, 128, 192, 256],
                          "prefill_max_pages": 4})
     model.loop = loop
@@ -281,5 +282,26 @@ def test_loop_deadline_with_stall():
         loop.release(rid)
         m = _wait_idle(loop)
         assert m["free_kv_pages"] == 255 and m["running"] == 0, m
+    finally:
+        loop.shutdown()
+
+
+@pytest.mark.parametrize("max_batch,n,spec", [(4, 4, True), (8, 2, False)])
+def test_loop_speculates_only_with_full_batch(max_batch, n, spec):
+    """Default policy: a decode chunk is speculated behind the running one only while every
+    batch slot is taken -- otherwise a request arriving would wait for two chunks."""
+    loop, model = make_loop(max_batch=max_batch, free_slots=False)
+    try:
+        prompts = [[11 + i, 12, 13] for i in range(n)]
+        loop.stall(0.5)  # all of them admitted in one step
+        ids = [loop.submit(p, 60, False) for p in prompts]
+        loop.stall(0.0)
+        for p, rid in zip(prompts, ids):
+            r = loop.wait(rid, 10.0)
+            assert r["tokens"] == expected(p, 60, False)
+            loop.release(rid)
+        m = _wait_idle(loop)
+        assert (m["speculated_chunks"] > 0) == spec, m
+        assert not model.errors, model.errors[:3]
     finally:
         loop.shutdown()

@@ -29,6 +29,27 @@ def _engine(max_batch=4, layers=3, seed=5):
                   max_prefill_tokens=256), w, cfg
 
 
+def _same_or_near_tie(eng, prompt, got, ref, margin=2e-2):
+    """``got`` equals ``ref`` -- or first differs where the reference logits of the two
+    candidates are within ``margin`` of the largest (a batch-shape rounding flip of the
+    random model, not a loop bug)."""
+    if got == ref:
+        return True
+    j = next((i for i, (x, y) in enumerate(zip(got, ref)) if x != y), min(len(got), len(ref)))
+    if j >= min(len(got), len(ref)):
+        return False  # one is a prefix of the other: a length bug
+    toks = prompt + ref[:j]
+    pages = eng.kv.allocator.alloc(-(-len(toks) // 64))
+    try:
+        _f, lg = eng.prefill([toks], [pages], return_logits=True)
+    finally:
+        eng.kv.allocator.free(pages)
+    lg = lg[0].float().cpu()
+    gap = abs(float(lg[got[j]] - lg[ref[j]]))
+    assert gap < margin * float(lg.abs().max()), (j, gap, float(lg.abs().max()), got, ref)
+    return True
+
+
 def _prompts(n):
     return [[(13 * b + 7 * i) % 250 + 3 for i in range(5 + 11 * b)] for b in range(n)]
 
@@ -142,6 +163,7 @@ def test_native_loop_8b_width_graphs():
     eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_batch=8)
     prompts = [[(97 * b + 31 * i) % 9000 + 200 for i in range(44 - 7 * b)] for b in range(4)]
     ref = [eng.generate([p], 16, stop_on_eos=False)[0].tokens for p in prompts]
+    eng.prefill_graph_after = 1  # every chunk shape through a captured graph
     srv = NativeEngineServer(eng, max_batch=8)
     try:
         outs = [None] * 4
@@ -149,7 +171,9 @@ def test_native_loop_8b_width_graphs():
             prompts[i], SamplingParams(max_tokens=16, stop_on_eos=False)))) for i in range(4)]
         [t.start() for t in ths]
         [t.join() for t in ths]
-        assert [o["tokens"] for o in outs] == ref
         torch.cuda.synchronize()
     finally:
         srv.close()
+    for p, o, r in zip(prompts, outs, ref):  # (the loop is gone: the engine is ours again)
+        assert len(o["tokens"]) == 16
+        assert _same_or_near_tie(eng, p, o["tokens"], r)
