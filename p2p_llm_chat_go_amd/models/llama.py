@@ -112,6 +112,15 @@ class LlamaModel:
         # a producer's qkv slice is done, so it does not hide behind the attention
         self.fuse_qkv_attn_oproj = os.environ.get("P2P_QKV_ATTN_OPROJ", "0") == "1"
         self.heads_max_rows = int(os.environ.get("P2P_HEADS_MAX_ROWS", "4"))
+        # decode steps of <= 4 rows at contexts <= 256 (TP = 1, dense, bf16 weights): every
+        # layer in ONE persistent launch (ops.decode_engine; hand-offs between workgroups
+        # instead of kernel boundaries).  Opt-in (P2P_DECODE_ENGINE=1): measured SLOWER at
+        # 8B -- 88-99 vs ~81 us per layer (profiles/r4_decode_engine_negative.jsonl): its
+        # weight streams beat the separate kernels, but a chip-wide hand-off costs 3.5-5 us
+        # under streaming load against ~1.5 us per kernel boundary
+        self.decode_engine = os.environ.get("P2P_DECODE_ENGINE", "0") == "1"
+        self._de = None
+        self._de_ok = {}
         # TP prefill: row-parallel GEMMs of >= this many rows overlap their all-reduce
         # (chunked, separate communication stream); decode-size sums use the one-shot AR
         self.overlap_min_rows = int(os.environ.get("P2P_TP_OVERLAP_MIN_ROWS", "256"))
@@ -196,6 +205,10 @@ class LlamaModel:
         cfg = self.cfg
         h = ws.h[:R]
         ops.gather_rows(self.w.embed, ids[:R], out=h)
+        if (self.decode_engine and tiles is None and row_bt is None and out_rows is None
+                and self._decode_engine_ok(R, max_ctx)):
+            self._de.run(h, pos[:R], slots[:R], self.rope, block_tables, ctx_lens[:R], ws.err)
+            return self._head(ws, h, R, out_rows, n_out, greedy)
         q, attn = ws.q[:R], ws.attn[:R]
         fused = (self.fuse_attn_oproj and tiles is None and self.tp == 1
                  and self.device.type == "cuda" and isinstance(self.w.layers[0].o, torch.Tensor)
@@ -241,6 +254,21 @@ class LlamaModel:
                                         workspace=ws.attn_ws)
                 self._row_parallel(lw.o, attn, h, ws, R)
             self._mlp(lw, ws, R)
+        return self._head(ws, h, R, out_rows, n_out, greedy)
+
+    def _decode_engine_ok(self, R: int, max_ctx: int) -> bool:
+        from ..ops.decode_engine import DecodeEngine, decode_engine_ok
+
+        key = (R, max_ctx)
+        ok = self._de_ok.get(key)
+        if ok is None:
+            ok = self._de_ok[key] = decode_engine_ok(self, R, max_ctx)
+        if ok and self._de is None:
+            self._de = DecodeEngine(self)
+        return ok
+
+    def _head(self, ws: Workspace, h, R: int, out_rows, n_out, greedy: bool):
+        cfg = self.cfg
         if n_out == 0:
             return None
         if out_rows is None:

@@ -117,6 +117,13 @@ _SIGS = {
                               c_int, c_void_p],
     "p2p_moe_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p],
+    # persistent decode engine (decode_engine.hip)
+    "p2p_decode_engine_ok": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "p2p_decode_engine_grid": [c_int, c_int, c_int],
+    "p2p_decode_engine_trace": [c_void_p],
+    "p2p_decode_engine": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                          c_float, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     # expert-parallel all-to-all over IPC peer buffers (ep_a2a.hip)
     "p2p_ep_set_timeout_ms": [c_int],
     "p2p_ep_dispatch": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
@@ -159,6 +166,10 @@ def lib():
         fn = getattr(L, "p2p_ep_buffer_bytes", None)
         if fn is not None:
             fn.argtypes = [c_int, c_int]
+            fn.restype = ctypes.c_size_t
+        fn = getattr(L, "p2p_decode_engine_ws_bytes", None)
+        if fn is not None:
+            fn.argtypes = [c_int, c_int, c_int, c_int, c_int]
             fn.restype = ctypes.c_size_t
         fn = getattr(L, "p2p_tiled_gemm_config", None)
         if fn is not None:
