@@ -46,6 +46,10 @@ int skinny_unit_ar(SKINNY_UNIT_ARGS);
 
 constexpr int MIDM_FLAG = 1 << 25;  // launch-code bit (ops.gemm.MIDM_FLAG)
 constexpr int WIDE_FLAG = 1 << 26;  // launch-code bit (ops.gemm.WIDE_FLAG), K slices in bits 8..15
+constexpr int PERSIST_FLAG = 1 << 28;  // ops.gemm.PERSIST_FLAG: persist_gemv.hip, CU multiple in 8..15
+extern "C" int p2p_persist_gemv(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
+                                int norm, void* out, int ldo, float eps, int grid_mult,
+                                hipStream_t st);
 extern "C" int p2p_wide_dispatch(const void* Wt, const void* X, int ldx, int M, int K, int N,
                                  int epi, int norm, void* out, int ldo, float eps, const void* ea_p,
                                  int req_split, hipStream_t st);
@@ -80,6 +84,9 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
     groups = N / 32;
     up_off = groups;
   }
+  // bit 28: the persistent GEMV (persist_gemv.hip; bf16 dense weights, M <= 16)
+  if ((waves & PERSIST_FLAG) && !ea.wscale && !ea.moe_cnt)
+    return p2p_persist_gemv(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, (waves >> 8) & 0xff, stream);
   // bit 26: the wide mid-M kernel (wide_gemm.hip; bf16 dense weights, K % 256 == 0)
   if ((waves & WIDE_FLAG) && epi != EPI_AR)
     return p2p_wide_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, &ea, (waves >> 8) & 0xff,

@@ -113,6 +113,8 @@ def _configs(K, M=1, tiled=False, midm=False, wide=False):
 
 
 def describe(code: int) -> str:
+    if code & G.PERSIST_FLAG:
+        return "persist/x%d" % max(1, (code >> 8) & 0xff)
     if code & G.TILED_FLAG:
         return "tiled"
     if code & G.MIDM_FLAG:
@@ -176,6 +178,8 @@ def autotune_model(model, batch_sizes=(1,), verbose=False, table: dict | None = 
                 # the 1 GB LM head stream: the wide kernel's 8 x 3 chunks of weights in flight
                 # per workgroup against the skinny launches
                 codes += [G.WIDE_FLAG]
+            # (the persistent GEMV, G.PERSIST_FLAG, is not a candidate: 1.3-1.6x slower than
+            # the skinny launches on every 8B decode shape, profiles/r4_persist_gemv_negative.jsonl)
             if bf and epi == G.EPI_QKV_ROPE and M > 16:
                 # pack the activations fragment-major first (one extra launch, timed with the
                 # GEMM): measured to pay on the qkv shape only (profiles/r3_afrag_probe.jsonl)

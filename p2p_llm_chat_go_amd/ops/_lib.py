@@ -117,6 +117,7 @@ _SIGS = {
                               c_int, c_void_p],
     "p2p_moe_combine": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p],
+    "p2p_persist_gemv_ok": [c_int, c_int, c_int, c_int],
     # persistent decode engine (decode_engine.hip)
     "p2p_decode_engine_ok": [c_int, c_int, c_int, c_int, c_int, c_int],
     "p2p_decode_engine_grid": [c_int, c_int, c_int],

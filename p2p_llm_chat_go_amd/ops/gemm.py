@@ -156,6 +156,15 @@ MIDM_FLAG = 1 << 25
 WIDE_FLAG = 1 << 26
 # launch-code bit: the skinny kernel's X is fragment-major (pack_frag), not row-major
 AFRAG_FLAG = 1 << 27
+# the persistent GEMV (csrc/kernels/persist_gemv.hip): one 4-wave workgroup per CU (x the
+# multiple in bits 8..15) walking balanced 16-column units with the weight stream carried
+# across them; M <= 16, bf16 weights, K % 1024 == 0.  Measured 1.3-1.6x slower than the
+# skinny launches (profiles/r4_persist_gemv_negative.jsonl): explicit launch codes only
+PERSIST_FLAG = 1 << 28
+
+
+def persist_ok(M: int, K: int, N: int, epi: int) -> bool:
+    return bool(_lib.lib().p2p_persist_gemv_ok(M, K, N, epi))
 
 
 _PACK_BUF: dict = {}
@@ -323,7 +332,7 @@ def skinny_ar_ok(wt, M: int) -> bool:
     tiled / mid-M kernel (prompt-sized M) keeps the partial store + one-shot kernel."""
     if M > SKINNY_MAX_M:
         return False
-    return not (_code(wt, M, EPI_AR, False, 0) & (TILED_FLAG | MIDM_FLAG | WIDE_FLAG))
+    return not (_code(wt, M, EPI_AR, False, 0) & (TILED_FLAG | MIDM_FLAG | WIDE_FLAG | PERSIST_FLAG))
 
 
 def skinny_gemm_ar(wt, x: torch.Tensor, h: torch.Tensor, car, waves: int = 0) -> torch.Tensor:

@@ -77,6 +77,42 @@ def test_skinny_gemm_silu(M):
     assert _rel(out.cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("epi", ["resid", "silu", "store", "f32"])
+@pytest.mark.parametrize("M", [1, 4, 16])
+@pytest.mark.parametrize("mult", [1, 2])
+def test_persist_gemv(epi, M, mult):
+    """The persistent GEMV launch code (ops.gemm.PERSIST_FLAG, csrc/kernels/persist_gemv.hip)
+    vs fp32: residual add, SwiGLU on half pairs (gate / up lanes in one MFMA operand),
+    store with RMSNorm, fp32 -- more units than workgroups (cross-unit prefetch)."""
+    from p2p_llm_chat_go_amd.ops import gemm as G
+
+    torch.manual_seed(M * 11 + mult)
+    K = 2048
+    N = 1536 if epi == "silu" else 1024
+    W = (torch.randn(N, K) * 0.03).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    acc = x.float() @ W.float().t()
+    rstd = torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    code = G.PERSIST_FLAG | (mult << 8)
+    Wt = ops.tile_weight(W).to(DEV)
+    e = {"resid": ops.EPI_RESID, "silu": ops.EPI_SILU, "store": ops.EPI_STORE, "f32": ops.EPI_F32}[epi]
+    assert G.persist_ok(M, K, N, e)
+    if epi == "resid":
+        h = torch.randn(M, N).to(torch.bfloat16)
+        ref = h.float() + acc
+        out = h.to(DEV)
+        ops.skinny_gemm(Wt, x.to(DEV), e, out=out, waves=code)
+    elif epi == "silu":
+        a = acc * rstd
+        ref = torch.nn.functional.silu(a[:, :N // 2]) * a[:, N // 2:]
+        out = ops.skinny_gemm(Wt, x.to(DEV), e, norm=True, waves=code)
+    else:
+        ref = acc * rstd
+        out = ops.skinny_gemm(Wt, x.to(DEV), e, norm=True, waves=code)
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref) < (5e-3 if epi == "f32" else 1e-2)
+
+
 def test_skinny_gemm_matches_cpu_path_bitwise_shape():
     # the CPU reference path of the same op agrees with the kernel
     torch.manual_seed(3)
