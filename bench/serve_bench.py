@@ -45,6 +45,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1, help="serve through engine.cluster on N GPUs")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--ep", type=int, default=1)
+    ap.add_argument("--warm-rounds", type=int, default=1,
+                    help="untimed rounds of the timed pattern first (every peer's requests in "
+                         "sequence): graphs for the shapes the mix hits -- a prompt-chunk shape "
+                         "is captured on its 2nd use")
     ap.add_argument("--loop", choices=("native", "python"), default="native",
                     help="native: the C++ step loop replaying captured graphs "
                          "(engine.native_loop); python: engine.server's loop")
@@ -78,18 +82,25 @@ def main():
         n = a.new_tokens - (i * 7919) % (a.jitter + 1)
         return SamplingParams(max_tokens=max(1, n), stop_on_eos=False)
 
-    # warm pass (graphs for every batch bucket the mix will hit)
+    results, lock = [], threading.Lock()
+
+    def peer(p, keep=True):
+        for r in range(a.requests):
+            out = srv.generate(prompts[p], params(p * 31 + r))
+            if keep:
+                with lock:
+                    results.append(out)
+
+    # warm pass (graphs for every batch bucket the burst hits), then untimed rounds of the
+    # timed pattern (the steady-state prompt-chunk shapes: one new prompt + riders)
     ths = [threading.Thread(target=srv.generate, args=(prompts[p], params(p), 600))
            for p in range(a.peers)]
     [t.start() for t in ths]
     [t.join() for t in ths]
-    results, lock = [], threading.Lock()
-
-    def peer(p):
-        for r in range(a.requests):
-            out = srv.generate(prompts[p], params(p * 31 + r))
-            with lock:
-                results.append(out)
+    for _ in range(a.warm_rounds):
+        ths = [threading.Thread(target=peer, args=(p, False)) for p in range(a.peers)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
 
     occ0 = stats()
     t0 = time.perf_counter()
@@ -111,7 +122,7 @@ def main():
         "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
         "queue_p50_ms": round(statistics.median(queue), 3),
         "queue_p99_ms": round(queue[min(len(queue) - 1, int(0.99 * len(queue)))], 3),
-        "decode_chunk": srv.decode_chunk, "loop": a.loop,
+        "decode_chunk": srv.decode_chunk, "loop": a.loop, "warm_rounds": a.warm_rounds,
         "mean_batch": round(toks / max(steps, 1), 2), "mixed": bool(a.mixed), "dtype": "bf16",
         "engine_time_s": {k: round(occ1[k] - occ0[k], 4) for k in
                           ("busy_s", "prefill_s", "decode_s", "prefill_calls", "decode_calls",
