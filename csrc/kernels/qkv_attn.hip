@@ -27,7 +27,7 @@ namespace {
 constexpr int PAGE = 64;
 constexpr int HD = 128;
 constexpr int QA_U = 4;       // producer: k-steps per pipeline batch
-constexpr int VS = HD + 8;    // V row stride in LDS (bf16): conflict-free 16-B writes
+constexpr int VT = 64 + 8;    // V^T row stride in LDS (keys, bf16): one row per head dim
 constexpr long long QA_SPIN_TICKS = 500000000ll;  // 5 s at the 100 MHz wall clock
 
 typedef unsigned long long u64;
@@ -222,10 +222,14 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
   const int kk = lane & 15, qd = lane >> 4;
   const int ctx = a.ctx_lens[r];
   const int nprev = ctx - 1;  // keys already in the cache; key nprev is this step's token
-  auto& vs = *reinterpret_cast<bf16(*)[KW][MKPW][VS]>(smem);
-  auto& so = *reinterpret_cast<float(*)[KW][G][HD]>(smem);  // after P.V (aliases vs)
-  char* p = smem + (sizeof(bf16) * KW * MKPW * VS > sizeof(float) * KW * G * HD
-                        ? sizeof(bf16) * KW * MKPW * VS
+  // V is kept TRANSPOSED per wave (vt[w][dim][key]): the P.V B operand of lane (kk, qd) is
+  // then 4 + 4 consecutive keys of one dim -- two 8-byte LDS reads per column block after
+  // the hand-off, where [key][dim] rows took eight 2-byte reads.  The transpose (scalar
+  // writes) happens at kernel start, behind the producers' weight stream.
+  auto& vt = *reinterpret_cast<bf16(*)[KW][HD][VT]>(smem);
+  auto& so = *reinterpret_cast<float(*)[KW][G][HD]>(smem);  // after P.V (aliases vt)
+  char* p = smem + (sizeof(bf16) * KW * HD * VT > sizeof(float) * KW * G * HD
+                        ? sizeof(bf16) * KW * HD * VT
                         : sizeof(float) * KW * G * HD);
   auto& cur = *reinterpret_cast<unsigned(*)[G + 2][64]>(p);  // q heads, k, v: bf16 pairs
   p += sizeof(unsigned) * (G + 2) * 64;
@@ -255,7 +259,8 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2)
-        *reinterpret_cast<bf16x8*>(&vs[w][16 * bb + kk][32 * s2 + 8 * qd]) = vr[bb][s2];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vt[w][32 * s2 + 8 * qd + j][16 * bb + kk] = vr[bb][s2][j];
   } else {
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb)
@@ -303,7 +308,9 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
           for (int s2 = 0; s2 < 4; ++s2) kr[bb][s2] = frag(G, s2);
         }
     }
-    *reinterpret_cast<unsigned*>(&vs[w][rn][2 * lane]) = cur[G + 1][lane];
+    const bf16x2 v2 = as_bf16x2(cur[G + 1][lane]);
+    vt[w][2 * lane][rn] = v2[0];
+    vt[w][2 * lane + 1][rn] = v2[1];
   }
   bf16x8 qf[4];
 #pragma unroll
@@ -360,11 +367,13 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
       }
 #pragma unroll
       for (int c = 0; c < HD / 16; ++c) {
+        const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(&vt[w][16 * c + kk][32 * t + 4 * qd]);
+        const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&vt[w][16 * c + kk][32 * t + 16 + 4 * qd]);
         bf16x8 vb;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          vb[j] = vs[w][32 * t + 4 * qd + j][16 * c + kk];
-          vb[4 + j] = vs[w][32 * t + 16 + 4 * qd + j][16 * c + kk];
+          vb[j] = v0[j];
+          vb[4 + j] = v1[j];
         }
         o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[c], 0, 0, 0);
       }
@@ -541,7 +550,7 @@ __device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem, const 
 
 template <int G>
 constexpr size_t consumer_lds() {
-  const size_t v = sizeof(bf16) * KW * MKPW * VS;
+  const size_t v = sizeof(bf16) * KW * HD * VT;
   const size_t o = sizeof(float) * KW * G * HD;
   return (v > o ? v : o) + sizeof(unsigned) * (G + 2) * 64 + 2 * sizeof(float) * KW * G;
 }
