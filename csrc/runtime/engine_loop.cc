@@ -109,13 +109,22 @@ const DecodeGraphDesc* EngineLoop::decode_graph(int B, int ctx, bool greedy) {
   return it->second.get();
 }
 
+const PrefillGraphDesc* EngineLoop::find_prefill_graph(int rows, int nseq, bool greedy) {
+  // the smallest registered graph of this row bucket holding >= nseq sequences (a graph's
+  // sequence bucket is the engine's, which a server with a smaller batch may round up)
+  std::lock_guard<std::mutex> lk(gmu_);
+  const PrefillGraphDesc* best = nullptr;
+  for (const auto& kv : pgraphs_) {
+    const PrefillGraphDesc* g = kv.second.get();
+    if (g->rows == rows && g->greedy == greedy && g->n_seq >= nseq && (!best || g->n_seq < best->n_seq))
+      best = g;
+  }
+  return best;
+}
+
 const PrefillGraphDesc* EngineLoop::prefill_graph(int rows, int nseq, bool greedy) {
   const auto key = std::make_tuple(rows, nseq, greedy);
-  {
-    std::lock_guard<std::mutex> lk(gmu_);
-    auto it = pgraphs_.find(key);
-    if (it != pgraphs_.end()) return it->second.get();
-  }
+  if (const PrefillGraphDesc* g = find_prefill_graph(rows, nseq, greedy)) return g;
   if (!provider_) return nullptr;
   // capturing costs a few forwards and a drained pipeline: a shape seen once (a rare mix of
   // riders and new prompts) runs eagerly, one that recurs is captured
@@ -125,9 +134,7 @@ const PrefillGraphDesc* EngineLoop::prefill_graph(int rows, int nseq, bool greed
   provider_("prefill", rows, nseq, greedy);
   capture_ns_ += now_ns() - t0;
   n_captures_++;
-  std::lock_guard<std::mutex> lk(gmu_);
-  auto it = pgraphs_.find(key);
-  return it == pgraphs_.end() ? nullptr : it->second.get();
+  return find_prefill_graph(rows, nseq, greedy);
 }
 
 // ------------------------------------------------------------------ lifecycle

@@ -168,6 +168,7 @@ class EngineLoop {
   void drain();    // read every chunk in flight
   void fail_all(const std::string& why);
   const DecodeGraphDesc* decode_graph(int B, int ctx, bool greedy);
+  const PrefillGraphDesc* find_prefill_graph(int rows, int nseq, bool greedy);
   const PrefillGraphDesc* prefill_graph(int rows, int nseq, bool greedy);
   static int bucket(int x, const std::vector<int>& b);
   void* pinned(int slot, size_t bytes);

@@ -95,14 +95,30 @@ class NativeEngineServer(EngineServer):
             self.loop.add_prefill_graph(g.describe())
         self._registered.add(key)
 
-    def prewarm(self, batches=None, rows=(16, 32, 48, 64, 96, 128)):
+    def prewarm(self, batches=None, rows=None, mode=None):
         """Capture the chat-typical shapes before the first request: decode graphs of every
-        batch bucket at the 256-token context, prefill chunks of one prompt."""
+        batch bucket at the 256-token context, and greedy prompt chunks of every (row
+        bucket, sequence bucket) -- a chunk's sequence count is the new prompts plus the
+        riders, so under load it is the batch bucket, and a shape first met under load
+        would otherwise be captured in the middle of serving (~15-100 ms stalls at the p99:
+        profiles/r4_serve_native_vs_python.jsonl).  ENGINE_PREWARM: "full" (default),
+        "basic" (one-prompt chunks of <= 128 rows), "off"."""
+        mode = mode or os.environ.get("ENGINE_PREWARM", "full")
+        if mode == "off":
+            return
         for B in batches or [b for b in BATCH_BUCKETS if b <= self.max_batch]:
             self._provide("decode", B, 256, True)
-        for r in rows:
-            if r <= self.engine.max_prefill_tokens:
-                self._provide("prefill", r, 1, True)
+        eng = self.engine
+        if mode == "basic":
+            seqs, rows = [1], rows or (16, 32, 48, 64, 96, 128)
+        else:
+            seqs = sorted({min(b, self.max_batch) for b in BATCH_BUCKETS
+                           if b < 2 * self.max_batch})
+            rows = rows or PREFILL_ROW_BUCKETS
+        for sb in seqs:
+            for r in rows:
+                if sb <= r <= eng.max_prefill_tokens:
+                    self._provide("prefill", r, sb, True)
 
     def _eager_prefill(self, prompts, pages, starts, samp):
         params = [SamplingParams(temperature=t, top_k=k, top_p=p, seed=s) for t, k, p, s in samp]
