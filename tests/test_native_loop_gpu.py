@@ -177,3 +177,85 @@ def test_native_loop_8b_width_graphs():
     for p, o, r in zip(prompts, outs, ref):  # (the loop is gone: the engine is ours again)
         assert len(o["tokens"]) == 16
         assert _same_or_near_tie(eng, p, o["tokens"], r)
+
+
+def test_native_loop_randomized_stress():
+    """Mixed traffic through the C++ loop for a while: concurrent peers sending prompts of
+    1-400 tokens (past the prefill graphs' context: the eager path), 1-60 new tokens, a third
+    of them sampled, some abandoned by a short deadline (cancelled inside the loop), some
+    streamed.  Every answered greedy request must equal the static engine's reply for it
+    (up to a near-tie), sampled ones must reproduce with their seed, nothing may error, and
+    every KV page must come back."""
+    import random
+
+    from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
+    from p2p_llm_chat_go_amd.engine.server import EngineTimeout
+
+    eng, _w, _cfg = _engine(max_batch=8)
+    rng = random.Random(7)
+    jobs = []
+    for i in range(40):
+        L = rng.choice([1, 3, 17, 44, 63, 64, 65, 130, 257, 400])
+        prompt = [rng.randrange(3, 250) for _ in range(L)]
+        n = rng.randrange(1, 61)
+        kind = rng.choice(["greedy", "greedy", "sampled", "cancel", "stream"])
+        jobs.append((prompt, n, kind, 1000 + i))
+    srv = NativeEngineServer(eng, max_batch=8, prefill_ctx=256, decode_chunk=4)
+    free0 = srv.metrics()["free_kv_pages"]
+    results = [None] * len(jobs)
+
+    def run(k):
+        for i in range(k, len(jobs), 8):  # 8 peers, 5 requests each, back to back
+            prompt, n, kind, seed = jobs[i]
+            if kind == "sampled":
+                p = SamplingParams(temperature=0.8, top_k=40, top_p=0.9, seed=seed, max_tokens=n,
+                                   stop_on_eos=False)
+            else:
+                p = SamplingParams(max_tokens=n, stop_on_eos=False)
+            try:
+                if kind == "cancel":
+                    srv.generate(prompt, p, timeout=0.002)
+                    results[i] = ("done-anyway", None)
+                elif kind == "stream":
+                    rid = srv._submit(prompt, p)
+                    got, done = [], False
+                    while not done:
+                        new, done = srv.loop.wait_tokens(rid, len(got), 5.0)
+                        got += new
+                    srv.loop.release(rid)
+                    results[i] = ("ok", got)
+                else:
+                    results[i] = ("ok", srv.generate(prompt, p)["tokens"])
+            except EngineTimeout:
+                results[i] = ("timeout", None)
+            except Exception as e:  # noqa: BLE001 -- reported below
+                results[i] = ("error", repr(e))
+
+    try:
+        ths = [threading.Thread(target=run, args=(k,)) for k in range(8)]
+        [t.start() for t in ths]
+        [t.join(timeout=300) for t in ths]
+        assert all(r is not None for r in results), "a peer hung"
+        errors = [r for r in results if r[0] == "error"]
+        assert not errors, errors[:3]
+        for _ in range(200):
+            m = srv.metrics()
+            if m["free_kv_pages"] == free0 and m["running"] == 0 and m["waiting"] == 0:
+                break
+            time.sleep(0.02)
+        assert m["free_kv_pages"] == free0 and m["running"] == 0, m
+        assert m["eager_prefill_calls"] >= 1, m  # the prompts past the graphs' context
+        for i, (prompt, n, kind, _seed) in enumerate(jobs):
+            if kind == "sampled" and results[i][0] == "ok":
+                assert len(results[i][1]) == n and all(0 <= t < 512 for t in results[i][1]), i
+    finally:
+        srv.close()
+    # greedy and streamed replies vs the static engine (after the loop is gone)
+    checked = 0
+    for i, (prompt, n, kind, _seed) in enumerate(jobs):
+        if kind in ("greedy", "stream") and results[i][0] == "ok":
+            ref = eng.generate([prompt], n, stop_on_eos=False)[0].tokens
+            assert len(results[i][1]) == n, (i, kind)
+            assert _same_or_near_tie(eng, prompt, results[i][1], ref), (i, kind)
+            checked += 1
+    assert checked >= 15
