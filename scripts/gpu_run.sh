@@ -30,14 +30,17 @@ for s in "${S[@]}"; do
              -- python3 bench.py --steps 3 --warmup 1 ;;
     serve) step serve 600 "${TAG}_serve.log" python bench/serve_bench.py ${SERVE_ARGS:-} ;;
     proxy) step proxy 600 "${TAG}_proxy.log" python bench/tp_rank_proxy.py ${PROXY_ARGS:-} ;;
-    pmc)  # PMC passes over PMC_CMD (a python3 command line), one counter set per run
+    pmc)  # PMC passes over PMC_CMD (a python3 command line), one counter set per run.  Keep
+          # the target short: counter collection serialises every kernel, and a run silent for
+          # 3 minutes is killed (the whole headline bench with its start-up autotune is too long)
+      [ -n "${PMC_CMD:-}" ] || { echo "pmc: set PMC_CMD"; exit 2; }
       i=0
       for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SALU" \
                  "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_LDS" \
                  "FETCH_SIZE TCP_TCC_READ_REQ_sum"; do
         i=$((i+1))
         step pmc$i 300 "${TAG}_pmc$i.log" rocprofv3 --pmc $set --kernel-trace -d gpurun_out/${TAG}_pmc$i -o run \
-             -- python3 ${PMC_CMD:-bench.py --steps 2 --warmup 1}
+             -- python3 $PMC_CMD
       done ;;
     cmd) step cmd ${CMD_TIMEOUT:-600} "${TAG}_cmd.log" bash -c "$CMD" ;;
     *) echo "unknown step $s"; exit 2 ;;
