@@ -78,6 +78,7 @@ LoopConfig loop_cfg(const py::dict& d) {
   c.admit_wait_us = val_of<double>(d, "admit_wait_us", 500.0);
   c.prefill_first = val_of<bool>(d, "prefill_first", true);
   c.mixed = val_of<bool>(d, "mixed", true);
+  c.riders_all = val_of<bool>(d, "riders_all", false);
   c.pipeline = val_of<bool>(d, "pipeline", true);
   c.device = val_of<int>(d, "device", 0);
   if (d.contains("batch_buckets")) c.batch_buckets = py::cast<std::vector<int>>(d["batch_buckets"]);

@@ -436,7 +436,11 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
     }
     if (cfg_.mixed) {
       // running sequences fill the chunk's last 64-row tile, never start another one
-      int room = (n_rows + 63) / 64 * 64 - n_rows;
+      // riders_all: every running sequence rides (bounded by the chunk budget) -- under high
+      // concurrency a prompt admitted alone would otherwise stall the sequences that do not
+      // fit the last tile for a whole step; else only the last 64-row tile's free rows
+      int room = cfg_.riders_all ? cfg_.max_prefill_tokens - n_rows
+                                 : (n_rows + 63) / 64 * 64 - n_rows;
       for (int64_t id : sched_.running()) {
         if (room <= 0 || (int)seqs.size() >= cfg_.max_batch) break;
         if (std::find(admitted.begin(), admitted.end(), id) != admitted.end()) continue;

@@ -89,6 +89,7 @@ struct LoopConfig {
   double admit_wait_us = 500.0;
   bool prefill_first = true;
   bool mixed = true;     // running sequences ride in a prefill chunk as one row each
+  bool riders_all = false;  // all of them (budget permitting), not just the last tile's room
   bool pipeline = true;  // enqueue decode chunk i+1 before reading chunk i
   int device = 0;
   std::vector<int> batch_buckets{1, 2, 4, 8, 16, 32, 64};

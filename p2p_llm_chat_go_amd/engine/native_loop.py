@@ -67,6 +67,10 @@ class NativeEngineServer(EngineServer):
             "admit_wait_us": float(os.environ.get("ENGINE_ADMIT_WAIT_US", "500")),
             "prefill_first": os.environ.get("ENGINE_PREFILL_FIRST", "1") != "0",
             "mixed": True, "pipeline": os.environ.get("ENGINE_PIPELINE", "1") != "0",
+            # every running sequence rides in a prompt chunk (ENGINE_RIDERS=tile: only the
+            # last 64-row tile's free rows): +4 % at 32 peers, +16 % at 64, same at 8
+            # (profiles/r4_serve_native_vs_python.jsonl)
+            "riders_all": os.environ.get("ENGINE_RIDERS", "all") == "all",
             "device": dev.index or 0, "batch_buckets": list(BATCH_BUCKETS),
             "ctx_buckets": list(CTX_BUCKETS),
             "row_buckets": [r for r in PREFILL_ROW_BUCKETS if r <= engine.max_prefill_tokens],

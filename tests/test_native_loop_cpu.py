@@ -161,14 +161,14 @@ class FakeModel:
         return [nxt(p[-1], len(p) - 1, 0 if t <= 0 else s) for p, (t, _k, _p, s) in zip(prompts, samp)]
 
 
-def make_loop(pipeline=True, max_batch=8, chunk=4, free_slots=True):
+def make_loop(pipeline=True, max_batch=8, chunk=4, free_slots=True, riders_all=False):
     N = load()
     N.loop_use_host_fake_hip()
     model = FakeModel(prefill_pages=4)
     loop = N.EngineLoop({"num_pages": 256, "max_batch": max_batch, "max_prefill_tokens": 256,
                          "max_ctx": 2048, "eos": [EOS], "decode_chunk": chunk,
                          "admit_wait_us": 200.0, "pipeline": pipeline,
-                         "pipeline_free_slots": free_slots,
+                         "pipeline_free_slots": free_slots, "riders_all": riders_all,
                          "row_buckets": [16, 32, 48, 64, 96, 128, 192, 256],
                          "prefill_max_pages": 4})
     model.loop = loop
@@ -187,9 +187,9 @@ def _wait_idle(loop, pages=255):
     return loop.metrics()
 
 
-@pytest.mark.parametrize("pipeline", [True, False])
-def test_loop_concurrent_requests_match_model(pipeline):
-    loop, model = make_loop(pipeline=pipeline)
+@pytest.mark.parametrize("pipeline,riders_all", [(True, False), (False, False), (True, True)])
+def test_loop_concurrent_requests_match_model(pipeline, riders_all):
+    loop, model = make_loop(pipeline=pipeline, riders_all=riders_all)
     rng = random.Random(3)
     reqs = []
     for i in range(24):
