@@ -68,6 +68,9 @@ class EngineServer:
         # a prefill step also advances every running sequence by one token (its row rides
         # in the prefill batch): admissions no longer stall the running batch for a step
         self.mixed = mixed
+        # every running sequence rides in a prompt chunk ("all", budget permitting) or only
+        # the chunk's last 64-row tile's free rows ("tile"): ENGINE_RIDERS (engine/native_loop)
+        self.riders_all = os.environ.get("ENGINE_RIDERS", "all") == "all"
         # after a reply finishes, wait up to this long for the next request before the next
         # step (closed-loop peers resubmit at once; a free slot left for a whole decode
         # chunk costs batch occupancy): ENGINE_ADMIT_WAIT_US, default 500 us
@@ -356,9 +359,12 @@ class EngineServer:
             prompts = [self._reqs[i]["prompt"] for i in plan.prefill]
             pages = [list(self.sched.get(i).pages) for i in plan.prefill]
             ride = [i for i in plan.decode if self.sched.get(i).state == 1] if self.mixed else []
-            # riders fill the prefill's last 64-row GEMM tile, never start another one
+            # riders: every running sequence (within the chunk budget), or only the rows left
+            # in the prefill's last 64-row GEMM tile
             n_rows = sum(len(p) for p in prompts)
-            ride = ride[:max(0, -(-n_rows // 64) * 64 - n_rows)]
+            room = (eng.max_prefill_tokens - n_rows if self.riders_all
+                    else -(-n_rows // 64) * 64 - n_rows)
+            ride = ride[:max(0, room)]
             starts = [0] * len(prompts)
             for i in ride:  # running sequences: one decode row each (last token at r.pos)
                 r = self.sched.get(i)
