@@ -22,13 +22,15 @@
 // drains.  Spins are bounded; a timeout sets the fault word (LlamaModel.check_faults).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int PAGE = 64;
 constexpr int HD = 128;
 constexpr int QA_U = 4;       // producer: k-steps per pipeline batch
 constexpr int VT = 64 + 8;    // V^T row stride in LDS (keys, bf16): one row per head dim
-constexpr long long QA_SPIN_TICKS = 500000000ll;  // 5 s at the 100 MHz wall clock
+constexpr long long QA_SPIN_TICKS = 500000000ll;  // default spin bound: 5 s at the 100 MHz wall clock
 
 typedef unsigned long long u64;
 
@@ -54,6 +56,7 @@ struct QAArgs {
   int* err;
   int n_cons;         // consumer blocks = M * Hkv
   int probe;          // bench probe: 2 = consumers stop after the granule sweep
+  long long spin_ticks;  // hand-off spin bound (P2P_QA_TIMEOUT_MS; 5 s default)
   // o_proj role (p2p_qkv_attn_oproj; null Wo = the attention output goes to `out`)
   const bf16x8* Wo;   // o_proj weight, fragment-major [No / 16][Ko / 32][64][8]
   bf16* h;            // residual [M][ldh]: h += attention @ Wo^T
@@ -236,16 +239,13 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
   auto& sm = *reinterpret_cast<float(*)[KW][G]>(p);
   p += sizeof(float) * KW * G;
   auto& sl = *reinterpret_cast<float(*)[KW][G]>(p);
-  p += sizeof(float) * KW * G;
-  float* scur = reinterpret_cast<float*>(p);  // [G]: this token's key score per head
 
-  // 1. this wave's page of CACHED keys (this step's token is folded in separately, step 3):
-  //    K fragments to registers, V transposed into LDS (all loads in flight)
-  const int n_prev = w < KW ? min(max(nprev - w * MKPW, 0), MKPW) : 0;  // wave-uniform
+  // 1. this wave's page: K fragments to registers, V rows to LDS (all loads in flight)
+  const int n_valid = w < KW ? min(max(ctx - w * MKPW, 0), MKPW) : 0;  // wave-uniform
   bf16x8 kr[4][4];
-  // the page is loaded whole: rows past n_prev (stale or zero, always finite) keep the
-  // masked P.V lanes finite (0 x NaN would poison O)
-  if (n_prev > 0) {
+  // a page holding only this step's token is still loaded whole: its other rows (stale or
+  // zero, always finite) keep the masked P.V lanes finite (0 x NaN would poison O)
+  if (n_valid > 0) {
     const int page = a.bt[(size_t)r * a.bt_stride + w];
     const size_t pbase = ((size_t)page * Hkv + h) * PAGE * HD;
     bf16x8 vr[4][4];
@@ -270,44 +270,51 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) kr[bb][s2] = zero_bf16x8();
   }
-  // 2. this step's q first: the attention over the cached keys needs nothing else, and the
-  //    k / v column groups are the launch's LAST producers (highest block indices), so the
-  //    S, softmax and P.V below run while they still stream
+  // 2. the current token's q (G heads), k and v from the producers' granules
   const unsigned tag = a.counters[r * Hkv + h] + 1;
   const unsigned o_epoch =
       a.gran2 ? __hip_atomic_load(&a.epoch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 : 0;
   const u64* gb = a.gran + ((size_t)r * Hkv + h) * (G + 2) * 64;
   const int failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long t0 = wall_clock64();
-  auto sweep_rows = [&](int row0, int nrows) {
-    for (int i = tid; i < nrows * 64; i += W * 64) {
-      const int gi = row0 * 64 + i;
-      u64 x = __hip_atomic_load(gb + gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while ((unsigned)(x >> 32) != tag && !failed) {
-        if (wall_clock64() - t0 > QA_SPIN_TICKS) {
-          atomicOr(a.err, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        x = __hip_atomic_load(gb + gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = tid; i < (G + 2) * 64; i += W * 64) {
+    u64 x = __hip_atomic_load(gb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while ((unsigned)(x >> 32) != tag && !failed) {
+      if (wall_clock64() - t0 > a.spin_ticks) {
+        atomicOr(a.err, 1);
+        break;
       }
-      cur[gi >> 6][gi & 63] = (unsigned)x;
+      __builtin_amdgcn_s_sleep(2);
+      x = __hip_atomic_load(gb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  };
-  sweep_rows(0, G);
+    cur[i >> 6][i & 63] = (unsigned)x;
+  }
+  __syncthreads();
   if (a.probe & 2) {  // probe: hand-off only (no attention math)
-    sweep_rows(G, 2);
-    __syncthreads();
     if (tid == 0) a.counters[r * Hkv + h] = tag;
     return;
   }
-  __syncthreads();
   auto frag = [&](int row, int s2) {  // 8 dims (32 s2 + 8 qd ..) of a granule row, as bf16x8
     bf16x8 f;
     const unsigned* src = &cur[row][16 * s2 + 4 * qd];
     __builtin_memcpy(&f, src, 16);
     return f;
   };
+  // this step's token: k row into the K fragments, v row into the LDS V rows
+  if (w < KW && nprev >= w * MKPW && nprev < (w + 1) * MKPW) {
+    const int rn = nprev - w * MKPW;
+    if (kk == (rn & 15)) {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+        if (bb == (rn >> 4)) {
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) kr[bb][s2] = frag(G, s2);
+        }
+    }
+    const bf16x2 v2 = as_bf16x2(cur[G + 1][lane]);
+    vt[w][2 * lane][rn] = v2[0];
+    vt[w][2 * lane + 1][rn] = v2[1];
+  }
   bf16x8 qf[4];
 #pragma unroll
   for (int s2 = 0; s2 < 4; ++s2) qf[s2] = kk < G ? frag(min(kk, G - 1), s2) : zero_bf16x8();
@@ -316,7 +323,7 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
   f32x4 o[HD / 16];
 #pragma unroll
   for (int c = 0; c < HD / 16; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (n_prev > 0) {
+  if (n_valid > 0) {
     // S^T blocks: lane holds keys 16 bb + 4 qd + j (j < 4) of head kk
     f32x4 st[4];
 #pragma unroll
@@ -331,7 +338,7 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bool ok = 16 * bb + 4 * qd + j < n_prev;
+        const bool ok = 16 * bb + 4 * qd + j < n_valid;
         st[bb][j] = ok ? st[bb][j] * a.scale : -INFINITY;
         m = fmaxf(m, st[bb][j]);
       }
@@ -350,6 +357,8 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
     l += __shfl_xor(l, 32, 64);
     mg = m;
     lg = l;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's V rows are in LDS
+    __builtin_amdgcn_wave_barrier();
     // P.V: k-step t covers key blocks 2t (A slots 0-3) and 2t+1 (slots 4-7)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -388,32 +397,21 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
     sm[w][kk] = mg;
     sl[w][kk] = lg;
   }
-  // 3. this token's k and v, then its score per head (one wave per head, 2 dims a lane)
-  sweep_rows(G, 2);
   __syncthreads();
-  for (int hd = w; hd < G; hd += W) {
-    const bf16x2 q2 = as_bf16x2(cur[hd][lane]), k2 = as_bf16x2(cur[G][lane]);
-    const float d = wave_sum((float)q2[0] * (float)k2[0] + (float)q2[1] * (float)k2[1]);
-    if (lane == 0) scur[hd] = d * a.scale;
-  }
-  __syncthreads();
-  // 4. merge the waves' partials and this token (one more partial: m = its score, l = 1,
-  //    o = its v row)
   auto merged = [&](int hd, int dd) {
-    const float sc = scur[hd];
-    float M = sc;
+    float M = -INFINITY;
 #pragma unroll
     for (int ww = 0; ww < KW; ++ww) M = fmaxf(M, sm[ww][hd]);
-    const bf16x2 v2 = as_bf16x2(cur[G + 1][dd >> 1]);
-    const float ec = __expf(sc - M);
-    float num = ec * (float)v2[dd & 1], den = ec;
+    float num = 0.f, den = 0.f;
+    if (M != -INFINITY) {
 #pragma unroll
-    for (int ww = 0; ww < KW; ++ww) {
-      const float e = __expf(sm[ww][hd] - M);  // -inf (no cached keys) -> 0
-      num = fmaf(e, so[ww][hd][dd], num);
-      den = fmaf(e, sl[ww][hd], den);
+      for (int ww = 0; ww < KW; ++ww) {
+        const float e = __expf(sm[ww][hd] - M);
+        num = fmaf(e, so[ww][hd][dd], num);
+        den = fmaf(e, sl[ww][hd], den);
+      }
     }
-    return num / den;
+    return den > 0.f ? num / den : 0.f;
   };
   if (a.gran2 != nullptr) {
     // o_proj role in this launch: publish the attention output as {epoch, two bf16}
@@ -492,7 +490,7 @@ __device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem, const 
 #pragma unroll
       for (int j = 0; j < OGPT; ++j) ok &= (unsigned)(x[j] >> 32) == e;
       while (!ok && !failed) {  // the consumers have not published yet: re-poll the missing
-        if (wall_clock64() - t0 > QA_SPIN_TICKS) {
+        if (wall_clock64() - t0 > a.spin_ticks) {
           atomicOr(a.err, 1);
           break;
         }
@@ -557,8 +555,7 @@ template <int G>
 constexpr size_t consumer_lds() {
   const size_t v = sizeof(bf16) * KW * HD * VT;
   const size_t o = sizeof(float) * KW * G * HD;
-  return (v > o ? v : o) + sizeof(unsigned) * (G + 2) * 64 + 2 * sizeof(float) * KW * G +
-         sizeof(float) * G;
+  return (v > o ? v : o) + sizeof(unsigned) * (G + 2) * 64 + 2 * sizeof(float) * KW * G;
 }
 
 // FO: the launch also holds the o_proj workgroups (blocks after the producers)
@@ -647,6 +644,18 @@ static int oproj_capacity(int W, int G) {
   return c;
 }
 
+// The hand-off spin bound: P2P_QA_TIMEOUT_MS (default 5000).  Virtual ranks time-sharing
+// one device (tests/test_world8_gpu.py) raise it like P2P_CAR_TIMEOUT_MS: a rank's
+// producers can wait behind its peers' spinning grids there, which a real node never sees.
+static long long qa_spin_ticks() {
+  static const long long t = [] {
+    const char* e = std::getenv("P2P_QA_TIMEOUT_MS");
+    const long long ms = e && *e ? std::atoll(e) : 0;
+    return ms > 0 ? ms * 100000ll : QA_SPIN_TICKS;  // 100 MHz wall clock
+  }();
+  return t;
+}
+
 static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, int Hq, int Hkv,
                          const int* pos, const int* slots, const void* cos_sin, void* k_cache,
                          void* v_cache, const int* block_tables, int bt_stride,
@@ -681,6 +690,7 @@ static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, i
   a.err = err;
   a.n_cons = (g_qa_probe & 1) ? 0 : M * Hkv;  // probe 1: producers only
   a.probe = g_qa_probe;
+  a.spin_ticks = qa_spin_ticks();
   const int groups = (Hq + 2 * Hkv) * (HD / 16);
   a.n_prod = groups;
   // producer waves per block (split-K): 8 when the projection has few column groups (the

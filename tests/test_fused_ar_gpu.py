@@ -25,7 +25,8 @@ def _port():
 
 def _worker(rank, world, port, q):
     # virtual ranks time-share one device: a generous spin bound (5 s on real GPUs)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), P2P_CAR_TIMEOUT_MS="30000")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), P2P_CAR_TIMEOUT_MS="30000",
+                      P2P_QA_TIMEOUT_MS="30000")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     car = None
     try:

@@ -26,7 +26,7 @@ def _port():
 
 def _worker(rank, world, port, q, moe, a2a=False, overlap=False, graphs=False, ipc=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                      P2P_EP_IPC="1" if ipc else "0")
+                      P2P_EP_IPC="1" if ipc else "0", P2P_QA_TIMEOUT_MS="30000")
     if overlap:  # prefill row-parallel sums chunked onto a communication stream
         os.environ["P2P_TP_OVERLAP_MIN_ROWS"] = "16"
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -58,9 +58,10 @@ def _check_logits(got, ref, what):
 
 def _worker(rank, world, port, q, kind, mode, env):
     # 8 processes time-share one device: a rank's kernel can wait on a peer whose queue is
-    # not scheduled yet, so the spin bound is generous here (5 s on real GPUs)
+    # not scheduled yet, so the spin bounds (all-reduce, fused qkv+attention hand-off) are
+    # generous here (5 s on real GPUs)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), P2P_CAR_TIMEOUT_MS="30000",
-                      **env)
+                      P2P_QA_TIMEOUT_MS="30000", **env)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     WORLD = world
     try:
@@ -88,6 +89,8 @@ def _worker(rank, world, port, q, kind, mode, env):
                      ep_mode=mode if moe else "allreduce")
         prompts = _prompts(rank, per_rank=(mode == "a2a"))
         n_new = 8
+        torch.cuda.synchronize()
+        dist.barrier()  # every rank built (rank 0 also holds the TP=1 weights) before decoding
         res = eng.generate(prompts, n_new, stop_on_eos=False)
         toks = [r.tokens for r in res]
         gs = list(eng._graphs.values())
@@ -143,16 +146,18 @@ def _worker(rank, world, port, q, kind, mode, env):
         dist.destroy_process_group()
 
 
-# Fused all-reduce epilogue (default) and the unfused pair.  The fused GEMM's workgroups
-# wait in place for the same workgroup of every peer: on 8 GPUs each device runs only its
-# own grid and in-order dispatch guarantees progress, but 8 virtual ranks on ONE device
-# with 4-wave workgroups (8 x 256 x 4 waves) can fill every wave slot with waiters and
-# starve the rank they wait for (a deadlock until the spin bound, seen on the box).  The
-# tests therefore cap the fused workgroups' split-K waves (P2P_FAR_MAX_WAVES) so all ranks'
-# grids fit the device at once; the numerics and the protocol are unchanged.
+# Fused all-reduce epilogue (default) at TP=4 and the unfused pair at TP=8.  The fused
+# GEMM's workgroups wait in place for the same workgroup of every peer: on 8 GPUs each
+# device runs only its own grid and in-order dispatch guarantees progress, but virtual
+# ranks on ONE device share its wave slots and LDS, so ranks whose grids are already
+# spinning can keep a late rank's earlier kernels from being scheduled at all (a deadlock
+# until the spin bound).  At 4 ranks with the split-K waves capped (P2P_FAR_MAX_WAVES) every
+# rank's grid fits; at 8 ranks it held only when the ranks happened to run in step (a warm
+# box) and timed out whenever one rank started late (round 4: 5 of 5 runs on fresh boxes),
+# so the 8-rank fused epilogue is covered bit-exactly by test_fused_ar_gpu.py (world 8, one
+# launch per rank in lockstep) and here the 8-rank engine runs the unfused pair.
 @pytest.mark.parametrize("kind,mode,world,env", [
-    ("dense", "tp", 8, {"P2P_FAR_MAX_WAVES": "1"}), ("dense", "tp", 8, {"P2P_TP_FUSED_AR": "0"}),
-    ("dense", "tp", 4, {"P2P_FAR_MAX_WAVES": "2"}),
+    ("dense", "tp", 8, {"P2P_TP_FUSED_AR": "0"}), ("dense", "tp", 4, {"P2P_FAR_MAX_WAVES": "2"}),
     ("moe", "allreduce", 8, {}), ("moe", "a2a", 8, {})])
 def test_world8_virtual_ranks_full_width(kind, mode, world, env):
     ctx = mp.get_context("spawn")
@@ -168,6 +173,9 @@ def test_world8_virtual_ranks_full_width(kind, mode, world, env):
     finally:
         [p.join(timeout=30) for p in ps]
         [p.terminate() for p in ps if p.is_alive()]
+    for rank, ok, info in sorted(res):
+        if not ok:
+            print("rank %d failed:\n%s" % (rank, info))
     for rank, ok, info in sorted(res):
         assert ok, (rank, info)
     print([info for rank, _, info in res if rank == 0][0])
