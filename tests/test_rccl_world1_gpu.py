@@ -101,4 +101,7 @@ def test_tpcomm_rccl_paths_world1():
                RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, "-c", SCRIPT], env=env, stdout=subprocess.PIPE,
                        stderr=subprocess.PIPE, text=True, timeout=240, cwd=ROOT)
+    if r.returncode != 0:
+        print(r.stdout[-3000:])
+        print(r.stderr[-8000:])
     assert r.returncode == 0 and "RCCL_WORLD1_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
