@@ -37,7 +37,9 @@ def _graph_time(fn, reps=3):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    # thread_local, as the engine's captures: in a TP group the RCCL watchdog thread polls
+    # its work events meanwhile, which the default global mode turns into a capture error
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         fn()
     g.replay()
     torch.cuda.synchronize()

@@ -65,7 +65,7 @@ def _worker(port, q):
         with torch.cuda.stream(s):
             comm.allreduce_add_(hg, pg)  # warm the communicator outside capture
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=s):
+            with torch.cuda.graph(graph, stream=s, capture_error_mode="thread_local"):
                 comm.allreduce_add_(hg, pg)
         torch.cuda.synchronize()
         for _ in range(3):

@@ -76,7 +76,11 @@ SCRIPT = textwrap.dedent(r"""
         comm.allreduce_(buf)  # warm the communicator outside capture
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    # thread_local as the engine captures (engine/graph.py): under the default global mode
+    # the process group's watchdog thread, polling the warm-up call's event during the
+    # capture, is an illegal call and aborts the process (the likely cause of one abort of
+    # this test on the box)
+    with torch.cuda.graph(graph, capture_error_mode="thread_local"):
         comm.allreduce_(buf)
         buf.mul_(2)
     for _ in range(3):
