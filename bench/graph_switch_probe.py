@@ -99,6 +99,14 @@ def main():
         "after_decode_then_one_node_graph": replay_only(lambda: (decode(cur), tiny.replay())),
         "after_decode_then_one_kernel": replay_only(lambda: (decode(cur), buf.add_(1)))}}),
           flush=True)
+    def decode_k(k):
+        g.state.load([1], [len(prompts[0])], pages)
+        g.replay(k)
+        g.state.hist[:1, :1].cpu()
+        torch.cuda.synchronize()
+
+    print(json.dumps({"replay_only_enqueue_ms_p50_after_k_decode_steps": {
+        str(k): replay_only(lambda k=k: decode_k(k)) for k in (1, 4, 16, 63)}}), flush=True)
     absorb = []
     for _ in range(a.iters):
         decode(cur)

@@ -14,6 +14,8 @@ replay.  Padding rows of a bucket stay on the null page.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -129,6 +131,12 @@ class DecodeGraph:
         self.graph = None
         self.greedy = greedy
         self.use_graph = use_graph and state.model.device.type == "cuda"
+        # multi-step graph (see _capture_steps): single-device engines only -- a TP / EP
+        # group would have to capture it collectively
+        comm = getattr(state.model, "comm", None)
+        solo = getattr(comm, "world", 1) <= 1
+        self.k_steps = int(os.environ.get("P2P_DECODE_GRAPH_STEPS", "8")) if solo else 1
+        self.graph_k = None
 
     def _body(self):
         if self.greedy:
@@ -179,13 +187,42 @@ class DecodeGraph:
         self.graph = g
         return self
 
+    def _capture_steps(self):
+        """The greedy step captured K times in ONE graph (P2P_DECODE_GRAPH_STEPS, default 8;
+        single-device engines).  Measured (bench/graph_switch_probe.py,
+        profiles/r4_graph_switch_probe.jsonl): every launch of the one-step graph leaves
+        ~8 us of host work that the NEXT launch of a different graph (the prompt chunk)
+        pays, 0.5 ms after a 63-step reply -- on the next request's TTFT.  K steps per
+        launch cut the launches K-fold.  Capture only records (nothing runs), so the
+        loaded batch state is untouched."""
+        st = self.state
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for _ in range(self.k_steps):
+                    self._body()
+        except Exception:  # noqa: BLE001 -- keep the one-step graph
+            torch.cuda.synchronize(st.model.device)
+            self.graph_k = False
+            return
+        self.graph_k = g
+
     def replay(self, n: int = 1):
         assert self.greedy
-        for _ in range(n):
-            if self.graph is not None:
-                self.graph.replay()
-            else:
+        if self.graph is None:
+            for _ in range(n):
                 self.state.body()
+            return
+        K = self.k_steps
+        if n >= K > 1 and self.graph_k is not False:
+            if self.graph_k is None:
+                self._capture_steps()
+            if self.graph_k:
+                while n >= K:
+                    self.graph_k.replay()
+                    n -= K
+        for _ in range(n):
+            self.graph.replay()
 
     def describe(self) -> dict:
         """Addresses and layout for the native loop (runtime/engine_loop.h DecodeGraphDesc)."""
