@@ -116,6 +116,8 @@ void bind_engine_loop(py::module_& m) {
              g.topp = ptr_of<float>(d, "topp");
              g.seeds = ptr_of<int64_t>(d, "seeds");
              g.err = ptr_of<int32_t>(d, "err");
+             g.exec_k = ptr_of<void>(d, "exec_k");
+             g.k_steps = val_of<int>(d, "k_steps", 0);
              if (!g.exec || !g.meta || !g.hist || !g.step || g.B <= 0 || g.max_steps <= 0 ||
                  (!g.greedy && !(g.temp && g.topk && g.topp && g.seeds)))
                throw std::runtime_error("add_decode_graph: incomplete description");

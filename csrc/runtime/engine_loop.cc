@@ -653,7 +653,13 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
     loaded_steps_ = 0;
     n_loads_++;
   }
-  for (int i = 0; i < k; ++i) hip_check(h.graphLaunch(g->exec, stream_), "decode graph launch");
+  // k steps: whole k_steps-step graphs first (each one-step launch leaves host work that
+  // the next launch of the prompt-chunk graph pays: ~8 us per launch, bench/graph_switch_probe.py)
+  int left = k;
+  if (g->exec_k && g->k_steps > 1)
+    for (; left >= g->k_steps; left -= g->k_steps)
+      hip_check(h.graphLaunch(g->exec_k, stream_), "decode graph launch");
+  for (; left > 0; --left) hip_check(h.graphLaunch(g->exec, stream_), "decode graph launch");
   Chunk c;
   c.g = g;
   c.ids = ids;

@@ -62,6 +62,8 @@ struct DecodeGraphDesc {
   float* topp = nullptr;
   int64_t* seeds = nullptr;
   int32_t* err = nullptr;       // the graph workspace's fault word (nonzero = invalid results)
+  void* exec_k = nullptr;       // optional: k_steps decode steps in one graph (greedy)
+  int k_steps = 0;
 };
 
 // PrefillGraph (engine/graph.py) of one captured prefill chunk.

@@ -232,6 +232,8 @@ class DecodeGraph:
              "hist": st.hist.data_ptr(), "max_steps": st.max_steps, "step": st.step.data_ptr(),
              "keys": st.ws.keys.data_ptr(), "keys_bytes": st.ws.keys.numel() * 8,
              "err": st.ws.err.data_ptr()}
+        if self.graph_k:
+            d.update(exec_k=self.graph_k.raw_cuda_graph_exec(), k_steps=self.k_steps)
         if not self.greedy:
             sp = st.samp
             d.update(temp=sp.temp.data_ptr(), topk=sp.topk.data_ptr(), topp=sp.topp.data_ptr(),

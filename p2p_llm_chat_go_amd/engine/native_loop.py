@@ -92,6 +92,8 @@ class NativeEngineServer(EngineServer):
             return
         if kind == "decode":
             g = eng.decode_graph(a, b, greedy=greedy)
+            if greedy and g.graph is not None and g.k_steps > 1 and g.graph_k is None:
+                g._capture_steps()  # the loop launches whole k-step graphs first
             self.loop.add_decode_graph(g.describe())
         else:
             # (the loop asks only for shapes that recur: prefill_graph_after)
