@@ -34,6 +34,15 @@
 
 namespace wide {
 
+#ifdef WIDE_STAMP
+// probe builds only (csrc/experimental/wide_stamp.hip): per-block wall-clock stamps
+// [entry, first chunk ready, main loop done, slabs drained, slices met, end, tile, split]
+__device__ long long* wide_stamp_buf;
+#define WSTAMP(i, v) do { if (wide_stamp_buf && threadIdx.x == 0) wide_stamp_buf[(size_t)blockIdx.x * 8 + (i)] = (v); } while (0)
+#else
+#define WSTAMP(i, v) do { } while (0)
+#endif
+
 constexpr int NT = 512;   // 8 waves
 constexpr int KC = 8;     // k-steps per chunk: wave w DMA-loads k-step w of every m-tile
 constexpr int MAX_SPLIT = 16;  // K slices per tile (the rstd reduction unrolls over them)
@@ -80,6 +89,9 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   const int nc_all = S / KC;
   const int c0 = split * nc_all / splitk, c1 = (split + 1) * nc_all / splitk;
   const int n = c1 - c0;
+  WSTAMP(0, wall_clock64());
+  WSTAMP(6, tile);
+  WSTAMP(7, split);
 
   const int gw = SILU ? (w < 4 ? tile * 4 + w : tile * 4 + (w - 4) + up_off) : tile * 8 + w;
   const bf16x8* wsrc = Wt + (size_t)gw * S * 64 + lane;
@@ -162,11 +174,13 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       if (!RES || t == 0) {  // RES: chunk 0's weights landed => this wave's DMA parts too
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        if (t == 0) WSTAMP(1, wall_clock64());
       }
       compute(c0 + t, wr[j]);
     }
   }
 
+  WSTAMP(2, wall_clock64());
   // ---- this slice's row sums of squares: wave pair (w, w ^ 4) holds m-tile w & 3 ----
   if constexpr (NORM) {
     ss += __shfl_xor(ss, 16, 64);
@@ -264,6 +278,10 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       const int rr = 4 * q + j;
       return rstd_from(ss_l[0][i][rr] + ss_l[1][i][rr]);
     });
+#ifdef WIDE_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    WSTAMP(5, wall_clock64());
     return;
   } else {
     // ---- parallel split-K: write-through slabs [tile][split][wave][MT] (f32x4 per lane) ----
@@ -284,6 +302,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    WSTAMP(3, wall_clock64());
     if (tid == 0) {
       const unsigned g0 = __hip_atomic_load(&sp.gen[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // read the generation BEFORE arriving
@@ -305,6 +324,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       }
     }
     __syncthreads();
+    WSTAMP(4, wall_clock64());
     // every slice's partials are visible.  Rows' rstd: one lane per row sums the slices'
     // row sums (all loads issued before the first add) into LDS
     __shared__ float rstd_l[64];
@@ -357,6 +377,10 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       if constexpr (!NORM) return 1.f;
       return rstd_l[16 * i + 4 * q + j];
     });
+#ifdef WIDE_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    WSTAMP(5, wall_clock64());
   }
 }
 
@@ -481,3 +505,9 @@ P2P_API void p2p_wide_resident(int on) { wide::g_res = on ? 1 : 0; }
 P2P_API void p2p_wide_max_split(int s) {
   wide::g_max_split = (s >= 1 && s <= wide::MAX_SPLIT) ? s : wide::MAX_SPLIT;
 }
+
+#ifdef WIDE_STAMP
+P2P_API int p2p_wide_stamp_set(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(wide::wide_stamp_buf), &p, sizeof(p));
+}
+#endif

@@ -161,6 +161,13 @@ int64_t EngineLoop::submit(const std::vector<int>& prompt, int max_new, bool sto
                            const LoopSampling& s) {
   std::lock_guard<std::mutex> lk(mu_);
   if (!dead_.empty()) throw std::runtime_error("engine replica is down: " + dead_);
+  // decode graphs are picked with slack for chunks that run past a reply's end (pick() in
+  // decode): a request whose prompt + max_new + slack exceeds the largest context bucket is
+  // refused here, alone, instead of failing every running request later
+  if (!cfg_.ctx_buckets.empty() &&
+      (int64_t)prompt.size() + max_new + 2 * cfg_.decode_chunk + 2 > cfg_.ctx_buckets.back())
+    throw std::invalid_argument("prompt + max_new exceeds the largest context bucket (" +
+                                std::to_string(cfg_.ctx_buckets.back()) + " tokens)");
   const int64_t id = sched_.add((int)prompt.size(), max_new, stop_on_eos, cfg_.eos);
   Req& r = reqs_[id];
   r.prompt = prompt;
@@ -190,6 +197,10 @@ bool EngineLoop::wait(int64_t id, double timeout_s, LoopResult* out) {
   out->tokens = s.tokens;
   out->done = r.done;
   out->error = r.error;
+  if (!r.done && (!dead_.empty() || stop_)) {  // nobody will finish it: report why now
+    out->done = true;
+    out->error = "engine replica is down: " + (dead_.empty() ? std::string("loop stopped") : dead_);
+  }
   out->done_reason = s.finish_reason.empty() ? (r.done ? "stop" : "") : s.finish_reason;
   out->prompt_eval_count = s.prompt_len;
   const int64_t t_first = r.t_first ? r.t_first : now_ns();
@@ -210,7 +221,7 @@ std::vector<int> EngineLoop::wait_tokens(int64_t id, size_t have, double timeout
   };
   done_cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.0, timeout_s)), ready);
   const auto& toks = sched_.get(id).tokens;
-  *done = it->second.done;
+  *done = it->second.done || !dead_.empty() || stop_;  // a dead loop finishes nothing more
   if (toks.size() <= have) return {};
   return std::vector<int>(toks.begin() + have, toks.end());
 }
@@ -446,6 +457,9 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
         if (std::find(admitted.begin(), admitted.end(), id) != admitted.end()) continue;
         const SchedRequest& r = sched_.get(id);
         if (r.state != RUNNING || r.tokens.empty()) continue;
+        // a rider past the prefill graphs' block-table width would send the whole chunk
+        // down the eager path: it decodes in the next step instead
+        if (r.pos / 64 + 1 > cfg_.prefill_max_pages) continue;
         Seq s;
         s.id = id;
         s.prompt = nullptr;
@@ -568,7 +582,7 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
     int32_t* ew = (int32_t*)pinned(kErr0 + 2, 4);
     if (g->err) hip_check(h.memcpyAsync(ew, g->err, 4, kD2H, stream_), "fault word D2H");
     hip_check(h.streamSynchronize(stream_), "prefill sync");
-    if (g->err && *ew != 0) throw std::runtime_error("kernel fault word set during prefill");
+    if (g->err && *ew != 0) on_fault(g->err, "prefill");
     for (int b = 0; b < nseq; ++b) first[b] = f[b];
   }
   const int64_t t1 = now_ns();
@@ -687,8 +701,11 @@ void EngineLoop::collect() {
   Chunk c = std::move(flight_.front());
   flight_.pop_front();
   hip_check(h.eventSynchronize(c.ev), "decode chunk sync");
-  if (c.g->err && *(int32_t*)pinned_[kErr0 + c.buf].first != 0)
-    throw std::runtime_error("kernel fault word set during decode (results invalid)");
+  if (c.g->err && *(int32_t*)pinned_[kErr0 + c.buf].first != 0) {
+    flight_.clear();  // chunks behind a faulted one ran on its invalid state
+    on_fault(c.g->err, "decode");
+  }
+  faults_in_row_ = 0;  // a clean decode chunk: whatever faulted before was transient
   const int32_t* hist = (const int32_t*)pinned_[kHist0 + c.buf].first;
   std::vector<std::vector<int>> toks(c.ids.size());
   for (size_t b = 0; b < c.ids.size(); ++b) {
@@ -702,6 +719,25 @@ void EngineLoop::collect() {
     if (flight_.empty()) sched_.flush_deferred();  // nothing in flight can touch them now
   }
   done_cv_.notify_all();
+}
+
+// A kernel's fault word was set (a bounded spin gave up: a split-K slice or a hand-off
+// that never arrived).  The word is cleared -- the Python path does the same in
+// check_faults -- so one transient timeout fails only the requests in this step;
+// kMaxFaultsInRow faulted steps in a row mark the replica dead, and the router stops
+// sending it traffic.
+void EngineLoop::on_fault(int32_t* err, const char* where) {
+  const HipApi& h = hip_api();
+  (void)h.memsetAsync(err, 0, 4, stream_);
+  (void)h.streamSynchronize(stream_);
+  loaded_ = nullptr;
+  const std::string why = std::string("kernel fault word set during ") + where +
+                          " (results invalid)";
+  if (++faults_in_row_ >= kMaxFaultsInRow) {
+    std::lock_guard<std::mutex> lk(mu_);
+    dead_ = why + ", " + std::to_string(faults_in_row_) + " steps in a row";
+  }
+  throw std::runtime_error(why);
 }
 
 void EngineLoop::drain() {

@@ -170,6 +170,7 @@ class EngineLoop {
   void collect();  // read the oldest chunk in flight
   void drain();    // read every chunk in flight
   void fail_all(const std::string& why);
+  [[noreturn]] void on_fault(int32_t* err, const char* where);
   const DecodeGraphDesc* decode_graph(int B, int ctx, bool greedy);
   const PrefillGraphDesc* find_prefill_graph(int rows, int nseq, bool greedy);
   const PrefillGraphDesc* prefill_graph(int rows, int nseq, bool greedy);
@@ -207,6 +208,8 @@ class EngineLoop {
   std::vector<int64_t> loaded_ids_;
   int loaded_steps_ = 0;                          // replays since the last load
   int hist_buf_ = 0;
+  static constexpr int kMaxFaultsInRow = 3;
+  int faults_in_row_ = 0;  // consecutive steps that ended with a kernel fault word set
 
   // metrics
   std::atomic<long> n_requests_{0}, n_tokens_{0}, n_prefill_calls_{0}, n_decode_calls_{0},

@@ -322,12 +322,16 @@ class PrefillGraph:
         v = {name: host[a:a + k] for name, (a, k) in self.offsets.items()}
         bt = v["bt"].reshape(S + 1, P)
         for s, pages in enumerate(block_tables):
-            assert len(pages) <= P, (len(pages), P)
+            # callers pass a sequence's whole allocation (prompt + max_new pages); the chunk
+            # reads only the pages of its context bucket, so the rest is cut off here (the
+            # native loop does the same, runtime/engine_loop.cc)
+            pages = pages[:P]
             bt[s, :len(pages)] = pages
         seq, pos = v["seq"], v["pos"]
         if n:
             a = np.asarray(rows, dtype=np.int32).reshape(n, 3)
             seq[:n], pos[:n], v["ids"][:n] = a[:, 0], a[:, 1], a[:, 2]
+            assert int(a[:, 1].max()) < P * PAGE, (int(a[:, 1].max()), P)
         seq[n:] = S  # dummy rows: sequence S (the null page), positions 0.. wrapped inside
         pos[n:] = np.arange(R - n, dtype=np.int32) % (P * PAGE)  # its block-table row
         slots = bt[seq, pos // PAGE] * PAGE + pos % PAGE

@@ -30,9 +30,14 @@ class TPComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        # P2P_CUSTOM_AR: 1 (default) IPC kernels, a failed peer-access preflight raises;
+        # auto: the same, but a failed preflight falls back to RCCL; 0: RCCL only
+        mode = os.environ.get("P2P_CUSTOM_AR", "1")
         if custom_ar is None:
-            custom_ar = os.environ.get("P2P_CUSTOM_AR", "1") == "1"
+            custom_ar = mode in ("1", "auto")
         self.want_custom_ar = custom_ar
+        self.car_fallback = mode == "auto"
+        self.peer_failures = []
         # one-/two-shot kernels cover sums up to this size (70B: every row-parallel sum
         # below the overlapped-RCCL threshold of 256 rows); larger ones use RCCL
         if car_max_bytes is None:
@@ -49,8 +54,20 @@ class TPComm:
         device = torch.device(device)
         if (self.want_custom_ar and device.type == "cuda" and self.car is None
                 and (self.world > 1 or self.car_at_world1)):
-            from .custom_ar import CustomAllReduce
+            from .custom_ar import (_HINT, CustomAllReduce, PeerAccessError,
+                                    describe_failures, peer_access_failures)
 
+            if self.world > 1:
+                self.peer_failures = peer_access_failures(self.group, device)
+                if self.peer_failures:
+                    msg = ("IPC collectives need peer access between every pair of the group's "
+                           "GPUs: " + describe_failures(self.peer_failures))
+                    if not self.car_fallback:
+                        raise PeerAccessError(msg + "; " + _HINT)
+                    import warnings
+
+                    warnings.warn(msg + "; using RCCL for every collective (P2P_CUSTOM_AR=auto)")
+                    return self
             self.car = CustomAllReduce(self.group, device, self.car_max_bytes)
         return self
 

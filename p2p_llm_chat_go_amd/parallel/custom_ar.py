@@ -39,6 +39,56 @@ class CollectiveTimeout(RuntimeError):
     """A one-shot collective gave up waiting for a peer rank (dead or hung)."""
 
 
+class PeerAccessError(RuntimeError):
+    """Two ranks of a TP / EP group cannot map each other's memory (no xGMI / PCIe peer
+    path, or ranks on different hosts): the IPC kernels cannot run in this group."""
+
+
+_HINT = ("set P2P_CUSTOM_AR=0 to run every collective on RCCL, or P2P_CUSTOM_AR=auto to "
+         "fall back to RCCL automatically when the peer check fails")
+
+
+def peer_access_failures(group=None, device=None, can_access=None) -> list:
+    """Collective preflight of the IPC kernels: every rank reports
+    (host, device ordinal, PCI bus id); each rank checks ``hipDeviceCanAccessPeer`` from its
+    device to every peer on another device of its host, and the failures of all ranks are
+    gathered, so the whole group sees the same list (every rank must make the same
+    IPC-or-RCCL choice: the kernels' tags count calls).  Ranks sharing one device (virtual
+    ranks) need no peer path.  Returns ``[(rank, dev, peer_rank, peer_dev, why), ...]``."""
+    import socket
+
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    dev = torch.device(device) if device is not None else torch.device(
+        "cuda", torch.cuda.current_device())
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    try:
+        bus = torch.cuda.get_device_properties(idx).pci_bus_id
+    except Exception:  # noqa: BLE001 -- older torch: no bus id, ordinals only
+        bus = None
+    me = (socket.gethostname(), idx, bus)
+    info = [None] * world
+    dist.all_gather_object(info, me, group=group)
+    can = can_access or torch.cuda.can_device_access_peer
+    mine = []
+    for r, (host, pidx, pbus) in enumerate(info):
+        if r == rank:
+            continue
+        if host != me[0]:
+            mine.append((rank, idx, r, pidx, "ranks on different hosts (%s, %s)" % (me[0], host)))
+        elif pidx == idx or (bus is not None and pbus == bus):
+            continue  # the same device: virtual ranks
+        elif not can(idx, pidx):
+            mine.append((rank, idx, r, pidx, "hipDeviceCanAccessPeer(%d, %d) = 0" % (idx, pidx)))
+    every = [None] * world
+    dist.all_gather_object(every, mine, group=group)
+    return [f for fs in every for f in fs]
+
+
+def describe_failures(fails) -> str:
+    return "; ".join("rank %d (device %d) -> rank %d (device %d): %s" % f for f in fails)
+
+
 # ranks the fused all-reduce epilogue's buffer holds (csrc/kernels/fused_ar.h FAR_MAX_RANKS)
 FAR_MAX_RANKS = 8
 
@@ -94,8 +144,11 @@ class CustomAllReduce:
                 bases.append(buf.value)
                 continue
             ptr = ctypes.c_void_p()
-            _lib.check(L.p2p_car_open_handle(ctypes.create_string_buffer(hb, hsz),
-                                             ctypes.byref(ptr)), "car_open_handle")
+            err = L.p2p_car_open_handle(ctypes.create_string_buffer(hb, hsz), ctypes.byref(ptr))
+            if err != 0:
+                raise PeerAccessError(
+                    "custom all-reduce: rank %d cannot map rank %d's IPC buffer (hipError %d, "
+                    "hipIpcOpenMemHandle); %s" % (self.rank, r, err, _HINT))
             self._opened.append(ptr)
             bases.append(ptr.value)
         return (ctypes.c_void_p * self.world)(*bases)

@@ -285,6 +285,27 @@ def test_prefill_graph_host_meta(rows, n_seq, pages, real):
     assert (covered == 1).all()
 
 
+def test_prefill_graph_host_meta_long_allocation():
+    """a caller passes the sequence's whole page allocation (prompt +
+    max_new tokens), which can be wider than the chunk's context bucket; host_meta keeps the
+    first max_pages pages (the only ones the chunk reads) instead of asserting."""
+    import types
+
+    from p2p_llm_chat_go_amd.engine.graph import PAGE, PrefillGraph
+
+    pages = 4  # a 256-token context bucket
+    g = PrefillGraph(types.SimpleNamespace(device="cpu", nq=32, nkv=8), None, 256, 1, pages,
+                     pages * PAGE)
+    alloc = [11, 12, 13, 14, 15, 16]  # 200-token prompt + 128 new tokens: 6 pages
+    rws = [(0, i, 5) for i in range(200)]
+    host = g.host_meta(rws, [alloc], [199]).numpy()
+    v = {k: host[a:a + n] for k, (a, n) in g.offsets.items()}
+    assert list(v["bt"][:pages]) == alloc[:pages]
+    assert v["slots"][199] == alloc[199 // PAGE] * PAGE + 199 % PAGE
+    with pytest.raises(AssertionError):  # a row past the context bucket is a caller bug
+        g.host_meta([(0, 300, 5)], [alloc], [0])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("lens", [[44], [5, 37, 12], [60, 3], [130], [44] * 7])
 def test_prefill_graph_equals_eager_gpu(lens):

@@ -48,11 +48,15 @@ def expected(prompt, max_new, stop_on_eos=True, seed=0):
 class FakeModel:
     """Host 'graphs' for the loop: decode steps and prefill chunks over numpy buffers."""
 
-    def __init__(self, prefill_pages):
+    def __init__(self, prefill_pages, k_steps=0):
         self.P = prefill_pages
         self.keep = []
         self.errors = []
         self.loop = None
+        self.k_steps = k_steps  # > 1: decode graphs also offer a k-step exec (exec_k)
+        self.k_runs = 0         # exec_k launches seen
+        self.fault_steps = set()  # decode step numbers (over all graphs) that set the fault word
+        self.n_steps = 0
 
     def _exec(self, fn):
         def run():
@@ -76,6 +80,7 @@ class FakeModel:
         topk = np.zeros(B, np.int32)
         topp = np.zeros(B, np.float32)
         seeds = np.zeros(B, np.int64)
+        err = np.zeros(1, np.int32)
 
         def run():
             ids, pos, cx = meta[:B], meta[B:2 * B], meta[2 * B:3 * B]
@@ -88,10 +93,21 @@ class FakeModel:
                 pos[b] += 1
                 cx[b] = pos[b] + 1
             step[0] = s + 1
-        self.keep += [meta, hist, step, keys, temp, topk, topp, seeds]
+            self.n_steps += 1
+            if self.n_steps in self.fault_steps:
+                err[0] = 1  # as a kernel whose bounded spin gave up
+
+        def run_k():
+            self.k_runs += 1
+            for _ in range(self.k_steps):
+                run()
+        self.keep += [meta, hist, step, keys, temp, topk, topp, seeds, err]
         d = {"B": B, "max_pages": P, "ctx": ctx, "greedy": greedy, "exec": self._exec(run),
              "meta": meta.ctypes.data, "hist": hist.ctypes.data, "max_steps": S,
-             "step": step.ctypes.data, "keys": keys.ctypes.data, "keys_bytes": keys.nbytes}
+             "step": step.ctypes.data, "keys": keys.ctypes.data, "keys_bytes": keys.nbytes,
+             "err": err.ctypes.data}
+        if greedy and self.k_steps > 1:
+            d.update(exec_k=self._exec(run_k), k_steps=self.k_steps)
         if not greedy:
             d.update(temp=temp.ctypes.data, topk=topk.ctypes.data, topp=topp.ctypes.data,
                      seeds=seeds.ctypes.data)
@@ -161,10 +177,10 @@ class FakeModel:
         return [nxt(p[-1], len(p) - 1, 0 if t <= 0 else s) for p, (t, _k, _p, s) in zip(prompts, samp)]
 
 
-def make_loop(pipeline=True, max_batch=8, chunk=4, free_slots=True, riders_all=False):
+def make_loop(pipeline=True, max_batch=8, chunk=4, free_slots=True, riders_all=False, k_steps=0):
     N = load()
     N.loop_use_host_fake_hip()
-    model = FakeModel(prefill_pages=4)
+    model = FakeModel(prefill_pages=4, k_steps=k_steps)
     loop = N.EngineLoop({"num_pages": 256, "max_batch": max_batch, "max_prefill_tokens": 256,
                          "max_ctx": 2048, "eos": [EOS], "decode_chunk": chunk,
                          "admit_wait_us": 200.0, "pipeline": pipeline,
@@ -305,3 +321,93 @@ def test_loop_speculates_only_with_full_batch(max_batch, n, spec):
         assert not model.errors, model.errors[:3]
     finally:
         loop.shutdown()
+
+
+def test_loop_full_batch_replays_k_step_graphs():
+    """with every batch slot taken and decode_chunk = 8 the loop launches
+    whole 8-step graphs (exec_k); replies still equal the model's."""
+    loop, model = make_loop(max_batch=4, chunk=8, free_slots=False, k_steps=8)
+    try:
+        prompts = [[21 + i, 22, 23] for i in range(4)]
+        loop.stall(0.5)  # all admitted in one step: a full batch
+        ids = [loop.submit(p, 70, False) for p in prompts]
+        loop.stall(0.0)
+        for p, rid in zip(prompts, ids):
+            r = loop.wait(rid, 10.0)
+            assert r["done"] and not r["error"], r
+            assert r["tokens"] == expected(p, 70, False)
+            loop.release(rid)
+        assert model.k_runs > 0
+        assert not model.errors, model.errors[:3]
+    finally:
+        loop.shutdown()
+
+
+def test_loop_fault_word_is_cleared_and_repeated_faults_mark_dead():
+    """a fault word set by one decode step fails the requests of that
+    step only -- the loop clears the word and serves the next request -- while faults in
+    kMaxFaultsInRow (3) consecutive steps mark the replica dead (the router's signal)."""
+    loop, model = make_loop(pipeline=False)
+    try:
+        model.fault_steps = {3}
+        rid = loop.submit([5, 6, 7], 10, False)
+        r = loop.wait(rid, 10.0)
+        loop.release(rid)
+        assert r["done"] and "fault word" in r["error"], r
+        rid = loop.submit([5, 6, 7], 10, False)  # the word was cleared: this one is served
+        r = loop.wait(rid, 10.0)
+        loop.release(rid)
+        assert r["done"] and not r["error"] and r["tokens"] == expected([5, 6, 7], 10, False), r
+        assert loop.dead() == ""
+        n = model.n_steps
+        model.fault_steps = set(range(n + 1, n + 100))  # every step faults from now on
+        for _ in range(3):
+            rid = loop.submit([8, 9], 10, False)
+            r = loop.wait(rid, 10.0)
+            loop.release(rid)
+            assert r["done"] and r["error"], r
+        assert "fault word" in loop.dead()
+        with pytest.raises(RuntimeError, match="replica is down"):
+            loop.submit([1, 2], 4, False)
+    finally:
+        loop.shutdown()
+
+
+def test_loop_refuses_request_past_largest_context_bucket():
+    """prompt + max_new + decode slack beyond the largest context bucket
+    is refused at submit, alone, instead of failing the running batch later."""
+    N = load()
+    N.loop_use_host_fake_hip()
+    model = FakeModel(prefill_pages=4)
+    loop = N.EngineLoop({"num_pages": 256, "max_batch": 4, "max_prefill_tokens": 256,
+                         "max_ctx": 2048, "eos": [EOS], "decode_chunk": 4,
+                         "ctx_buckets": [256, 512, 1024, 2048],
+                         "row_buckets": [16, 32, 64, 128, 256], "prefill_max_pages": 4})
+    model.loop = loop
+    loop.set_provider(model.provide)
+    loop.set_eager_prefill(model.eager)
+    loop.start()
+    try:
+        with pytest.raises(ValueError, match="largest context bucket"):
+            loop.submit([1] * 100, 2048 - 100, False)
+        rid = loop.submit([1, 2, 3], 20, False)  # the loop still serves
+        r = loop.wait(rid, 10.0)
+        loop.release(rid)
+        assert r["done"] and r["tokens"] == expected([1, 2, 3], 20, False)
+    finally:
+        loop.shutdown()
+
+
+def test_loop_dead_wait_tokens_reports_down():
+    """once the loop is stopped, wait_tokens reports done (no busy spin to
+    the deadline) and wait() carries the reason."""
+    loop, model = make_loop()
+    loop.stall(5.0)
+    rid = loop.submit([5, 6], 10, False)
+    loop.stop()
+    t0 = time.perf_counter()
+    new, done = loop.wait_tokens(rid, 0, 5.0)
+    assert done and time.perf_counter() - t0 < 1.0
+    r = loop.wait(rid, 1.0)
+    assert r["done"] and "replica is down" in r["error"], r
+    loop.shutdown()

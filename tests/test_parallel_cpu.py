@@ -268,3 +268,56 @@ def test_local_collective_timeout_raises_on_every_rank():
     for p in ps:
         p.join(30)
     assert res[0][1].startswith("raised: a one-shot") and res[1][1] == "raised: local spin timeout"
+
+
+def _peer_worker(rank, world, port, q, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), P2P_CUSTOM_AR=mode)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    from p2p_llm_chat_go_amd.parallel import custom_ar
+    from p2p_llm_chat_go_amd.parallel.comm import TPComm
+
+    def no_path_1_2(a, b):  # mocked hipDeviceCanAccessPeer: devices 1 and 2 see no peer path
+        return {a, b} != {1, 2}
+
+    fails = custom_ar.peer_access_failures(None, torch.device("cuda", rank), can_access=no_path_1_2)
+    # TPComm.setup on "GPU" rank devices with the same mock: raise (default) or fall back
+    real = custom_ar.peer_access_failures
+    custom_ar.peer_access_failures = lambda g, d: real(g, d, can_access=no_path_1_2)
+    comm = TPComm()
+    try:
+        comm.setup(torch.device("cuda", rank))
+        outcome = ("fallback", comm.car is None, len(comm.peer_failures))
+    except custom_ar.PeerAccessError as e:
+        outcome = ("raised", str(e))
+    dist.destroy_process_group()
+    _put_exit(q, (rank, sorted(fails), outcome))
+
+
+@pytest.mark.parametrize("mode", ["1", "auto"])
+def test_peer_access_preflight_names_pair(mode):
+    """before mapping IPC buffers every rank checks peer access to every
+    other device of the group; the failing pairs are gathered so all ranks agree, the error
+    names them and points at P2P_CUSTOM_AR=0, and P2P_CUSTOM_AR=auto falls back to RCCL."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    port = _port()
+    q = ctx.Queue()
+    world = 4
+    ps = [ctx.Process(target=_peer_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(30)
+    want = [(1, 1, 2, 2), (2, 2, 1, 1)]
+    for rank, fails, outcome in res:
+        assert [f[:4] for f in fails] == want, fails  # every rank sees the same pairs
+        if mode == "1":
+            assert outcome[0] == "raised"
+            assert "rank 1 (device 1) -> rank 2 (device 2)" in outcome[1]
+            assert "P2P_CUSTOM_AR=0" in outcome[1]
+        else:
+            assert outcome == ("fallback", True, 2)
