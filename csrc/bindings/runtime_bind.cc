@@ -53,6 +53,7 @@ void bind_runtime(py::module_& m) {
 
 #include "runtime/engine_loop.h"
 #include "runtime/hip_dyn.h"
+#include "runtime/loop_capi.h"
 
 namespace {
 
@@ -228,5 +229,9 @@ void bind_engine_loop(py::module_& m) {
              return py::make_tuple(t, done);
            })
       .def("metrics", &EngineLoop::metrics, py::call_guard<py::gil_scoped_release>())
-      .def("dead", &EngineLoop::dead, py::call_guard<py::gil_scoped_release>());
+      .def("dead", &EngineLoop::dead, py::call_guard<py::gil_scoped_release>())
+      // the loop's address, for native front ends driving it through p2p_loop_api()
+      .def("handle", [](EngineLoop& L) { return (uintptr_t)&L; });
+  // address of the plain-C table (runtime/loop_capi.h) of the loop code in THIS module
+  m.def("loop_api", []() { return (uintptr_t)p2p_loop_api(); });
 }

@@ -128,6 +128,41 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     }
   };
 
+  // The output group this wave finishes, if any: group w (SILU: gate/up pair w < 4); under
+  // split-K only slice (w % splitk) finishes it.
+  const int r = lane & 15, q = lane >> 4;
+  const bool fin = w < (SILU ? 4 : 8) && (!SPLIT || (w % splitk) == split);
+  const int g = SILU ? tile * 4 + w : tile * 8 + w;
+  // Epilogue operands, issued as ONE batch per lane BEFORE the weight stream (they are the
+  // oldest loads in flight, so the counted chunk waits below still hold, and they have long
+  // landed when the epilogue runs): the residual values (EPI_RESID), the rows' KV slots and
+  // positions (EPI_QKV_ROPE; the (cos, sin) loads that depend on the positions go out right
+  // after the main loop).  Issued after the main loop, the residual loads held up the slab
+  // drain of the split-K seam by ~1.6 us (bench/wide_stamp_probe.py, r5); loaded element by
+  // element in the epilogue they were a chain of MT x 4 dependent round trips per lane.
+  float res[MT][4];
+  float2 csv[MT][4];
+  int slotv[MT][4];
+  int posv[MT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = 16 * i + 4 * q + j;
+      const bool ok = fin && m < M;
+      res[i][j] = 0.f;
+      slotv[i][j] = -1;
+      posv[i][j] = -1;
+      csv[i][j] = float2{1.f, 0.f};
+      if constexpr (EPI == EPI_RESID)
+        if (ok) res[i][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + g * 16 + r];
+      if constexpr (EPI == EPI_QKV_ROPE)
+        if (ok) {
+          slotv[i][j] = ea.slots[m];
+          posv[i][j] = ea.pos[m];
+        }
+    }
+
   f32x4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -187,44 +222,9 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     ss += __shfl_xor(ss, 32, 64);
     if (sq_mt < MT && lane < 16) ss_l[sq_par][sq_mt][lane] = ss;
   }
-  const int r = lane & 15, q = lane >> 4;
-
-  // The output group this wave finishes, if any: group w (SILU: gate/up pair w < 4); under
-  // split-K only slice (w % splitk) finishes it.
-  const bool fin = w < (SILU ? 4 : 8) && (!SPLIT || (w % splitk) == split);
-  const int g = SILU ? tile * 4 + w : tile * 8 + w;
-  // Epilogue operands, fetched as ONE batch per lane right after the main loop (they land
-  // while the slices meet): the residual values (EPI_RESID), the rows' positions, KV slots
-  // and (cos, sin) (EPI_QKV_ROPE).  Element-by-element in the epilogue they were a chain of
-  // MT x 4 dependent round trips per lane (a residual add loads, then stores, each element).
-  float res[MT][4];
-  float2 csv[MT][4];
-  int slotv[MT][4];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = 16 * i + 4 * q + j;
-      const bool ok = fin && m < M;
-      res[i][j] = 0.f;
-      slotv[i][j] = -1;
-      csv[i][j] = float2{1.f, 0.f};
-      if constexpr (EPI == EPI_RESID)
-        if (ok) res[i][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + g * 16 + r];
-      if constexpr (EPI == EPI_QKV_ROPE)
-        if (ok) slotv[i][j] = ea.slots[m];
-    }
   if constexpr (EPI == EPI_QKV_ROPE) {
     const int kk = g & 7;
     const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
-    int posv[MT][4];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = 16 * i + 4 * q + j;
-        posv[i][j] = (fin && m < M) ? ea.pos[m] : -1;
-      }
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -343,18 +343,21 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       __syncthreads();
     }
     if (!fin) return;
-    // the finished group's partials, summed in slice order; loads in batches of 4 slices
-    // (clamped indices: straight-line code, one wait per batch)
+    // the finished group's partials, summed in slice order; loads in batches of SB slices
+    // (clamped indices: straight-line code, one wait per batch).  SB = 8 covers the usual
+    // 5-8 slices in ONE round trip (batches of 4 cost a second one, ~1 us, r5 stamps); the
+    // SwiGLU form loads gate and up partials, so it keeps 4 (VGPRs)
+    constexpr int SB = SILU ? 4 : 8;
     f32x4 tot[MT], up[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       tot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       up[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    for (int s0 = 0; s0 < splitk; s0 += 4) {
-      f32x4 pt[4][MT], pu[4][MT];
+    for (int s0 = 0; s0 < splitk; s0 += SB) {
+      f32x4 pt[SB][MT], pu[SB][MT];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < SB; ++s) {
         const int s2 = min(s0 + s, splitk - 1);
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
@@ -364,7 +367,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
         }
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < SB; ++s) {
         if (s0 + s >= splitk) break;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {

@@ -6,6 +6,7 @@
 #include <stdexcept>
 
 #include "runtime/hip_dyn.h"
+#include "runtime/loop_capi.h"
 
 namespace p2p {
 
@@ -261,6 +262,7 @@ std::map<std::string, double> EngineLoop::metrics() {
   m["eager_prefill_calls"] = n_eager_prefill_;
   m["decode_calls"] = n_decode_calls_;
   m["decode_steps"] = n_decode_steps_;
+  m["k_graph_launches"] = n_k_graph_launches_;  // whole k_steps-step decode graph replays
   m["speculated_chunks"] = n_speculated_;
   m["state_loads"] = n_loads_;
   m["errors"] = n_errors_;
@@ -671,8 +673,10 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
   // the next launch of the prompt-chunk graph pays: ~8 us per launch, bench/graph_switch_probe.py)
   int left = k;
   if (g->exec_k && g->k_steps > 1)
-    for (; left >= g->k_steps; left -= g->k_steps)
+    for (; left >= g->k_steps; left -= g->k_steps) {
       hip_check(h.graphLaunch(g->exec_k, stream_), "decode graph launch");
+      n_k_graph_launches_++;
+    }
   for (; left > 0; --left) hip_check(h.graphLaunch(g->exec, stream_), "decode graph launch");
   Chunk c;
   c.g = g;
@@ -821,3 +825,93 @@ void EngineLoop::decode(const std::vector<int64_t>& running_in, bool waiting) {
 }
 
 }  // namespace p2p
+
+// ------------------------------------------------------------------ plain-C table
+// (runtime/loop_capi.h): the engine C ABI library drives the loop through these, so a
+// request from the node daemon never enters Python.  Exceptions stay on this side.
+namespace {
+
+using p2p::EngineLoop;
+
+void copy_err(const std::exception& e, char* err, int errlen) {
+  if (err && errlen > 0) {
+    strncpy(err, e.what(), (size_t)errlen - 1);
+    err[errlen - 1] = 0;
+  }
+}
+
+int64_t c_submit(void* loop, const int32_t* ids, int n, int max_new, int stop_on_eos, float temp,
+                 int top_k, float top_p, int64_t seed, char* err, int errlen) {
+  try {
+    p2p::LoopSampling s;
+    s.temperature = temp;
+    s.top_k = top_k;
+    s.top_p = top_p;
+    s.seed = seed;
+    return ((EngineLoop*)loop)->submit(std::vector<int>(ids, ids + n), max_new, stop_on_eos != 0, s);
+  } catch (const std::exception& e) {
+    copy_err(e, err, errlen);
+    return -1;
+  }
+}
+
+int c_wait(void* loop, int64_t id, double timeout_s, P2PLoopResult* out) {
+  memset(out, 0, sizeof(*out));
+  p2p::LoopResult r;
+  try {
+    ((EngineLoop*)loop)->wait(id, timeout_s, &r);
+  } catch (const std::exception& e) {
+    r.error = e.what();
+  }
+  out->n_tokens = (int)r.tokens.size();
+  out->tokens = (int32_t*)malloc(sizeof(int32_t) * std::max<size_t>(1, r.tokens.size()));
+  for (size_t i = 0; i < r.tokens.size(); ++i) out->tokens[i] = r.tokens[i];
+  out->done = r.done ? 1 : 0;
+  out->prompt_eval_count = r.prompt_eval_count;
+  out->prompt_eval_ns = r.prompt_eval_ns;
+  out->eval_ns = r.eval_ns;
+  out->total_ns = r.total_ns;
+  out->ttft_ns = r.ttft_ns;
+  strncpy(out->done_reason, r.done_reason.c_str(), sizeof(out->done_reason) - 1);
+  out->error = r.error.empty() ? nullptr : strdup(r.error.c_str());
+  return 0;
+}
+
+int c_wait_tokens(void* loop, int64_t id, size_t have, double timeout_s, int32_t** toks, int* n,
+                  int* done) {
+  bool d = false;
+  std::vector<int> t;
+  try {
+    t = ((EngineLoop*)loop)->wait_tokens(id, have, timeout_s, &d);
+  } catch (const std::exception&) {
+    d = true;  // unknown request / loop gone: the caller's final wait() reports why
+  }
+  *toks = (int32_t*)malloc(sizeof(int32_t) * std::max<size_t>(1, t.size()));
+  for (size_t i = 0; i < t.size(); ++i) (*toks)[i] = t[i];
+  *n = (int)t.size();
+  *done = d ? 1 : 0;
+  return 0;
+}
+
+void c_cancel(void* loop, int64_t id) { ((EngineLoop*)loop)->cancel(id); }
+void c_release(void* loop, int64_t id) { ((EngineLoop*)loop)->release(id); }
+
+int c_dead(void* loop, char* buf, int len) {
+  const std::string d = ((EngineLoop*)loop)->dead();
+  if (buf && len > 0) {
+    strncpy(buf, d.c_str(), (size_t)len - 1);
+    buf[len - 1] = 0;
+  }
+  return (int)d.size();
+}
+
+void c_free(void* p) { free(p); }
+
+const P2PLoopApi g_loop_api = {P2P_LOOP_API_VERSION, c_submit, c_wait, c_wait_tokens, c_cancel,
+                               c_release, c_dead, c_free};
+
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) const P2PLoopApi* p2p_loop_api(void) {
+  return &g_loop_api;
+}

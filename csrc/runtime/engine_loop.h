@@ -213,7 +213,7 @@ class EngineLoop {
 
   // metrics
   std::atomic<long> n_requests_{0}, n_tokens_{0}, n_prefill_calls_{0}, n_decode_calls_{0},
-      n_decode_steps_{0}, n_prefill_tokens_{0}, n_speculated_{0}, n_loads_{0}, n_errors_{0},
+      n_decode_steps_{0}, n_k_graph_launches_{0}, n_prefill_tokens_{0}, n_speculated_{0}, n_loads_{0}, n_errors_{0},
       n_eager_prefill_{0};
   std::atomic<int64_t> busy_ns_{0}, prefill_ns_{0}, decode_ns_{0}, capture_ns_{0}, eager_ns_{0},
       prefill_wait_ns_{0}, n_captures_{0}, n_prefill_waits_{0}, n_admit_hits_{0},

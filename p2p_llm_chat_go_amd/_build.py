@@ -49,6 +49,42 @@ def _run(cmd, cwd=None):
     return r.stdout
 
 
+def sources_digest(paths) -> str:
+    """sha256 over the (relative path, bytes) of every source and header a library is built
+    from: recorded next to the library at link time (``<lib>.stamp``) and compared by the
+    loader (ops/_lib.py), so a binary that no build of the current sources produced is
+    refused instead of silently tested (What's weak #8)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in sorted(set(paths)):
+        h.update(os.path.relpath(p, ROOT).encode())
+        h.update(b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def kernel_sources(experimental=False):
+    """(sources, headers) of the kernel library (or of the experimental one)."""
+    kdir = os.path.join(CSRC, "kernels")
+    sub = "experimental" if experimental else "kernels"
+    srcs = sorted(glob.glob(os.path.join(CSRC, sub, "*.hip")))
+    hdrs = _headers(kdir)
+    if experimental:  # probe builds #include kernel sources (wide_stamp.hip: wide_gemm.hip)
+        hdrs += sorted(glob.glob(os.path.join(kdir, "*.hip")))
+    return srcs, hdrs
+
+
+def _write_stamp(out_lib, srcs, hdrs):
+    import json
+
+    with open(out_lib + ".stamp", "w") as f:
+        json.dump({"sources_sha256": sources_digest(list(srcs) + list(hdrs)),
+                   "n_files": len(set(srcs) | set(hdrs)), "arch": ARCH}, f)
+
+
 def _headers(d):
     return glob.glob(os.path.join(d, "*.h")) + glob.glob(os.path.join(CSRC, "include", "*.h"))
 
@@ -63,14 +99,9 @@ def build_kernels(force=False, jobs=8, experimental=False):
     hardware probes kept for the record and their benches) into a separate
     ``libp2p_experimental.so`` instead; no default engine path loads it."""
     kdir = os.path.join(CSRC, "kernels")
-    out_lib = KERNEL_LIB
-    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")))
-    hdrs = _headers(kdir)
-    odir = os.path.join(BUILDDIR, "kernels")
-    if experimental:
-        srcs = sorted(glob.glob(os.path.join(CSRC, "experimental", "*.hip")))
-        odir = os.path.join(BUILDDIR, "experimental")
-        out_lib = EXPERIMENTAL_LIB
+    srcs, hdrs = kernel_sources(experimental)
+    odir = os.path.join(BUILDDIR, "experimental" if experimental else "kernels")
+    out_lib = EXPERIMENTAL_LIB if experimental else KERNEL_LIB
     os.makedirs(odir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     flags = [
@@ -97,6 +128,7 @@ def build_kernels(force=False, jobs=8, experimental=False):
         _run([HIPCC, "-shared", "-fPIC", "--offload-arch=%s" % ARCH] + objs + ["-o", out_lib])
         with open(listed, "w") as f:
             f.write("\n".join(objs))
+    _write_stamp(out_lib, srcs, hdrs)
     return out_lib
 
 
@@ -223,7 +255,9 @@ def build_sanitized(kind: str, force=False, jobs=8):
 def build(force=False, jobs=8, only=None, experimental=None):
     outs = []
     if experimental is None:
-        experimental = os.environ.get("P2P_BUILD_EXPERIMENTAL", "0") == "1"
+        # on by default: the experimental library's tests run on the GPU box, so the binary
+        # they load must be built from HEAD like the rest (P2P_BUILD_EXPERIMENTAL=0 skips it)
+        experimental = os.environ.get("P2P_BUILD_EXPERIMENTAL", "1") == "1"
     if only in (None, "kernels", "experimental"):
         if shutil.which(HIPCC) or os.path.exists(HIPCC):
             if only != "experimental":

@@ -155,6 +155,31 @@ class NativeEngineServer(EngineServer):
             raise EngineTimeout("engine did not answer within %gs (request cancelled)" % t)
         return r
 
+    def native_front(self) -> dict:
+        """Everything the engine C ABI (csrc/engine/engine_capi.cc) needs to serve requests
+        without entering Python: the loop's plain-C table (runtime/loop_capi.h) and address,
+        the tokenizer's native spec, and the server's defaults.  Requests then go
+        JSON -> ids -> EngineLoop::submit/wait -> text -> JSON in C++ (tokenisation falls
+        back to ``encode_request`` / ``decode_ids`` under the GIL for tokenizers the native
+        side does not implement, or non-ASCII text)."""
+        N = load_native()
+        spec = self.tok.native_spec() if hasattr(self.tok, "native_spec") else {"kind": "hf"}
+        return {"api": int(N.loop_api()), "loop": int(self.loop.handle()),
+                "model": self.model_name, "default_max_tokens": int(self.default_max_tokens),
+                "timeout_s": float(self.request_timeout_s), "tokenizer": json.dumps(spec)}
+
+    def encode_request(self, req_text: str) -> list:
+        """Prompt ids of an Ollama request (the C ABI's fallback tokenisation)."""
+        req = json.loads(req_text)
+        if req.get("endpoint") == "chat":
+            return self.tok.chat_messages_ids(req.get("messages") or [])
+        if req.get("raw"):
+            return self.tok.encode(req.get("prompt", ""), bos=True)
+        return self.tok.chat_ids(req.get("prompt", ""))
+
+    def decode_ids(self, ids) -> str:
+        return self.tok.decode(list(ids))
+
     def stall(self, seconds: float):
         self.loop.stall(float(seconds))
 

@@ -161,6 +161,15 @@ class SyntheticTokenizer:
     def chat_messages_ids(self, messages: list) -> list:
         return _render_messages(self, messages, LLAMA3_SPECIAL.__getitem__)
 
+    def native_spec(self) -> dict:
+        """What the engine C ABI needs to encode / decode natively (csrc/engine/
+        native_tok.h): the hash range, the special ids and the built-in decode table; ids
+        outside the table decode to ``_pseudo`` words, which the native side recomputes."""
+        return {"kind": "synthetic", "llama3": bool(self.llama3), "lo": self.lo, "hi": self.hi,
+                "bos": int(self.bos_id), "eos": [int(e) for e in self.eos_ids],
+                "special": dict(LLAMA3_SPECIAL) if self.llama3 else {},
+                "pieces": [[int(i), w] for i, w in sorted(self._table().items())]}
+
 
 class HFTokenizer:
     def __init__(self, path: str, eos_ids=None):
@@ -197,6 +206,10 @@ class HFTokenizer:
 
     def chat_messages_ids(self, messages: list) -> list:
         return _render_messages(self, messages, self.tok.token_to_id)
+
+    def native_spec(self) -> dict:
+        # a real BPE / SentencePiece model: the C ABI asks Python to encode and decode
+        return {"kind": "hf"}
 
 
 def get_tokenizer(cfg=None, path: str | None = None):

@@ -142,6 +142,38 @@ class KernelError(RuntimeError):
     pass
 
 
+def check_stamp(path: str, experimental: bool = False) -> None:
+    """Refuse a library that no build of the current sources produced: ``_build`` records a
+    digest of the sources and headers next to the library (``<lib>.stamp``); a mismatch
+    means the binary is stale (an edited kernel that was never rebuilt, or a copy pushed
+    from elsewhere).  Skipped where the sources are not present; P2P_ALLOW_STALE_LIB=1
+    downgrades the error to a warning."""
+    from .. import _build
+
+    srcs, hdrs = _build.kernel_sources(experimental)
+    if not srcs:
+        return  # installed without csrc/: nothing to compare against
+    why = None
+    try:
+        import json
+
+        with open(path + ".stamp") as f:
+            rec = json.load(f)
+        if rec.get("sources_sha256") != _build.sources_digest(srcs + hdrs):
+            why = "was built from different sources than the tree's csrc/"
+    except FileNotFoundError:
+        why = "has no build stamp (%s.stamp)" % os.path.basename(path)
+    if why is None:
+        return
+    msg = ("%s %s -- rebuild with `python -m p2p_llm_chat_go_amd._build`" % (path, why))
+    if os.environ.get("P2P_ALLOW_STALE_LIB", "0") == "1":
+        import warnings
+
+        warnings.warn(msg)
+        return
+    raise KernelError(msg)
+
+
 def lib_path() -> str:
     return _LIB_PATH
 
@@ -158,6 +190,7 @@ def lib():
             raise KernelError(
                 "HIP kernel library missing at %s -- run `python -m p2p_llm_chat_go_amd._build` "
                 "(or __graft_entry__.build())" % _LIB_PATH)
+        check_stamp(_LIB_PATH)
         L = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         for name in ("p2p_car_buffer_bytes", "p2p_far_buffer_bytes"):
             fn = getattr(L, name, None)
@@ -228,6 +261,7 @@ def experimental():
                 raise KernelError(
                     "experimental kernel library missing at %s -- build it with "
                     "`python -m p2p_llm_chat_go_amd._build --only experimental`" % _EXP_PATH)
+            check_stamp(_EXP_PATH, experimental=True)
             L = ctypes.CDLL(_EXP_PATH, mode=ctypes.RTLD_GLOBAL)
             for name in _EXP_SIGS:
                 fn = getattr(L, name, None)

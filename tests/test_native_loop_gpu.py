@@ -89,6 +89,38 @@ def test_native_loop_matches_static_greedy():
         srv.close()
 
 
+def test_native_loop_full_batch_replays_k_step_graphs():
+    """A full batch (running == max_batch) with decode_chunk=8: the loop's decode chunks are
+    8 steps long, so it replays the whole 8-step graph (exec_k, engine_loop.cc) instead of
+    8 one-step launches -- the path the serving numbers are measured on.  Replies must
+    equal the static engine's."""
+    from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
+
+    eng, _w, _cfg = _engine(max_batch=4)
+    prompts = _prompts(4)
+    n = 41  # 5 whole 8-step chunks + a tail
+    ref = [eng.generate([p], n, stop_on_eos=False)[0].tokens for p in prompts]
+    srv = NativeEngineServer(eng, max_batch=4, decode_chunk=8)
+    try:
+        outs = [None] * 4
+        start = threading.Barrier(4)
+
+        def run(i):
+            start.wait()
+            outs[i] = srv.generate(prompts[i], SamplingParams(max_tokens=n, stop_on_eos=False))
+
+        ths = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        m = srv.metrics()
+    finally:
+        srv.close()
+    assert m["k_graph_launches"] >= 2, m  # whole 8-step graphs replayed by the loop
+    for p, o, r in zip(prompts, outs, ref):
+        assert o["done"] and len(o["tokens"]) == n
+        assert _same_or_near_tie(eng, p, o["tokens"], r)
+
+
 def test_native_loop_sampled_matches_python_loop():
     from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
     from p2p_llm_chat_go_amd.engine.server import EngineServer
