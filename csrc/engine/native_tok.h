@@ -137,20 +137,14 @@ class NativeTok {
       ids->push_back(sp_id("<|end_header_id|>"));
       return encode("\n\n", ids);
     }
+    // "\n\n".join of every system content (empty ones included, as in Python)
     std::string system;
+    bool first = true;
     for (auto& m : ms)
-      if (m.first == "system") system += (system.empty() ? "" : "\n\n") + m.second;
-    // (Python joins every system content, empty ones included)
-    {
-      std::string j;
-      bool first = true;
-      for (auto& m : ms)
-        if (m.first == "system") {
-          j += (first ? "" : "\n\n") + m.second;
-          first = false;
-        }
-      system = j;
-    }
+      if (m.first == "system") {
+        system += (first ? "" : "\n\n") + m.second;
+        first = false;
+      }
     for (auto& m : ms) {
       if (m.first == "system") continue;
       if (m.first == "assistant") {

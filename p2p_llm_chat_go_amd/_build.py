@@ -198,8 +198,11 @@ def build_native(force=False, jobs=8):
         pylib = ["-L" + (sysconfig.get_config_var("LIBDIR") or "/usr/lib"),
                  "-lpython%s" % sysconfig.get_config_var("VERSION")]
         ehdrs = glob.glob(os.path.join(CSRC, "engine", "*.h"))
-        if force or _stale(lib, eng_src + ehdrs):
-            _run([CXX] + base + ["-shared", "-I", pyinc] + eng_src + ["-o", lib] + pylib + ["-ldl"])
+        # (links the runtime archive for the JSON codec; the loop itself is driven through
+        # the table of the pybind module that owns it, runtime/loop_capi.h)
+        if force or _stale(lib, eng_src + ehdrs + hdrs + [ar]):
+            _run([CXX] + base + ["-shared", "-I", pyinc] + eng_src + [ar, "-o", lib] + pylib
+                 + libs + ["-ldl"])
         outs.append(lib)
     return outs
 

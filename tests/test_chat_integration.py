@@ -492,6 +492,19 @@ def test_node_daemon_hosts_engine_in_process(procs, dev):
         "".join(x.get("response", "") for x in lines))]
     st, body, _ = http("POST", a + "/suggest", {"message": "Hey! How's it going?"})
     assert st == 200 and "suggestion" in json.loads(body)
+    if dev.startswith("cuda"):
+        # on a GPU the server runs the native loop and the C ABI serves requests without
+        # the interpreter: JSON -> native tokenizer -> EngineLoop -> text -> JSON in C++
+        # (the one GIL entry counted is this /metrics call's own)
+        m = {}
+        for line in http("GET", a + "/metrics")[1].splitlines():
+            k, _, v = line.partition(" ")
+            m[k] = float(v) if v else 0.0
+        assert m.get("p2p_engine_capi_native_requests", 0) >= 3, m
+        assert m.get("p2p_engine_capi_native_tokenizer") == 1, m
+        assert m.get("p2p_engine_capi_python_tokenize") == 0, m
+        assert m.get("p2p_engine_capi_python_decode") == 0, m
+        assert m.get("p2p_engine_capi_gil_entries") == 1, m
 
 
 def test_connection_manager_trims_to_low_watermark(procs):
