@@ -44,6 +44,10 @@ def main():
                     help="1: running sequences ride in prefill steps (mixed batches)")
     ap.add_argument("--gpus", type=int, default=1, help="serve through engine.cluster on N GPUs")
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--virtual", type=int, default=0,
+                    help="1: every rank of the group on ONE GPU (virtual ranks; compares the "
+                         "serving loops, not multi-GPU speed)")
+    ap.add_argument("--kv-pages", type=int, default=0, help="KV pages per rank (0: from free memory)")
     ap.add_argument("--ep", type=int, default=1)
     ap.add_argument("--warm-rounds", type=int, default=1,
                     help="untimed rounds of the timed pattern first (every peer's requests in "
@@ -139,7 +143,8 @@ def cluster_main(a):
 
     cs = ClusterServer(a.model, gpus=a.gpus, tp=a.tp, ep=a.ep,
                        device="cpu" if a.device == "cpu" else "cuda",
-                       max_batch=max(8, a.peers), max_tokens=a.new_tokens)
+                       max_batch=max(8, a.peers), max_tokens=a.new_tokens,
+                       virtual_ranks=bool(a.virtual), kv_pages=a.kv_pages or None)
 
     def req(p, r):
         n = a.new_tokens - ((p * 31 + r) * 7919) % (a.jitter + 1)
@@ -179,6 +184,10 @@ def cluster_main(a):
         "ttft_p50_ms": round(statistics.median(ttft), 3),
         "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
         "routed": [r.get("routed") for r in m.get("per_replica", [])], "dtype": "bf16",
+        "loop": "native" if all(r.get("native_loop") for r in m.get("per_replica", [])) else "python",
+        "mirror_frames": sum(r.get("mirror_frames", 0) for r in m.get("per_replica", [])),
+        "k_graph_launches": sum(r.get("k_graph_launches", 0) for r in m.get("per_replica", [])),
+        "virtual_ranks": bool(a.virtual),
         "data": "synthetic chat prompts, random-init weights"}), flush=True)
 
 

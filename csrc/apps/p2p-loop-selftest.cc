@@ -14,14 +14,21 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
+#include <string>
+#include <tuple>
 #include <random>
 #include <thread>
 #include <utility>
 #include <vector>
 
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include "runtime/engine_loop.h"
 #include "runtime/hip_dyn.h"
+#include "runtime/mirror.h"
 
 using namespace p2p;
 
@@ -66,10 +73,14 @@ void* exec_of(std::function<int()> f) {
   return reinterpret_cast<void*>(g_table[i]);
 }
 
+uint64_t mix(uint64_t h, uint64_t v) { return (h ^ v) * 0x100000001B3ull; }
+
 struct DecodeGraph {
   std::vector<int32_t> meta, hist, step{0};
   std::vector<int64_t> keys{0};
   DecodeGraphDesc d;
+  uint64_t trace = 1469598103934665603ull;  // FNV over (step, meta) at every replay
+  long launches = 0;
   DecodeGraph(int B, int ctx) : meta((size_t)B * (4 + ctx / PAGE)), hist((size_t)B * ctx) {
     d.B = B;
     d.max_pages = ctx / PAGE;
@@ -81,8 +92,11 @@ struct DecodeGraph {
     d.step = step.data();
     d.keys = keys.data();
     d.keys_bytes = sizeof(int64_t);
-    d.exec = exec_of([this] {
+    auto one = [this] {
       const int B = d.B, S = d.max_steps, s = step[0];
+      launches++;
+      trace = mix(trace, (uint64_t)s);
+      for (int32_t v : meta) trace = mix(trace, (uint64_t)(uint32_t)v);
       if (s >= S) {
         g_bad++;
         return 1;
@@ -97,6 +111,13 @@ struct DecodeGraph {
       }
       step[0] = s + 1;
       return 0;
+    };
+    d.exec = exec_of(one);
+    d.k_steps = 4;  // a whole 4-step graph (the loop launches those first)
+    d.exec_k = exec_of([one] {
+      int rc = 0;
+      for (int i = 0; i < 4; ++i) rc |= one();
+      return rc;
     });
   }
 };
@@ -104,6 +125,8 @@ struct DecodeGraph {
 struct PrefillGraph {
   std::vector<int32_t> meta, first;
   PrefillGraphDesc d;
+  uint64_t trace = 1469598103934665603ull;
+  long launches = 0;
   PrefillGraph(int R, int S) : first(S) {
     const int P = PREFILL_PAGES, qtile = 16;
     const int max_tiles = (R + qtile - 1) / qtile + S + 1 + R / (P * PAGE) + 1;
@@ -130,6 +153,8 @@ struct PrefillGraph {
     d.first = first.data();
     d.exec = exec_of([this] {
       const int R = d.rows, S = d.n_seq;
+      launches++;
+      for (int32_t v : meta) trace = mix(trace, (uint64_t)(uint32_t)v);
       const int32_t* seq = meta.data() + d.off_seq;
       const int32_t* pos = meta.data() + d.off_pos;
       const int32_t* ids = meta.data() + d.off_ids;
@@ -247,6 +272,153 @@ int run(bool pipeline, bool riders_all) {
   return failures.load() == 0 && g_bad.load() == 0 && checked.load() > 20 ? 0 : 1;
 }
 
+// A TP group of 1 leader + 2 followers (runtime/mirror.h): the leader's loop serves mixed
+// traffic while two EngineMirror threads apply its frames to graphs of their own, over
+// socketpairs.  Every follower graph must have been replayed exactly as often as the
+// leader's, with the same metadata at every replay (trace), and each follower must have
+// captured every shape and run every eager prefill the leader did.
+int run_group() {
+  constexpr int NF = 2;
+  LoopConfig c;
+  c.num_pages = 512;
+  c.max_batch = 8;
+  c.max_prefill_tokens = 256;
+  c.max_ctx = 2048;
+  c.eos = {EOS};
+  c.decode_chunk = 8;
+  c.admit_wait_us = 200.0;
+  c.row_buckets = {16, 32, 48, 64, 96, 128, 192, 256};
+  c.prefill_max_pages = PREFILL_PAGES;
+  c.prefill_graph_after = 1;
+  EngineLoop loop(c);
+  int sv[NF][2];
+  std::vector<int> fds;
+  for (int f = 0; f < NF; ++f) {
+    if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv[f]) != 0) return 1;
+    fds.push_back(sv[f][0]);
+  }
+  loop.set_mirror(fds);
+  using DMap = std::map<std::tuple<int, int>, std::unique_ptr<DecodeGraph>>;
+  using PMap = std::map<std::tuple<int, int>, std::unique_ptr<PrefillGraph>>;
+  DMap ld;
+  PMap lp;
+  std::atomic<int> leader_eager{0};
+  loop.set_provider([&](const std::string& kind, int a, int b, bool greedy) {
+    loop.mirror_provide(kind, a, b, greedy);  // as NativeEngineServer._provide does
+    if (kind == "decode") {
+      ld[{a, b}].reset(new DecodeGraph(a, b));
+      loop.add_decode_graph(ld[{a, b}]->d);
+    } else {
+      lp[{a, b}].reset(new PrefillGraph(a, b));
+      loop.add_prefill_graph(lp[{a, b}]->d);
+    }
+  });
+  auto eager = [](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>&,
+                  const std::vector<int>&, const std::vector<LoopSampling>&) {
+    std::vector<int> f;
+    for (const auto& p : prompts) f.push_back(nxt(p.back(), (int)p.size() - 1));
+    return f;
+  };
+  loop.set_eager_prefill([&](const std::vector<std::vector<int>>& p, const std::vector<std::vector<int>>& pg,
+                             const std::vector<int>& st, const std::vector<LoopSampling>& sm) {
+    leader_eager++;
+    return eager(p, pg, st, sm);
+  });
+  struct Follower {
+    std::unique_ptr<EngineMirror> m;
+    DMap d;
+    PMap p;
+    std::atomic<int> eager{0};
+    std::string result = "?";
+    std::thread th;
+  };
+  Follower fol[NF];
+  for (int f = 0; f < NF; ++f) {
+    Follower& F = fol[f];
+    F.m.reset(new EngineMirror(sv[f][1], 0));
+    EngineMirror* M = F.m.get();
+    F.m->set_provider([&F, M](const std::string& kind, int a, int b, bool) {
+      if (kind == "decode") {
+        F.d[{a, b}].reset(new DecodeGraph(a, b));
+        M->add_decode_graph(F.d[{a, b}]->d);
+      } else {
+        F.p[{a, b}].reset(new PrefillGraph(a, b));
+        M->add_prefill_graph(F.p[{a, b}]->d);
+      }
+    });
+    F.m->set_eager_prefill([&F, eager](const std::vector<std::vector<int>>& p,
+                                       const std::vector<std::vector<int>>& pg,
+                                       const std::vector<int>& st, const std::vector<LoopSampling>& sm) {
+      F.eager++;
+      return eager(p, pg, st, sm);
+    });
+    F.th = std::thread([&F] { F.result = F.m->run(); });
+  }
+  loop.start();
+  std::atomic<int> failures{0}, checked{0};
+  auto peer = [&](int k) {
+    std::mt19937 rng(77 + k);
+    for (int n = 0; n < 10; ++n) {
+      const int L = std::vector<int>{3, 17, 44, 64, 120, 300}[rng() % 6];
+      std::vector<int> prompt(L);
+      for (int& t : prompt) t = (int)(rng() % (V - 1));
+      const int max_new = 1 + (int)(rng() % 40);
+      const int64_t id = loop.submit(prompt, max_new, false, LoopSampling());
+      LoopResult r;
+      if (!loop.wait(id, 30.0, &r) || !r.error.empty()) failures++;
+      loop.release(id);
+      if (r.tokens != expected(prompt, max_new, false)) failures++;
+      checked++;
+    }
+  };
+  std::vector<std::thread> ths;
+  for (int k = 0; k < 8; ++k) ths.emplace_back(peer, k);
+  for (auto& t : ths) t.join();
+  auto lm = loop.metrics();
+  loop.shutdown();  // sends the stop frame
+  for (int f = 0; f < NF; ++f) {
+    fol[f].th.join();
+    fol[f].m->shutdown();
+    close(sv[f][0]);
+    close(sv[f][1]);
+    if (!fol[f].result.empty()) {
+      std::fprintf(stderr, "selftest: follower %d ended with '%s'\n", f, fol[f].result.c_str());
+      failures++;
+    }
+    if (fol[f].d.size() != ld.size() || fol[f].p.size() != lp.size() ||
+        fol[f].eager.load() != leader_eager.load()) {
+      std::fprintf(stderr, "selftest: follower %d captured %zu/%zu graphs, %d/%d eager\n", f,
+                   fol[f].d.size() + fol[f].p.size(), ld.size() + lp.size(), fol[f].eager.load(),
+                   leader_eager.load());
+      failures++;
+    }
+    for (auto& kv : ld) {
+      auto it = fol[f].d.find(kv.first);
+      if (it == fol[f].d.end() || it->second->trace != kv.second->trace ||
+          it->second->launches != kv.second->launches) {
+        std::fprintf(stderr, "selftest: follower %d decode graph replays differ\n", f);
+        failures++;
+      }
+    }
+    for (auto& kv : lp) {
+      auto it = fol[f].p.find(kv.first);
+      if (it == fol[f].p.end() || it->second->trace != kv.second->trace ||
+          it->second->launches != kv.second->launches) {
+        std::fprintf(stderr, "selftest: follower %d prefill graph replays differ\n", f);
+        failures++;
+      }
+    }
+  }
+  long k_launch = (long)lm["k_graph_launches"];
+  std::printf("group: checked=%d failures=%d frames=%ld k_graph_launches=%ld eager=%d graphs=%zu\n",
+              checked.load(), failures.load(), (long)lm["mirror_frames"], k_launch,
+              leader_eager.load(), ld.size() + lp.size());
+  return failures.load() == 0 && g_bad.load() == 0 && checked.load() == 80 && k_launch > 0 &&
+                 leader_eager.load() > 0
+             ? 0
+             : 1;
+}
+
 }  // namespace
 
 int main() {
@@ -255,6 +427,7 @@ int main() {
   rc |= run(true, false);
   rc |= run(false, true);
   rc |= run(true, true);
+  rc |= run_group();
   if (rc == 0) std::printf("LOOP_SELFTEST_OK\n");
   return rc;
 }

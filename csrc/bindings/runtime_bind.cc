@@ -54,6 +54,7 @@ void bind_runtime(py::module_& m) {
 #include "runtime/engine_loop.h"
 #include "runtime/hip_dyn.h"
 #include "runtime/loop_capi.h"
+#include "runtime/mirror.h"
 
 namespace {
 
@@ -91,6 +92,83 @@ LoopConfig loop_cfg(const py::dict& d) {
   return c;
 }
 
+DecodeGraphDesc decode_desc(const py::dict& d) {
+  DecodeGraphDesc g;
+  g.B = val_of<int>(d, "B", 0);
+  g.max_pages = val_of<int>(d, "max_pages", 0);
+  g.ctx = val_of<int>(d, "ctx", 0);
+  g.greedy = val_of<bool>(d, "greedy", true);
+  g.exec = ptr_of<void>(d, "exec");
+  g.meta = ptr_of<int32_t>(d, "meta");
+  g.hist = ptr_of<int32_t>(d, "hist");
+  g.max_steps = val_of<int>(d, "max_steps", 0);
+  g.step = ptr_of<int32_t>(d, "step");
+  g.keys = ptr_of<void>(d, "keys");
+  g.keys_bytes = val_of<size_t>(d, "keys_bytes", 0);
+  g.temp = ptr_of<float>(d, "temp");
+  g.topk = ptr_of<int32_t>(d, "topk");
+  g.topp = ptr_of<float>(d, "topp");
+  g.seeds = ptr_of<int64_t>(d, "seeds");
+  g.err = ptr_of<int32_t>(d, "err");
+  g.exec_k = ptr_of<void>(d, "exec_k");
+  g.k_steps = val_of<int>(d, "k_steps", 0);
+  if (!g.exec || !g.meta || !g.hist || !g.step || g.B <= 0 || g.max_steps <= 0 ||
+      (!g.greedy && !(g.temp && g.topk && g.topp && g.seeds)))
+    throw std::runtime_error("add_decode_graph: incomplete description");
+  return g;
+}
+
+PrefillGraphDesc prefill_desc(const py::dict& d) {
+  PrefillGraphDesc g;
+  g.rows = val_of<int>(d, "rows", 0);
+  g.n_seq = val_of<int>(d, "n_seq", 0);
+  g.max_pages = val_of<int>(d, "max_pages", 0);
+  g.qtile = val_of<int>(d, "qtile", 16);
+  g.max_tiles = val_of<int>(d, "max_tiles", 0);
+  g.greedy = val_of<bool>(d, "greedy", true);
+  g.exec = ptr_of<void>(d, "exec");
+  g.meta = ptr_of<int32_t>(d, "meta");
+  g.meta_len = val_of<size_t>(d, "meta_len", 0);
+  g.off_bt = val_of<size_t>(d, "off_bt", 0);
+  g.off_seq = val_of<size_t>(d, "off_seq", 0);
+  g.off_pos = val_of<size_t>(d, "off_pos", 0);
+  g.off_ids = val_of<size_t>(d, "off_ids", 0);
+  g.off_slots = val_of<size_t>(d, "off_slots", 0);
+  g.off_ctx = val_of<size_t>(d, "off_ctx", 0);
+  g.off_out = val_of<size_t>(d, "off_out", 0);
+  g.off_spos = val_of<size_t>(d, "off_spos", 0);
+  g.off_tiles = val_of<size_t>(d, "off_tiles", 0);
+  g.first = ptr_of<int32_t>(d, "first");
+  g.temp = ptr_of<float>(d, "temp");
+  g.topk = ptr_of<int32_t>(d, "topk");
+  g.topp = ptr_of<float>(d, "topp");
+  g.seeds = ptr_of<int64_t>(d, "seeds");
+  g.err = ptr_of<int32_t>(d, "err");
+  if (!g.exec || !g.meta || !g.first || g.rows <= 0 || g.n_seq <= 0 || !g.meta_len ||
+      (!g.greedy && !(g.temp && g.topk && g.topp && g.seeds)))
+    throw std::runtime_error("add_prefill_graph: incomplete description");
+  return g;
+}
+
+EngineLoop::GraphProvider py_provider(py::function f) {
+  auto fn = std::make_shared<py::function>(std::move(f));
+  return [fn](const std::string& kind, int a, int b, bool greedy) {
+    py::gil_scoped_acquire gil;
+    (*fn)(kind, a, b, greedy);
+  };
+}
+
+EngineLoop::EagerPrefill py_eager(py::function f) {
+  auto fn = std::make_shared<py::function>(std::move(f));
+  return [fn](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>& pages,
+              const std::vector<int>& starts, const std::vector<LoopSampling>& samp) {
+    py::gil_scoped_acquire gil;
+    py::list sp;
+    for (auto& s : samp) sp.append(py::make_tuple(s.temperature, s.top_k, s.top_p, s.seed));
+    return py::cast<std::vector<int>>((*fn)(prompts, pages, starts, sp));
+  };
+}
+
 }  // namespace
 
 void bind_engine_loop(py::module_& m) {
@@ -98,86 +176,14 @@ void bind_engine_loop(py::module_& m) {
         "tests: run the native engine loop on host memory with host-function 'graphs'");
   py::class_<EngineLoop>(m, "EngineLoop")
       .def(py::init([](py::dict d) { return new EngineLoop(loop_cfg(d)); }))
-      .def("add_decode_graph",
-           [](EngineLoop& L, py::dict d) {
-             DecodeGraphDesc g;
-             g.B = val_of<int>(d, "B", 0);
-             g.max_pages = val_of<int>(d, "max_pages", 0);
-             g.ctx = val_of<int>(d, "ctx", 0);
-             g.greedy = val_of<bool>(d, "greedy", true);
-             g.exec = ptr_of<void>(d, "exec");
-             g.meta = ptr_of<int32_t>(d, "meta");
-             g.hist = ptr_of<int32_t>(d, "hist");
-             g.max_steps = val_of<int>(d, "max_steps", 0);
-             g.step = ptr_of<int32_t>(d, "step");
-             g.keys = ptr_of<void>(d, "keys");
-             g.keys_bytes = val_of<size_t>(d, "keys_bytes", 0);
-             g.temp = ptr_of<float>(d, "temp");
-             g.topk = ptr_of<int32_t>(d, "topk");
-             g.topp = ptr_of<float>(d, "topp");
-             g.seeds = ptr_of<int64_t>(d, "seeds");
-             g.err = ptr_of<int32_t>(d, "err");
-             g.exec_k = ptr_of<void>(d, "exec_k");
-             g.k_steps = val_of<int>(d, "k_steps", 0);
-             if (!g.exec || !g.meta || !g.hist || !g.step || g.B <= 0 || g.max_steps <= 0 ||
-                 (!g.greedy && !(g.temp && g.topk && g.topp && g.seeds)))
-               throw std::runtime_error("add_decode_graph: incomplete description");
-             L.add_decode_graph(g);
-           })
-      .def("add_prefill_graph",
-           [](EngineLoop& L, py::dict d) {
-             PrefillGraphDesc g;
-             g.rows = val_of<int>(d, "rows", 0);
-             g.n_seq = val_of<int>(d, "n_seq", 0);
-             g.max_pages = val_of<int>(d, "max_pages", 0);
-             g.qtile = val_of<int>(d, "qtile", 16);
-             g.max_tiles = val_of<int>(d, "max_tiles", 0);
-             g.greedy = val_of<bool>(d, "greedy", true);
-             g.exec = ptr_of<void>(d, "exec");
-             g.meta = ptr_of<int32_t>(d, "meta");
-             g.meta_len = val_of<size_t>(d, "meta_len", 0);
-             g.off_bt = val_of<size_t>(d, "off_bt", 0);
-             g.off_seq = val_of<size_t>(d, "off_seq", 0);
-             g.off_pos = val_of<size_t>(d, "off_pos", 0);
-             g.off_ids = val_of<size_t>(d, "off_ids", 0);
-             g.off_slots = val_of<size_t>(d, "off_slots", 0);
-             g.off_ctx = val_of<size_t>(d, "off_ctx", 0);
-             g.off_out = val_of<size_t>(d, "off_out", 0);
-             g.off_spos = val_of<size_t>(d, "off_spos", 0);
-             g.off_tiles = val_of<size_t>(d, "off_tiles", 0);
-             g.first = ptr_of<int32_t>(d, "first");
-             g.temp = ptr_of<float>(d, "temp");
-             g.topk = ptr_of<int32_t>(d, "topk");
-             g.topp = ptr_of<float>(d, "topp");
-             g.seeds = ptr_of<int64_t>(d, "seeds");
-             g.err = ptr_of<int32_t>(d, "err");
-             if (!g.exec || !g.meta || !g.first || g.rows <= 0 || g.n_seq <= 0 || !g.meta_len ||
-                 (!g.greedy && !(g.temp && g.topk && g.topp && g.seeds)))
-               throw std::runtime_error("add_prefill_graph: incomplete description");
-             L.add_prefill_graph(g);
-           })
-      .def("set_provider",
-           [](EngineLoop& L, py::function f) {
-             auto fn = std::make_shared<py::function>(std::move(f));
-             L.set_provider([fn](const std::string& kind, int a, int b, bool greedy) {
-               py::gil_scoped_acquire gil;
-               (*fn)(kind, a, b, greedy);
-             });
-           })
+      .def("add_decode_graph", [](EngineLoop& L, py::dict d) { L.add_decode_graph(decode_desc(d)); })
+      .def("add_prefill_graph", [](EngineLoop& L, py::dict d) { L.add_prefill_graph(prefill_desc(d)); })
+      .def("set_provider", [](EngineLoop& L, py::function f) { L.set_provider(py_provider(f)); })
       .def("set_eager_prefill",
-           [](EngineLoop& L, py::function f) {
-             auto fn = std::make_shared<py::function>(std::move(f));
-             L.set_eager_prefill([fn](const std::vector<std::vector<int>>& prompts,
-                                      const std::vector<std::vector<int>>& pages,
-                                      const std::vector<int>& starts,
-                                      const std::vector<LoopSampling>& samp) {
-               py::gil_scoped_acquire gil;
-               py::list sp;
-               for (auto& s : samp)
-                 sp.append(py::make_tuple(s.temperature, s.top_k, s.top_p, s.seed));
-               return py::cast<std::vector<int>>((*fn)(prompts, pages, starts, sp));
-             });
-           })
+           [](EngineLoop& L, py::function f) { L.set_eager_prefill(py_eager(f)); })
+      // TP / EP group leader: record every device operation for the followers (mirror.h)
+      .def("set_mirror", &EngineLoop::set_mirror)
+      .def("mirror_provide", &EngineLoop::mirror_provide, py::call_guard<py::gil_scoped_release>())
       .def("start", &EngineLoop::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &EngineLoop::stop, py::call_guard<py::gil_scoped_release>())
       .def("shutdown", &EngineLoop::shutdown, py::call_guard<py::gil_scoped_release>())
@@ -234,4 +240,14 @@ void bind_engine_loop(py::module_& m) {
       .def("handle", [](EngineLoop& L) { return (uintptr_t)&L; });
   // address of the plain-C table (runtime/loop_capi.h) of the loop code in THIS module
   m.def("loop_api", []() { return (uintptr_t)p2p_loop_api(); });
+  // TP / EP group follower: applies the leader loop's device operations (mirror.h)
+  py::class_<EngineMirror>(m, "EngineMirror")
+      .def(py::init<int, int>(), py::arg("fd"), py::arg("device"))
+      .def("add_decode_graph", [](EngineMirror& M, py::dict d) { M.add_decode_graph(decode_desc(d)); })
+      .def("add_prefill_graph", [](EngineMirror& M, py::dict d) { M.add_prefill_graph(prefill_desc(d)); })
+      .def("set_provider", [](EngineMirror& M, py::function f) { M.set_provider(py_provider(f)); })
+      .def("set_eager_prefill", [](EngineMirror& M, py::function f) { M.set_eager_prefill(py_eager(f)); })
+      .def("run", &EngineMirror::run, py::call_guard<py::gil_scoped_release>())
+      .def("metrics", &EngineMirror::metrics)
+      .def("shutdown", &EngineMirror::shutdown, py::call_guard<py::gil_scoped_release>());
 }

@@ -7,6 +7,7 @@
 
 #include "runtime/hip_dyn.h"
 #include "runtime/loop_capi.h"
+#include "runtime/mirror.h"
 
 namespace p2p {
 
@@ -89,6 +90,16 @@ void EngineLoop::add_prefill_graph(const PrefillGraphDesc& d) {
 }
 
 void EngineLoop::set_provider(GraphProvider p) { provider_ = std::move(p); }
+
+void EngineLoop::set_mirror(const std::vector<int>& fds) {
+  mirror_ = fds.empty() ? nullptr : std::make_unique<MirrorSender>(fds);
+}
+
+void EngineLoop::mirror_provide(const std::string& kind, int a, int b, bool greedy) {
+  if (!mirror_) return;
+  mirror_->provide(kind == "decode" ? 'D' : 'P', a, b, greedy);
+  mirror_->flush();
+}
 void EngineLoop::set_eager_prefill(EagerPrefill f) { eager_ = std::move(f); }
 
 const DecodeGraphDesc* EngineLoop::decode_graph(int B, int ctx, bool greedy) {
@@ -156,6 +167,13 @@ void EngineLoop::stop() {
   cv_.notify_all();
   done_cv_.notify_all();
   if (th_.joinable()) th_.join();
+  if (mirror_ && !mirror_stopped_) {  // the followers' mirrors return from run()
+    mirror_stopped_ = true;
+    try {
+      mirror_->stop();
+    } catch (...) {
+    }
+  }
 }
 
 int64_t EngineLoop::submit(const std::vector<int>& prompt, int max_new, bool stop_on_eos,
@@ -280,6 +298,10 @@ std::map<std::string, double> EngineLoop::metrics() {
   m["waiting"] = sched_.n_waiting();
   m["free_kv_pages"] = sched_.free_pages();
   m["native_loop"] = 1;
+  if (mirror_) {
+    m["mirror_frames"] = mirror_->frames();
+    m["mirror_bytes"] = mirror_->bytes();
+  }
   return m;
 }
 
@@ -383,6 +405,11 @@ void EngineLoop::step() {
   int done = 0;
   {
     std::lock_guard<std::mutex> lk(mu_);
+    // pages of requests that ended without a decode chunk after them (a 1-token reply, a
+    // cancel, a reply that ended in its prefill) wait in the deferred list for the next
+    // collect(); with nothing in flight nothing can still write them: free them now (else
+    // an idle loop holds them until the next request decodes)
+    if (flight_.empty()) sched_.flush_deferred();
     const int64_t t = now_ns();
     for (int64_t id : sched_.take_finished()) {
       auto it = reqs_.find(id);
@@ -502,6 +529,10 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
     }
     riders.clear();
     const int64_t te = now_ns();
+    if (mirror_) {  // the followers run the same eager prefill (its collectives pair up)
+      mirror_->eager(prompts, pages, starts, samp);
+      mirror_->flush();
+    }
     first = eager_(prompts, pages, starts, samp);
     eager_ns_ += now_ns() - te;
     n_eager_prefill_++;
@@ -577,6 +608,18 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
       hip_check(h.memcpyAsync(g->topk, tk, S * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->topp, tp, S * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->seeds, sd, S * 8, kH2D, stream_), "samp H2D");
+    }
+    if (mirror_) {
+      const char K = 'P';
+      mirror_->h2d(K, g->rows, g->n_seq, g->greedy, kFMeta, m, g->meta_len * 4);
+      if (!g->greedy) {
+        mirror_->h2d(K, g->rows, g->n_seq, g->greedy, kFTemp, pinned_[kSampF].first, S * 4);
+        mirror_->h2d(K, g->rows, g->n_seq, g->greedy, kFTopk, pinned_[kSampI].first, S * 4);
+        mirror_->h2d(K, g->rows, g->n_seq, g->greedy, kFTopp, pinned_[kSampP].first, S * 4);
+        mirror_->h2d(K, g->rows, g->n_seq, g->greedy, kFSeeds, pinned_[kSampS].first, S * 8);
+      }
+      mirror_->launch(K, g->rows, g->n_seq, g->greedy, 0, 1);
+      mirror_->flush();
     }
     hip_check(h.graphLaunch(g->exec, stream_), "prefill graph launch");
     int32_t* f = (int32_t*)pinned(kFirst, S * 4);
@@ -664,6 +707,18 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
       hip_check(h.memcpyAsync(g->topp, tp, B * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->seeds, sd, B * 8, kH2D, stream_), "samp H2D");
     }
+    if (mirror_) {
+      const char K = 'D';
+      mirror_->h2d(K, g->B, g->ctx, g->greedy, kFMeta, m, n * 4);
+      mirror_->memset0(K, g->B, g->ctx, g->greedy, kFStep, 4);
+      if (g->keys && g->keys_bytes) mirror_->memset0(K, g->B, g->ctx, g->greedy, kFKeys, g->keys_bytes);
+      if (!g->greedy) {
+        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTemp, pinned_[kSampF].first, B * 4);
+        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTopk, pinned_[kSampI].first, B * 4);
+        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTopp, pinned_[kSampP].first, B * 4);
+        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFSeeds, pinned_[kSampS].first, B * 8);
+      }
+    }
     loaded_ = g;
     loaded_ids_ = ids;
     loaded_steps_ = 0;
@@ -671,13 +726,18 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
   }
   // k steps: whole k_steps-step graphs first (each one-step launch leaves host work that
   // the next launch of the prompt-chunk graph pays: ~8 us per launch, bench/graph_switch_probe.py)
-  int left = k;
-  if (g->exec_k && g->k_steps > 1)
-    for (; left >= g->k_steps; left -= g->k_steps) {
-      hip_check(h.graphLaunch(g->exec_k, stream_), "decode graph launch");
-      n_k_graph_launches_++;
-    }
-  for (; left > 0; --left) hip_check(h.graphLaunch(g->exec, stream_), "decode graph launch");
+  const int nk = (g->exec_k && g->k_steps > 1) ? k / g->k_steps : 0;
+  const int n1 = k - nk * g->k_steps;
+  if (mirror_) {  // the followers replay the same graphs (their collectives pair with ours)
+    if (nk) mirror_->launch('D', g->B, g->ctx, g->greedy, 1, (uint32_t)nk);
+    if (n1) mirror_->launch('D', g->B, g->ctx, g->greedy, 0, (uint32_t)n1);
+    mirror_->flush();
+  }
+  for (int i = 0; i < nk; ++i) {
+    hip_check(h.graphLaunch(g->exec_k, stream_), "decode graph launch");
+    n_k_graph_launches_++;
+  }
+  for (int i = 0; i < n1; ++i) hip_check(h.graphLaunch(g->exec, stream_), "decode graph launch");
   Chunk c;
   c.g = g;
   c.ids = ids;
@@ -734,6 +794,13 @@ void EngineLoop::on_fault(int32_t* err, const char* where) {
   const HipApi& h = hip_api();
   (void)h.memsetAsync(err, 0, 4, stream_);
   (void)h.streamSynchronize(stream_);
+  if (mirror_) {  // a group's fault words are set together (a peer's spin gave up too)
+    try {
+      mirror_->faults();
+      mirror_->flush();
+    } catch (...) {
+    }
+  }
   loaded_ = nullptr;
   const std::string why = std::string("kernel fault word set during ") + where +
                           " (results invalid)";

@@ -38,6 +38,8 @@
 
 namespace p2p {
 
+class MirrorSender;  // runtime/mirror.h
+
 struct LoopSampling {
   float temperature = 0.f;  // <= 0: greedy
   int top_k = 40;
@@ -128,6 +130,12 @@ class EngineLoop {
   void add_prefill_graph(const PrefillGraphDesc& d);
   void set_provider(GraphProvider p);
   void set_eager_prefill(EagerPrefill f);
+  // TP / EP group leader: every device operation of the loop (metadata copies, counter
+  // resets, graph replays, eager prefills) is also sent to the followers' EngineMirror over
+  // these channel fds (owned by the caller), one frame per step (runtime/mirror.h)
+  void set_mirror(const std::vector<int>& fds);
+  // a graph provider about to capture (kind, a, b, greedy): the followers capture it too
+  void mirror_provide(const std::string& kind, int a, int b, bool greedy);
   void start();
   void stop();
   void shutdown();  // stop + release the loop's HIP resources (stream, events, pinned memory)
@@ -198,6 +206,8 @@ class EngineLoop {
   std::map<std::tuple<int, int, bool>, int> puses_;  // uses of not-yet-captured chunk shapes
   GraphProvider provider_;
   EagerPrefill eager_;
+  std::unique_ptr<MirrorSender> mirror_;
+  bool mirror_stopped_ = false;
 
   // device-side state of the loop thread
   void* stream_ = nullptr;

@@ -1,0 +1,352 @@
+// Leader -> follower replay of the native engine loop's device operations (mirror.h).
+#include "runtime/mirror.h"
+
+#include <errno.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <stdexcept>
+
+#include "runtime/hip_dyn.h"
+
+namespace p2p {
+
+namespace {
+
+void write_all(int fd, const char* p, size_t n) {
+  while (n > 0) {
+    ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
+    if (w < 0 && errno == ENOTSOCK) w = write(fd, p, n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw std::runtime_error(std::string("group channel write failed: ") + strerror(errno));
+    }
+    p += w;
+    n -= (size_t)w;
+  }
+}
+
+// false on a clean EOF before the first byte
+bool read_exact(int fd, char* p, size_t n) {
+  size_t got = 0;
+  while (got < n) {
+    ssize_t r = read(fd, p + got, n - got);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      throw std::runtime_error(std::string("group channel read failed: ") + strerror(errno));
+    }
+    if (r == 0) {
+      if (got == 0) return false;
+      throw std::runtime_error("group channel closed mid-frame");
+    }
+    got += (size_t)r;
+  }
+  return true;
+}
+
+struct Reader {
+  const std::string& s;
+  size_t i = 0;
+  template <class T>
+  T get() {
+    if (i + sizeof(T) > s.size()) throw std::runtime_error("mirror frame truncated");
+    T v;
+    memcpy(&v, s.data() + i, sizeof(T));
+    i += sizeof(T);
+    return v;
+  }
+  const char* bytes(size_t n) {
+    if (i + n > s.size()) throw std::runtime_error("mirror frame truncated");
+    const char* p = s.data() + i;
+    i += n;
+    return p;
+  }
+  std::vector<int> ints() {
+    const uint32_t n = get<uint32_t>();
+    std::vector<int> v(n);
+    if (n) memcpy(v.data(), bytes((size_t)n * 4), (size_t)n * 4);
+    return v;
+  }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------ leader
+void MirrorSender::head(char op, char kind, int a, int b, bool greedy) {
+  put<char>(op);
+  put<char>(kind);
+  put<int32_t>(a);
+  put<int32_t>(b);
+  put<uint8_t>(greedy ? 1 : 0);
+}
+
+void MirrorSender::h2d(char kind, int a, int b, bool greedy, uint8_t field, const void* src,
+                       size_t n) {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  head('H', kind, a, b, greedy);
+  put<uint8_t>(field);
+  put<uint32_t>((uint32_t)n);
+  buf_.append((const char*)src, n);
+}
+
+void MirrorSender::memset0(char kind, int a, int b, bool greedy, uint8_t field, size_t n) {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  head('M', kind, a, b, greedy);
+  put<uint8_t>(field);
+  put<uint32_t>((uint32_t)n);
+}
+
+void MirrorSender::launch(char kind, int a, int b, bool greedy, uint8_t which, uint32_t count) {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  head('L', kind, a, b, greedy);
+  put<uint8_t>(which);
+  put<uint32_t>(count);
+}
+
+void MirrorSender::faults() {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  put<char>('F');
+}
+
+void MirrorSender::provide(char kind, int a, int b, bool greedy) {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  head('V', kind, a, b, greedy);
+}
+
+void MirrorSender::eager(const std::vector<std::vector<int>>& prompts,
+                         const std::vector<std::vector<int>>& pages, const std::vector<int>& starts,
+                         const std::vector<LoopSampling>& samp) {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  put<char>('E');
+  put<uint32_t>((uint32_t)prompts.size());
+  for (size_t i = 0; i < prompts.size(); ++i) {
+    put<uint32_t>((uint32_t)prompts[i].size());
+    buf_.append((const char*)prompts[i].data(), prompts[i].size() * 4);
+    const std::vector<int>& pg = i < pages.size() ? pages[i] : std::vector<int>();
+    put<uint32_t>((uint32_t)pg.size());
+    buf_.append((const char*)pg.data(), pg.size() * 4);
+    put<int32_t>(i < starts.size() ? starts[i] : 0);
+    const LoopSampling s = i < samp.size() ? samp[i] : LoopSampling();
+    put<float>(s.temperature);
+    put<int32_t>(s.top_k);
+    put<float>(s.top_p);
+    put<int64_t>(s.seed);
+  }
+}
+
+void MirrorSender::stop() {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  put<char>('S');
+  flush();
+}
+
+void MirrorSender::flush() {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  if (buf_.empty()) return;
+  const uint32_t n = (uint32_t)buf_.size();
+  std::string frame(reinterpret_cast<const char*>(&n), 4);
+  frame += buf_;
+  buf_.clear();
+  for (int fd : fds_) write_all(fd, frame.data(), frame.size());
+  frames_++;
+  bytes_ += (long)frame.size();
+}
+
+// ------------------------------------------------------------------ follower
+EngineMirror::~EngineMirror() {}
+
+void EngineMirror::shutdown() {
+  const HipApi& h = hip_api();
+  if (!h.ok) return;
+  for (int i = 0; i < 2; ++i) {
+    if (stage_[i]) h.hostFree(stage_[i]);
+    if (stage_ev_[i]) h.eventDestroy(stage_ev_[i]);
+    stage_[i] = stage_ev_[i] = nullptr;
+    stage_n_[i] = 0;
+  }
+  if (stream_) h.streamDestroy(stream_);
+  stream_ = nullptr;
+}
+
+void EngineMirror::add_decode_graph(const DecodeGraphDesc& d) {
+  Graph g;
+  g.kind = 'D';
+  g.a = d.B;
+  g.b = d.ctx;
+  g.greedy = d.greedy;
+  g.exec = d.exec;
+  g.exec_k = d.exec_k;
+  g.fields[kFMeta] = d.meta;
+  g.fields[kFStep] = d.step;
+  g.fields[kFKeys] = d.keys;
+  g.fields[kFTemp] = d.temp;
+  g.fields[kFTopk] = d.topk;
+  g.fields[kFTopp] = d.topp;
+  g.fields[kFSeeds] = d.seeds;
+  g.err = d.err;
+  std::lock_guard<std::mutex> lk(gmu_);
+  graphs_[std::make_tuple('D', g.a, g.b, g.greedy)] = g;
+}
+
+void EngineMirror::add_prefill_graph(const PrefillGraphDesc& d) {
+  Graph g;
+  g.kind = 'P';
+  g.a = d.rows;
+  g.b = d.n_seq;
+  g.greedy = d.greedy;
+  g.exec = d.exec;
+  g.fields[kFMeta] = d.meta;
+  g.fields[kFTemp] = d.temp;
+  g.fields[kFTopk] = d.topk;
+  g.fields[kFTopp] = d.topp;
+  g.fields[kFSeeds] = d.seeds;
+  g.err = d.err;
+  std::lock_guard<std::mutex> lk(gmu_);
+  graphs_[std::make_tuple('P', g.a, g.b, g.greedy)] = g;
+}
+
+EngineMirror::Graph* EngineMirror::find(char kind, int a, int b, bool greedy) {
+  std::lock_guard<std::mutex> lk(gmu_);
+  auto it = graphs_.find(std::make_tuple(kind, a, b, greedy));
+  if (it == graphs_.end())
+    throw std::runtime_error(std::string("mirror: no ") + (kind == 'D' ? "decode" : "prefill") +
+                             " graph (" + std::to_string(a) + ", " + std::to_string(b) + ", " +
+                             (greedy ? "greedy" : "sampled") + ") on this rank");
+  return &it->second;
+}
+
+void* EngineMirror::staging(size_t n) {
+  const HipApi& h = hip_api();
+  const int i = cur_;
+  if (stage_ev_[i]) hip_check(h.eventSynchronize(stage_ev_[i]), "mirror staging reuse");
+  if (stage_n_[i] < n) {
+    if (stage_[i]) h.hostFree(stage_[i]);
+    stage_[i] = nullptr;
+    const size_t sz = std::max(n, (size_t)1 << 16);
+    hip_check(h.hostMalloc(&stage_[i], sz, 0), "mirror staging");
+    stage_n_[i] = sz;
+  }
+  return stage_[i];
+}
+
+std::map<std::string, double> EngineMirror::metrics() {
+  std::map<std::string, double> m;
+  m["mirror_frames"] = n_frames_;
+  m["mirror_launches"] = n_launches_;
+  m["mirror_provides"] = n_provides_;
+  m["mirror_eager"] = n_eager_;
+  std::lock_guard<std::mutex> lk(gmu_);
+  m["mirror_graphs"] = (double)graphs_.size();
+  return m;
+}
+
+void EngineMirror::apply(const std::string& frame) {
+  const HipApi& h = hip_api();
+  // h2d payloads of this frame go through one pinned staging buffer (copied up front)
+  char* st = (char*)staging(frame.size());
+  memcpy(st, frame.data(), frame.size());
+  Reader r{frame};
+  bool used_stage = false;
+  while (r.i < frame.size()) {
+    const char op = r.get<char>();
+    if (op == 'S') {
+      throw std::string("");  // stop: handled by run()
+    }
+    if (op == 'F') {
+      std::lock_guard<std::mutex> lk(gmu_);
+      for (auto& kv : graphs_)
+        if (kv.second.err) hip_check(h.memsetAsync(kv.second.err, 0, 4, stream_), "mirror fault reset");
+      continue;
+    }
+    if (op == 'E') {
+      const uint32_t n = r.get<uint32_t>();
+      std::vector<std::vector<int>> prompts, pages;
+      std::vector<int> starts;
+      std::vector<LoopSampling> samp;
+      for (uint32_t i = 0; i < n; ++i) {
+        prompts.push_back(r.ints());
+        pages.push_back(r.ints());
+        starts.push_back(r.get<int32_t>());
+        LoopSampling s;
+        s.temperature = r.get<float>();
+        s.top_k = r.get<int32_t>();
+        s.top_p = r.get<float>();
+        s.seed = r.get<int64_t>();
+        samp.push_back(s);
+      }
+      if (!eager_) throw std::runtime_error("mirror: no eager prefill callback");
+      hip_check(h.streamSynchronize(stream_), "mirror sync");  // the model code runs on its stream
+      eager_(prompts, pages, starts, samp);
+      n_eager_++;
+      continue;
+    }
+    const char kind = r.get<char>();
+    const int a = r.get<int32_t>(), b = r.get<int32_t>();
+    const bool greedy = r.get<uint8_t>() != 0;
+    if (op == 'V') {
+      if (!provider_) throw std::runtime_error("mirror: no graph provider");
+      hip_check(h.streamSynchronize(stream_), "mirror sync");
+      provider_(kind == 'D' ? "decode" : "prefill", a, b, greedy);
+      n_provides_++;
+      (void)find(kind, a, b, greedy);  // the provider must have registered it
+      continue;
+    }
+    Graph* g = find(kind, a, b, greedy);
+    if (op == 'H') {
+      const uint8_t f = r.get<uint8_t>();
+      const uint32_t n = r.get<uint32_t>();
+      const size_t off = r.i;
+      (void)r.bytes(n);
+      if (f > kFSeeds || !g->fields[f]) throw std::runtime_error("mirror: bad h2d field");
+      hip_check(h.memcpyAsync(g->fields[f], st + off, n, kH2D, stream_), "mirror h2d");
+      used_stage = true;
+    } else if (op == 'M') {
+      const uint8_t f = r.get<uint8_t>();
+      const uint32_t n = r.get<uint32_t>();
+      if (f > kFSeeds || !g->fields[f]) throw std::runtime_error("mirror: bad memset field");
+      hip_check(h.memsetAsync(g->fields[f], 0, n, stream_), "mirror memset");
+    } else if (op == 'L') {
+      const uint8_t which = r.get<uint8_t>();
+      const uint32_t count = r.get<uint32_t>();
+      void* ex = which ? g->exec_k : g->exec;
+      if (!ex) throw std::runtime_error("mirror: graph has no such exec");
+      for (uint32_t i = 0; i < count; ++i) hip_check(h.graphLaunch(ex, stream_), "mirror launch");
+      n_launches_ += count;
+    } else {
+      throw std::runtime_error(std::string("mirror: unknown op ") + op);
+    }
+  }
+  if (used_stage) {
+    if (!stage_ev_[cur_]) hip_check(h.eventCreateWithFlags(&stage_ev_[cur_], 2), "mirror event");
+    hip_check(h.eventRecord(stage_ev_[cur_], stream_), "mirror event");
+    cur_ ^= 1;
+  }
+}
+
+std::string EngineMirror::run() {
+  const HipApi& h = hip_api();
+  try {
+    if (!h.ok) throw std::runtime_error("mirror: " + h.error);
+    hip_check(h.setDevice(device_), "hipSetDevice");
+    if (!stream_) hip_check(h.streamCreateWithFlags(&stream_, 1), "hipStreamCreate");
+    std::string frame;
+    while (true) {
+      uint32_t n = 0;
+      if (!read_exact(fd_, (char*)&n, 4)) throw std::runtime_error("group channel closed (leader gone)");
+      frame.resize(n);
+      if (n && !read_exact(fd_, &frame[0], n)) throw std::runtime_error("group channel closed");
+      n_frames_++;
+      try {
+        apply(frame);
+      } catch (const std::string&) {  // stop
+        hip_check(h.streamSynchronize(stream_), "mirror drain");
+        return "";
+      }
+    }
+  } catch (const std::exception& e) {
+    return e.what();
+  }
+}
+
+}  // namespace p2p

@@ -1,0 +1,130 @@
+// Native serving loop for TP / EP groups: the leader's EngineLoop drives its followers.
+//
+// Every rank of a group captured the same graphs (same shapes, same collectives), so a
+// group step is the same sequence of device operations on every rank: copy the step's
+// metadata into a graph's input buffers, reset its counters, replay it.  The leader's loop
+// (engine_loop.cc) records each of those operations as it performs them -- a few hundred
+// bytes per prefill chunk or decode chunk -- and sends them, one frame per step, over the
+// group's host channel (the socketpair that connects the leader and each follower process);
+// a follower's EngineMirror thread applies them in order on its own stream to its own
+// graphs, so the collectives inside the graphs line up without any Python in the loop on
+// either side.  Operations that need the model code -- capturing a graph for a new shape,
+// the eager prefill of a prompt longer than every captured chunk -- travel the same
+// channel, in order, and call back into the follower's Python (graph provider / eager
+// prefill), exactly as the leader's loop calls its own.
+//
+// Replaces the Python LockstepEngine broadcast of round 4 (engine/cluster.py) on the hot
+// path: no pickled plan per call, no host sync per decode chunk on the followers, and the
+// multi-step decode graphs (captured collectively, through the same provider calls) serve
+// groups too.  (The reference has no parallelism; this serves BASELINE configs 3 and 5,
+// the same click as `web/streamlit_app.py:161-173`.)
+//
+// Frame: u32 length (little endian) + payload; payload = a sequence of records
+//   'H' h2d      kind a b greedy field n data[n]   (copy into the graph's field buffer)
+//   'M' memset0  kind a b greedy field n            (zero n bytes of a field)
+//   'L' launch   kind a b greedy which count        (which 0: one-step exec, 1: exec_k)
+//   'F' faults                                      (zero every graph's fault word)
+//   'V' provide  kind a b greedy                    (capture + register this shape)
+//   'E' eager    n_seq {prompt, pages, start, sampling} x n_seq
+//   'S' stop
+// kind: 'D' decode graph (B, ctx bucket), 'P' prefill graph (rows, seq bucket).
+#pragma once
+#include <stdint.h>
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "runtime/engine_loop.h"
+
+namespace p2p {
+
+enum MirrorField : uint8_t {
+  kFMeta = 0,
+  kFStep = 1,
+  kFKeys = 2,
+  kFTemp = 3,
+  kFTopk = 4,
+  kFTopp = 5,
+  kFSeeds = 6,
+};
+
+class MirrorSender {
+ public:
+  explicit MirrorSender(std::vector<int> fds) : fds_(std::move(fds)) {}
+  void h2d(char kind, int a, int b, bool greedy, uint8_t field, const void* src, size_t n);
+  void memset0(char kind, int a, int b, bool greedy, uint8_t field, size_t n);
+  void launch(char kind, int a, int b, bool greedy, uint8_t which, uint32_t count);
+  void faults();
+  void provide(char kind, int a, int b, bool greedy);
+  void eager(const std::vector<std::vector<int>>& prompts,
+             const std::vector<std::vector<int>>& pages, const std::vector<int>& starts,
+             const std::vector<LoopSampling>& samp);
+  void stop();
+  void flush();  // one frame to every follower; throws if a channel is broken
+  long frames() const { return frames_; }
+  long bytes() const { return bytes_; }
+
+ private:
+  void head(char op, char kind, int a, int b, bool greedy);
+  template <class T>
+  void put(T v) {
+    buf_.append(reinterpret_cast<const char*>(&v), sizeof(T));
+  }
+  std::vector<int> fds_;
+  std::string buf_;
+  std::recursive_mutex mu_;
+  std::atomic<long> frames_{0}, bytes_{0};
+};
+
+class EngineMirror {
+ public:
+  EngineMirror(int fd, int device) : fd_(fd), device_(device) {}
+  ~EngineMirror();
+  EngineMirror(const EngineMirror&) = delete;
+  EngineMirror& operator=(const EngineMirror&) = delete;
+
+  void add_decode_graph(const DecodeGraphDesc& d);
+  void add_prefill_graph(const PrefillGraphDesc& d);
+  void set_provider(EngineLoop::GraphProvider p) { provider_ = std::move(p); }
+  void set_eager_prefill(EngineLoop::EagerPrefill f) { eager_ = std::move(f); }
+  // Applies frames until the leader's stop ("" returned) or a failure (its description:
+  // a closed channel, an unknown graph, a HIP error).  Blocking; call without the GIL.
+  std::string run();
+  std::map<std::string, double> metrics();
+  void shutdown();  // release the stream and staging buffers
+
+ private:
+  struct Graph {
+    char kind;
+    int a, b;
+    bool greedy;
+    void* exec = nullptr;
+    void* exec_k = nullptr;
+    void* fields[7] = {};
+    int32_t* err = nullptr;
+  };
+  Graph* find(char kind, int a, int b, bool greedy);
+  void apply(const std::string& frame);
+  void* staging(size_t n);
+
+  int fd_, device_;
+  void* stream_ = nullptr;
+  std::mutex gmu_;
+  std::map<std::tuple<char, int, int, bool>, Graph> graphs_;
+  EngineLoop::GraphProvider provider_;
+  EngineLoop::EagerPrefill eager_;
+  // double-buffered pinned staging of the frames' h2d payloads: buffer i is reused only
+  // once the operations of the frame that last used it completed (its event)
+  void* stage_[2] = {nullptr, nullptr};
+  size_t stage_n_[2] = {0, 0};
+  void* stage_ev_[2] = {nullptr, nullptr};
+  int cur_ = 0;
+  std::atomic<long> n_frames_{0}, n_launches_{0}, n_provides_{0}, n_eager_{0};
+};
+
+}  // namespace p2p

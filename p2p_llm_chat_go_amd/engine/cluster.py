@@ -286,6 +286,11 @@ def _follower_loop(eng, conn):
         elif op == "generate":
             _, prompts, n, eos, every = msg
             eng.generate(prompts, n, eos, every)
+        elif op == "mirror":  # the native group loop: the leader's frames from here on
+            from .native_loop import run_follower_mirror
+
+            run_follower_mirror(eng, conn.fileno(), msg[1])
+            return
         elif op == "prefill_part":  # dp_split: this rank's share, result back to the leader
             _, prompts, bts, ret, sampling, starts, pad = msg
             res = eng.prefill(prompts, bts, return_logits=ret, sampling=sampling, starts=starts,
@@ -353,7 +358,8 @@ def _rank_main(spec, replica, rank, device, port, parent_conn, follower_conns, l
             import torch.distributed as dist
 
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-            backend = "nccl" if device.startswith("cuda") else "gloo"
+            # virtual ranks (tests: a whole group on ONE device) cannot share RCCL's device
+            backend = "nccl" if device.startswith("cuda") and not spec.get("virtual") else "gloo"
             kw = {"device_id": torch.device(device)} if backend == "nccl" else {}
             dist.init_process_group(backend, rank=rank, world_size=group,
                                     timeout=datetime.timedelta(seconds=spec.get("pg_timeout", 600)),
@@ -385,17 +391,25 @@ def _leader_main(spec, replica, eng, parent_conn, follower_conns):
     from .server import EngineServer
     from .tokenizer import get_tokenizer
 
+    from .native_loop import PREFILL_CTX, NativeEngineServer, group_native_ok, make_server
+
     group = spec.get("tp", 1) * spec.get("ep", 1)
     split = spec.get("ep", 1) > 1 and spec.get("ep_mode", "allreduce") == "a2a"
     front = LockstepEngine(eng, follower_conns, dp_split=split) if group > 1 else eng
     tok = get_tokenizer(eng.cfg, spec.get("tokenizer") or spec.get("checkpoint"))
     kw = dict(model_name=spec.get("model_name", "llama3.1"),
               default_max_tokens=spec.get("max_tokens", 128))
+    mirror = group > 1 and group_native_ok(eng, split)
     if group == 1:  # a single-GPU replica runs the native step loop when it can
-        from .native_loop import make_server
-
         server = make_server(eng, tok, **kw)
-    else:  # TP/EP groups: the Python loop, whose calls the leader broadcasts
+    elif mirror:
+        # TP / EP group on the native loop: the followers switch to their EngineMirror (the
+        # channels carry the leader loop's frames from now on, runtime/mirror.h)
+        for c in follower_conns:
+            c.send(("mirror", PREFILL_CTX))
+        server = NativeEngineServer(eng, tok, mirror_fds=[c.fileno() for c in follower_conns],
+                                    **kw)
+    else:  # EP a2a (DP attention): the Python loop, whose calls the leader broadcasts
         server = EngineServer(front, tok, **kw)
     send_lock = threading.Lock()
     cancelled = set()
@@ -446,8 +460,8 @@ def _leader_main(spec, replica, eng, parent_conn, follower_conns):
             cancelled.add(msg[1])
             continue
         threading.Thread(target=run, args=(op, msg[1], msg[2]), daemon=True).start()
-    server.close()
-    if group > 1:
+    server.close()  # (native group loop: its stop frame ends the followers' mirrors)
+    if group > 1 and not mirror:
         front.stop()
     os._exit(0)
 
@@ -473,7 +487,8 @@ class ClusterServer:
                  max_batch: int = 16, max_tokens: int = 128, model_name: str = "llama3.1",
                  weights: str | None = None, tokenizer: str | None = None, sd_seed=None,
                  kv_pages=None, warmup: bool = True, start_timeout: float = 1800.0,
-                 first_gpu: int = 0, checkpoint: str | None = None, ep_mode: str = "allreduce"):
+                 first_gpu: int = 0, checkpoint: str | None = None, ep_mode: str = "allreduce",
+                 virtual_ranks: bool = False):
         import multiprocessing as mp
 
         group = tp * ep
@@ -484,7 +499,7 @@ class ClusterServer:
         spec = dict(model=model, tp=tp, ep=ep, max_batch=max_batch, max_tokens=max_tokens,
                     model_name=model_name, weights=weights, tokenizer=tokenizer, sd_seed=sd_seed,
                     kv_pages=kv_pages, warmup=warmup, world=gpus, checkpoint=checkpoint or None,
-                    ep_mode=ep_mode)
+                    ep_mode=ep_mode, virtual=virtual_ranks)
         ctx = mp.get_context("spawn")
         self._replicas = []
         self._rid = itertools.count(1)
@@ -498,6 +513,8 @@ class ClusterServer:
             procs = []
             for k in range(group):
                 dev = "cuda:%d" % (first_gpu + r * group + k) if device == "cuda" else "cpu"
+                if device == "cuda" and virtual_ranks:  # tests: every rank on one device
+                    dev = "cuda:%d" % first_gpu
                 if k == 0:
                     args = (spec, r, 0, dev, port, leader_end, [p[0] for p in pipes], None)
                 else:

@@ -105,8 +105,17 @@ class Engine:
         self._graphs = {}
         # graph-captured prefill chunks (engine.graph.PrefillGraph): dense TP=1 engines on
         # the GPU; P2P_PREFILL_GRAPH=0 keeps every prefill eager
+        # TP groups: chunks whose every collective runs on the one-shot IPC kernels (the
+        # row-parallel sums fit the IPC buffer: rows x hidden x 2 bytes), so the graph holds
+        # no host-side collective; longer chunks stay eager.  Every rank decides alike (same
+        # calls, same use counts), so the group's graphs pair up.
+        car = getattr(comm, "car", None)
+        self.prefill_graph_max_rows = PREFILL_ROW_BUCKETS[-1]
+        if tp_size > 1:
+            self.prefill_graph_max_rows = (car.max_bytes // (2 * cfg.hidden)) if car is not None else 0
         self.prefill_graphs_enabled = (
-            use_graph and self.device.type == "cuda" and tp_size == 1 and not cfg.is_moe
+            use_graph and self.device.type == "cuda" and not cfg.is_moe
+            and (tp_size == 1 or self.prefill_graph_max_rows >= PREFILL_ROW_BUCKETS[0])
             and os.environ.get("P2P_PREFILL_GRAPH", "1") != "0")
         self._pgraphs = {}
         # a chunk shape is captured once it has been seen this many times (eager before):
@@ -164,7 +173,7 @@ class Engine:
     def _graph_prefill_ok(self, n_rows: int, B: int, max_ctx: int, n_dummy: int,
                           return_logits: bool) -> bool:
         return (self.prefill_graphs_enabled and not return_logits and not n_dummy
-                and n_rows <= min(self.max_prefill_tokens, PREFILL_ROW_BUCKETS[-1])
+                and n_rows <= min(self.max_prefill_tokens, self.prefill_graph_max_rows)
                 and B <= self.max_batch and max_ctx <= CTX_BUCKETS[-1])
 
     def autotune(self, batch_sizes=(1,), verbose=False):

@@ -131,11 +131,15 @@ class DecodeGraph:
         self.graph = None
         self.greedy = greedy
         self.use_graph = use_graph and state.model.device.type == "cuda"
-        # multi-step graph (see _capture_steps): single-device engines only -- a TP / EP
-        # group would have to capture it collectively
+        # multi-step graph (see _capture_steps).  A TP / EP group captures it collectively:
+        # every rank captures the same K steps for the same shapes (the Python lockstep
+        # replays the same n on every rank; the native group loop mirrors the leader's
+        # provider calls), and the IPC collectives keep their epochs on the device, so K
+        # recorded steps replay like K launches (P2P_GROUP_GRAPH_STEPS overrides for groups)
         comm = getattr(state.model, "comm", None)
         solo = getattr(comm, "world", 1) <= 1
-        self.k_steps = int(os.environ.get("P2P_DECODE_GRAPH_STEPS", "8")) if solo else 1
+        k = os.environ.get("P2P_DECODE_GRAPH_STEPS", "8")
+        self.k_steps = int(k if solo else os.environ.get("P2P_GROUP_GRAPH_STEPS", k))
         self.graph_k = None
 
     def _body(self):
@@ -307,6 +311,12 @@ class PrefillGraph:
             from .sampling import SamplerSlots
 
             self.samp = SamplerSlots(S, dev)
+            if model.tp > 1:  # vocab-parallel draw: top-128 per shard, one all-gather
+                W = model.tp
+                self.cand_v = torch.empty(S, 128, device=dev, dtype=torch.float32)
+                self.cand_id = torch.empty(S, 128, device=dev, dtype=torch.int32)
+                self.cand_all_v = torch.empty(W * S, 128, device=dev, dtype=torch.float32)
+                self.cand_all_id = torch.empty(W * S, 128, device=dev, dtype=torch.int32)
         self.graph = None
 
     # ------------------------------------------------------------------ host side
@@ -364,6 +374,13 @@ class PrefillGraph:
                         greedy=self.greedy, tiles=self.tiles, qtile=self.qtile)
         if self.greedy:
             m.finalize_greedy(ws, self.n_out, out=self.first)
+        elif m.tp > 1:  # the shard's logits: the same draw as the decode graph's (DecodeState)
+            sp, lg = self.samp, ws.logits[:self.n_out]
+            ops.topk_candidates(lg, m.w.tp_rank * (m.cfg.vocab // m.tp), self.cand_v, self.cand_id)
+            m.comm.all_gather_rows_into(self.cand_all_v, self.cand_v)
+            m.comm.all_gather_rows_into(self.cand_all_id, self.cand_id)
+            ops.sample_candidates(self.cand_all_v, self.cand_all_id, m.tp, sp.temp, sp.topk,
+                                  sp.topp, sp.seeds, self.spos, out=self.first)
         else:
             sp = self.samp
             ops.sample(ws.logits[:self.n_out], sp.temp, sp.topk, sp.topp, sp.seeds, self.spos,

@@ -14,8 +14,10 @@ for the loop (``provider``).  The loop replays:
 
 Prompts longer than the largest prefill bucket fall back to Python's chunked prefill
 (``eager``).  Used for single-GPU replicas (TP = EP = 1) when the engine runs its graphs
-on a GPU (``ENGINE_NATIVE_LOOP``, default on); TP/EP groups keep the Python loop, whose
-calls the cluster broadcasts to the follower ranks.
+on a GPU (``ENGINE_NATIVE_LOOP``, default on), and for TP / EP groups: the leader's loop
+records its device operations and the followers' ``EngineMirror`` threads replay them
+(``run_follower_mirror``, ``csrc/runtime/mirror.h``); only the EP a2a mode (DP attention,
+per-rank sequences) keeps the Python loop and its pickled broadcast.
 """
 from __future__ import annotations
 
@@ -45,7 +47,8 @@ class NativeEngineServer(EngineServer):
     def __init__(self, engine: Engine, tokenizer=None, model_name: str = "llama3.1",
                  max_batch: int | None = None, decode_chunk: int = 8,
                  default_max_tokens: int = 128, max_ctx: int | None = None,
-                 prewarm: bool = True, prefill_ctx: int | None = None):
+                 prewarm: bool = True, prefill_ctx: int | None = None,
+                 mirror_fds: list | None = None):
         # no Python engine thread: the EngineServer state this class uses is set here
         self.engine = engine
         self.tok = tokenizer or get_tokenizer(engine.cfg)
@@ -73,12 +76,19 @@ class NativeEngineServer(EngineServer):
             "riders_all": os.environ.get("ENGINE_RIDERS", "all") == "all",
             "device": dev.index or 0, "batch_buckets": list(BATCH_BUCKETS),
             "ctx_buckets": list(CTX_BUCKETS),
-            "row_buckets": [r for r in PREFILL_ROW_BUCKETS if r <= engine.max_prefill_tokens],
+            "row_buckets": [r for r in PREFILL_ROW_BUCKETS
+                            if r <= min(engine.max_prefill_tokens, engine.prefill_graph_max_rows)],
             "prefill_max_pages": self.prefill_ctx // 64,
             "prefill_graph_after": engine.prefill_graph_after})
+        if mirror_fds:
+            # TP / EP group leader (engine.cluster): the followers' EngineMirror threads
+            # replay every device operation of this loop (runtime/mirror.h)
+            self.loop.set_mirror([int(f) for f in mirror_fds])
+        self.group = 1 + len(mirror_fds or ())
         self.loop.set_provider(self._provide)
         self.loop.set_eager_prefill(self._eager_prefill)
         self._registered = set()
+        self.k_step_graphs = 0  # decode graphs registered with a whole k-step graph
         if prewarm:
             self.prewarm()
         self.loop.start()
@@ -86,19 +96,16 @@ class NativeEngineServer(EngineServer):
     # --------------------------------------------------------------- graphs
     def _provide(self, kind: str, a: int, b: int, greedy: bool):
         """Capture (once) and register the graph the loop asked for (loop thread, GIL)."""
-        eng = self.engine
         key = (kind, a, b, greedy)
         if key in self._registered:
             return
+        self.loop.mirror_provide(kind, a, b, greedy)  # a group's followers capture it too
+        desc = capture_for_loop(self.engine, kind, a, b, greedy, self.prefill_ctx)
         if kind == "decode":
-            g = eng.decode_graph(a, b, greedy=greedy)
-            if greedy and g.graph is not None and g.k_steps > 1 and g.graph_k is None:
-                g._capture_steps()  # the loop launches whole k-step graphs first
-            self.loop.add_decode_graph(g.describe())
+            self.k_step_graphs += 1 if desc.get("exec_k") else 0
+            self.loop.add_decode_graph(desc)
         else:
-            # (the loop asks only for shapes that recur: prefill_graph_after)
-            g = eng.prefill_graph(a, b, self.prefill_ctx, greedy=greedy)
-            self.loop.add_prefill_graph(g.describe())
+            self.loop.add_prefill_graph(desc)
         self._registered.add(key)
 
     def prewarm(self, batches=None, rows=None, mode=None):
@@ -123,7 +130,7 @@ class NativeEngineServer(EngineServer):
             rows = rows or PREFILL_ROW_BUCKETS
         for sb in seqs:
             for r in rows:
-                if sb <= r <= eng.max_prefill_tokens:
+                if sb <= r <= min(eng.max_prefill_tokens, eng.prefill_graph_max_rows):
                     self._provide("prefill", r, sb, True)
 
     def _eager_prefill(self, prompts, pages, starts, samp):
@@ -187,7 +194,9 @@ class NativeEngineServer(EngineServer):
         self.loop.shutdown()
 
     def metrics(self) -> dict:
-        return {k: (int(v) if float(v).is_integer() else v) for k, v in self.loop.metrics().items()}
+        m = {k: (int(v) if float(v).is_integer() else v) for k, v in self.loop.metrics().items()}
+        m["k_step_graphs"] = self.k_step_graphs
+        return m
 
     def handle_json_stream(self, req_text: str, emit) -> str:
         """Ollama streaming (NDJSON) on the loop: token batches as they are decoded."""
@@ -256,6 +265,59 @@ class NativeEngineServer(EngineServer):
             out["response"] = ""
             out["context"] = []
         return json.dumps(out)
+
+
+def capture_for_loop(eng: Engine, kind: str, a: int, b: int, greedy: bool, prefill_ctx: int) -> dict:
+    """Capture (or reuse) the graph of one loop shape and describe it for the native loop /
+    a follower's mirror: decode (batch bucket a, context bucket b) with its whole k-step
+    graph, or a prompt chunk (row bucket a, sequence bucket b).  Every rank of a group runs
+    this for the same shapes in the same order (the leader's provider, mirrored), so the
+    collectives recorded in the graphs pair up."""
+    if kind == "decode":
+        g = eng.decode_graph(a, b, greedy=greedy)
+        if greedy and g.graph is not None and g.k_steps > 1 and g.graph_k is None:
+            g._capture_steps()  # the loop launches whole k-step graphs first
+        return g.describe()
+    # (the loop asks only for shapes that recur: prefill_graph_after)
+    return eng.prefill_graph(a, b, prefill_ctx, greedy=greedy).describe()
+
+
+def group_native_ok(engine: Engine, dp_split: bool) -> bool:
+    """A TP / EP group serves on the native loop (leader) + mirrors (followers) when its
+    engines run graphs on GPUs and every rank serves the same sequences (not the EP a2a
+    mode's DP attention, whose ranks hold different sequences)."""
+    return (not dp_split and engine.device.type == "cuda" and engine.use_graph
+            and engine.prefill_graphs_enabled
+            and os.environ.get("ENGINE_NATIVE_LOOP", "1") != "0")
+
+
+def run_follower_mirror(engine: Engine, fd: int, prefill_ctx: int) -> None:
+    """A follower rank's side of the native group loop: apply the leader's frames from the
+    channel ``fd`` until its stop.  Graph captures and eager prefills the leader mirrors
+    call back here (same code as the leader's provider).  Raises if the mirror failed."""
+    N = load_native()
+    dev = engine.device
+    m = N.EngineMirror(int(fd), dev.index or 0)
+
+    def provide(kind, a, b, greedy):
+        desc = capture_for_loop(engine, kind, a, b, greedy, prefill_ctx)
+        (m.add_decode_graph if kind == "decode" else m.add_prefill_graph)(desc)
+
+    def eager(prompts, pages, starts, samp):
+        params = [SamplingParams(temperature=t, top_k=k, top_p=p, seed=s) for t, k, p, s in samp]
+        first = engine.prefill(prompts, pages, sampling=params,
+                               starts=starts if any(starts) else None, graph=False)
+        return [int(x) for x in first.cpu().tolist()]
+
+    m.set_provider(provide)
+    m.set_eager_prefill(eager)
+    err = m.run()
+    import torch
+
+    torch.cuda.synchronize(dev)
+    m.shutdown()
+    if err:
+        raise RuntimeError("group mirror failed: %s" % err)
 
 
 def make_server(engine: Engine, tokenizer=None, **kw) -> EngineServer:
