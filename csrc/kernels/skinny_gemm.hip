@@ -1,3 +1,4 @@
+#include <dlfcn.h>
 // Skinny (M <= 64) bf16 GEMM on MFMA for decode / short-prefill projections.
 //
 //   out[m, n] = epilogue( rstd[m] * sum_k X[m, k] * W[n, k] )
@@ -47,9 +48,14 @@ int skinny_unit_ar(SKINNY_UNIT_ARGS);
 constexpr int MIDM_FLAG = 1 << 25;  // launch-code bit (ops.gemm.MIDM_FLAG)
 constexpr int WIDE_FLAG = 1 << 26;  // launch-code bit (ops.gemm.WIDE_FLAG), K slices in bits 8..15
 constexpr int PERSIST_FLAG = 1 << 28;  // ops.gemm.PERSIST_FLAG: persist_gemv.hip, CU multiple in 8..15
-extern "C" int p2p_persist_gemv(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
-                                int norm, void* out, int ldo, float eps, int grid_mult,
-                                hipStream_t st);
+// the persistent GEMV lives in the experimental library (measured slower than the skinny
+// launches, profiles/r4_persist_gemv_negative.jsonl): resolved when that library is loaded
+typedef int (*persist_gemv_fn)(const void* Wt, const void* X, int ldx, int M, int K, int N, int epi,
+                               int norm, void* out, int ldo, float eps, int grid_mult,
+                               hipStream_t st);
+static persist_gemv_fn persist_gemv() {
+  return (persist_gemv_fn)dlsym(RTLD_DEFAULT, "p2p_persist_gemv");
+}
 extern "C" int p2p_wide_dispatch(const void* Wt, const void* X, int ldx, int M, int K, int N,
                                  int epi, int norm, void* out, int ldo, float eps, const void* ea_p,
                                  int req_split, hipStream_t st);
@@ -85,8 +91,11 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
     up_off = groups;
   }
   // bit 28: the persistent GEMV (persist_gemv.hip; bf16 dense weights, M <= 16)
-  if ((waves & PERSIST_FLAG) && !ea.wscale && !ea.moe_cnt)
-    return p2p_persist_gemv(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, (waves >> 8) & 0xff, stream);
+  if ((waves & PERSIST_FLAG) && !ea.wscale && !ea.moe_cnt) {
+    const persist_gemv_fn f = persist_gemv();
+    if (!f) return (int)hipErrorNotSupported;  // experimental library not loaded
+    return f(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, (waves >> 8) & 0xff, stream);
+  }
   // bit 26: the wide mid-M kernel (wide_gemm.hip; bf16 dense weights, K % 256 == 0)
   if ((waves & WIDE_FLAG) && epi != EPI_AR)
     return p2p_wide_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, &ea, (waves >> 8) & 0xff,

@@ -201,10 +201,6 @@ def lib():
         if fn is not None:
             fn.argtypes = [c_int, c_int]
             fn.restype = ctypes.c_size_t
-        fn = getattr(L, "p2p_decode_engine_ws_bytes", None)
-        if fn is not None:
-            fn.argtypes = [c_int, c_int, c_int, c_int, c_int]
-            fn.restype = ctypes.c_size_t
         fn = getattr(L, "p2p_tiled_gemm_config", None)
         if fn is not None:
             fn.argtypes = [c_int, c_int, c_int]
@@ -245,7 +241,8 @@ _exp = None
 
 # experimental library (csrc/experimental: measured-negative fusions, hardware probes)
 _EXP_SIGS = ("p2p_attn_oproj", "p2p_attn_oproj_heads", "p2p_attn_oproj_heads_tune",
-             "p2p_l3_prefetch")
+             "p2p_l3_prefetch", "p2p_persist_gemv_ok", "p2p_decode_engine_ok",
+             "p2p_decode_engine_grid", "p2p_decode_engine_trace", "p2p_decode_engine")
 
 
 def experimental():
@@ -268,6 +265,10 @@ def experimental():
                 if fn is not None:
                     fn.argtypes = _SIGS[name]
                     fn.restype = c_int
+            fn = getattr(L, "p2p_decode_engine_ws_bytes", None)
+            if fn is not None:
+                fn.argtypes = [c_int, c_int, c_int, c_int, c_int]
+                fn.restype = ctypes.c_size_t
             _exp = L
     return _exp
 

@@ -1,5 +1,5 @@
 """Persistent decode engine: every layer of a dense TP=1 decode step (<= 4 rows, contexts
-<= 256 keys) in ONE launch of one workgroup per CU (csrc/kernels/decode_engine.hip).
+<= 256 keys) in ONE launch of one workgroup per CU (csrc/experimental/decode_engine.hip, libp2p_experimental.so).
 
 The separate-launch decode layer (qkv+attention, o_proj, gate_up, down) pays a dependent
 kernel boundary between every pair of weight streams; here the four streams are phases of
@@ -43,7 +43,7 @@ class DecodeEngine:
             kc, vc = kv.layer(i)
             kvp += [kc.data_ptr(), vc.data_ptr()]
         self.kvptr = torch.tensor(kvp, dtype=torch.int64, device=dev)
-        L = _lib.lib()
+        L = _lib.experimental()
         nbytes = L.p2p_decode_engine_ws_bytes(MAX_ROWS, self.H, self.I, self.Hq, self.Hkv)
         self.ws = torch.zeros((nbytes + 7) // 8, dtype=torch.int64, device=dev)
         self.epoch = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -53,7 +53,7 @@ class DecodeEngine:
         """h [R, H] bf16: embedding rows in, final residual out (before the final norm)."""
         R = h.shape[0]
         assert R <= MAX_ROWS and h.stride(1) == 1 and h.dtype == torch.bfloat16
-        L = _lib.lib()
+        L = _lib.experimental()
         _lib.check(L.p2p_decode_engine(
             self.wptr.data_ptr(), self.kvptr.data_ptr(), self.L, R, self.H, self.I, self.Hq,
             self.Hkv, float(self.eps), float(self.scale), h.data_ptr(), h.stride(0),
@@ -73,5 +73,5 @@ def decode_engine_ok(model, R: int, max_ctx: int) -> bool:
     if not all(isinstance(t, torch.Tensor) and t.dtype == torch.bfloat16
                for t in (lw.qkv, lw.o, lw.gate_up, lw.down)):
         return False  # weight-only fp8 keeps the separate launches
-    L = _lib.lib()
+    L = _lib.experimental()
     return bool(L.p2p_decode_engine_ok(R, cfg.hidden, cfg.ffn, model.nq, model.nkv, max_ctx))

@@ -156,7 +156,7 @@ MIDM_FLAG = 1 << 25
 WIDE_FLAG = 1 << 26
 # launch-code bit: the skinny kernel's X is fragment-major (pack_frag), not row-major
 AFRAG_FLAG = 1 << 27
-# the persistent GEMV (csrc/kernels/persist_gemv.hip): one 4-wave workgroup per CU (x the
+# the persistent GEMV (csrc/experimental/persist_gemv.hip, libp2p_experimental.so): one 4-wave workgroup per CU (x the
 # multiple in bits 8..15) walking balanced 16-column units with the weight stream carried
 # across them; M <= 16, bf16 weights, K % 1024 == 0.  Measured 1.3-1.6x slower than the
 # skinny launches (profiles/r4_persist_gemv_negative.jsonl): explicit launch codes only
@@ -164,7 +164,7 @@ PERSIST_FLAG = 1 << 28
 
 
 def persist_ok(M: int, K: int, N: int, epi: int) -> bool:
-    return bool(_lib.lib().p2p_persist_gemv_ok(M, K, N, epi))
+    return bool(_lib.experimental().p2p_persist_gemv_ok(M, K, N, epi))
 
 
 _PACK_BUF: dict = {}
@@ -315,6 +315,8 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
         os_ = out[m0:m0 + mc]
         wp, sp = _wptr(wt)
         code = _code(wt, mc, epi, norm, waves)
+        if code & PERSIST_FLAG:
+            _lib.experimental()  # the persistent GEMV's library (its symbol, found by dlsym)
         if code & AFRAG_FLAG and not x_packed:
             xs = _packed(xs)  # a launch of its own: the autotuner times pack + GEMM together
         _lib.check(L.p2p_skinny_gemm(wp, xs.data_ptr(), x.stride(0), mc, K, N, epi,
