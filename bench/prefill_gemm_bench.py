@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--deep-modes", type=int, nargs="*", default=[0, 1])
     ap.add_argument("--only", nargs="*", default=None, help="variant names to run")
     ap.add_argument("--no-hipblaslt", action="store_true")
+    ap.add_argument("--gemms", nargs="*", default=None, help="projection names to run")
     a = ap.parse_args()
     H, F = LLAMA31_8B.hidden, LLAMA31_8B.ffn
     variants = [("v2_auto", (2, 0, 0)), ("v2_256x256_phased", (2, 1, 1)),
@@ -46,7 +47,10 @@ def main():
         for name, N, K, fn in [
             ("qkv", 6144, H, lambda W: ops.skinny_gemm(W, x, ops.EPI_STORE, norm=True, out=o)),
             ("gate_up", 2 * F, H, lambda W: ops.skinny_gemm(W, x, ops.EPI_SILU, norm=True, out=act)),
-            ("down", H, F, lambda W: ops.skinny_gemm(W, xf, ops.EPI_RESID, out=h))]:
+            ("down", H, F, lambda W: ops.skinny_gemm(W, xf, ops.EPI_RESID, out=h)),
+            ("o_proj", H, H, lambda W: ops.skinny_gemm(W, x, ops.EPI_RESID, out=h))]:
+            if a.gemms and name not in a.gemms:
+                continue
             W = (torch.randn(N // 16, K // 32, 64, 8, device="cuda") * 0.02).to(torch.bfloat16)
             flops = 2 * M * N * K
             vs = variants

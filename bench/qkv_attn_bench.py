@@ -76,6 +76,11 @@ def run(name, Hq, Hkv, K, M, ctx_len, L=32, hidden=None):
             res["qkv_attn_oproj_w%d" % wv] = graph_time(lambda i: fused_oproj(i, wv), n_inner=L)
     for wv in (4, 8):
         res["fused_w%d" % wv] = graph_time(lambda i: fused(i, wv), n_inner=L)
+        # k-split producers (launch code bits 8..15: slices per column group)
+        for ks in (2, 3, 4, 6, 8):
+            if (K // 32) // ks >= 16:
+                res["fused_w%d_ks%d" % (wv, ks)] = graph_time(lambda i: fused(i, wv | (ks << 8)),
+                                                              n_inner=L)
     res["two_kernels"] = graph_time(two, n_inner=L)
     res["qkv_only"] = graph_time(qkv_only, n_inner=L)
     for mode, label in ((0, "fused"), (1, "fused_producers_only"), (2, "fused_handoff_only")):

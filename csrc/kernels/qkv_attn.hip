@@ -20,6 +20,15 @@
 // earlier call or layer never carries the current tag.  Consumers only wait on producers,
 // producers never wait, and consumer blocks are few (M x Hkv <= 128): the grid always
 // drains.  Spins are bounded; a timeout sets the fault word (LlamaModel.check_faults).
+//
+// K-split producers (launch code bits 8..15 = ks > 1, round 5): a producer unit is one
+// k-slice of one column group -- groups x ks units, so the weight stream is spread evenly
+// over the CUs where whole groups are not (the 8B qkv: 384 groups = 1.5 per CU, 768 halves
+// = 3; the 70B TP=8 shard: 80 groups on 256 CUs, 480 sixths).  Units publish fp32 partial
+// sums as {tag, fp32} granules; the consumer of (row, kv head) sums the slices in slice
+// order (deterministic), applies the row's rstd (it sums the squares of the row itself,
+// behind the weight stream), RoPE, writes this token's k / v to the cache and goes on with
+// the attention.
 #include "common.h"
 
 #include <cstdlib>
@@ -63,8 +72,9 @@ struct QAArgs {
   int ldh, No, Ko;    // Ko = Hq * 128
   u64* gran2;         // [M][Ko / 2] attention-output granules {epoch, two bf16}
   unsigned* epoch;    // [2]: launch epoch, o_proj arrival ticket
-  int n_prod;         // producer blocks
+  int n_prod;         // producer blocks (groups x ks)
   int n_o;            // o_proj blocks = No / 16
+  int ks;             // k-slices per column group (1: whole-group producers)
 };
 
 __device__ __forceinline__ unsigned bits16(float x) {
@@ -200,6 +210,94 @@ __device__ __forceinline__ void producer(const QAArgs& a, int g, char* smem) {
   }
 }
 
+// K-split producer: unit pg = k-slice (pg / groups) of column group (pg % groups); the
+// block's waves split the slice's k-steps; the summed partial (no rstd, no RoPE: the
+// consumer finishes those) goes out as {tag, fp32} granules [M][Hkv][G + 2][ks][128].
+template <int G, int W>
+__device__ __forceinline__ void producer_split(const QAArgs& a, int pg, char* smem) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int groups = a.n_prod / a.ks;
+  const int g = pg % groups, sk = pg / groups;
+  const int S = a.K >> 5;
+  const int u0 = (S * sk) / a.ks, u1 = (S * (sk + 1)) / a.ks;
+  const int s0 = u0 + ((u1 - u0) * w) / W, s1 = u0 + ((u1 - u0) * (w + 1)) / W;
+  const bf16x8* wp = a.Wt + (size_t)g * S * 64 + lane;
+  const bool xv = r < a.M;
+  const bf16* xp = a.X + (size_t)(xv ? r : 0) * a.ldx + 8 * q;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  auto load = [&](int s, bf16x8(&bw)[QA_U], bf16x8(&ax)[QA_U]) {
+#pragma unroll
+    for (int u = 0; u < QA_U; ++u) {
+      bw[u] = __builtin_nontemporal_load(wp + (size_t)(s + u) * 64);
+      ax[u] = xv ? *reinterpret_cast<const bf16x8*>(xp + (s + u) * 32) : zero_bf16x8();
+    }
+  };
+  auto compute = [&](const bf16x8(&bw)[QA_U], const bf16x8(&ax)[QA_U]) {
+#pragma unroll
+    for (int u = 0; u < QA_U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[u], bw[u], acc, 0, 0, 0);
+  };
+  const int n = s1 - s0, nb = n / QA_U;
+  if (nb > 0) {
+    bf16x8 bA[QA_U], bB[QA_U], aA[QA_U], aB[QA_U];
+    load(s0, bA, aA);
+    int b = 0;
+    for (; b + 2 < nb; b += 2) {
+      load(s0 + (b + 1) * QA_U, bB, aB);
+      compute(bA, aA);
+      load(s0 + (b + 2) * QA_U, bA, aA);
+      compute(bB, aB);
+    }
+    if (b + 1 < nb) {
+      load(s0 + (b + 1) * QA_U, bB, aB);
+      compute(bA, aA);
+      compute(bB, aB);
+    } else {
+      compute(bA, aA);
+    }
+  }
+  for (int s = s0 + nb * QA_U; s < s1; ++s) {
+    const bf16x8 b1 = __builtin_nontemporal_load(wp + (size_t)s * 64);
+    const bf16x8 a1 = xv ? *reinterpret_cast<const bf16x8*>(xp + s * 32) : zero_bf16x8();
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+  }
+  float* red = reinterpret_cast<float*>(smem);  // [W - 1][4][64]
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[((w - 1) * 4 + j) * 64 + lane] = acc[j];
+  }
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int ww = 0; ww < W - 1; ++ww)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += red[(ww * 4 + j) * 64 + lane];
+  const int head = g >> 3, kk = g & 7;
+  const int d = (r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8);
+  const int Hq = a.Hq, Hkv = a.Hkv;
+  int kvh, sl;
+  if (head < Hq) {
+    kvh = head / G;
+    sl = head % G;
+  } else if (head < Hq + Hkv) {
+    kvh = head - Hq;
+    sl = G;
+  } else {
+    kvh = head - Hq - Hkv;
+    sl = G + 1;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = 4 * q + j;
+    if (m < a.M) {
+      const unsigned tag = a.counters[m * Hkv + kvh] + 1;
+      const u64 gr = ((u64)tag << 32) | (u64)__float_as_uint(acc[j]);
+      __hip_atomic_store(a.gran + ((((size_t)m * Hkv + kvh) * (G + 2) + sl) * a.ks + sk) * HD + d, gr,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- consumer
 // Wave w owns the 64 keys of page w of the row (contexts <= 256 keys).  The math is the
 // MFMA form of decode attention (v_mfma_f32_16x16x32_bf16, query heads on the N axis,
@@ -274,20 +372,97 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
   const unsigned tag = a.counters[r * Hkv + h] + 1;
   const unsigned o_epoch =
       a.gran2 ? __hip_atomic_load(&a.epoch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 : 0;
-  const u64* gb = a.gran + ((size_t)r * Hkv + h) * (G + 2) * 64;
   const int failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long t0 = wall_clock64();
-  for (int i = tid; i < (G + 2) * 64; i += W * 64) {
-    u64 x = __hip_atomic_load(gb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while ((unsigned)(x >> 32) != tag && !failed) {
-      if (wall_clock64() - t0 > a.spin_ticks) {
-        atomicOr(a.err, 1);
-        break;
+  if (a.ks > 1) {
+    // k-split producers: this row's rstd first (its squares, behind the weight stream) ...
+    const bf16* xr = a.X + (size_t)r * a.ldx;
+    float ss = 0.f;
+    for (int i = tid; i < (a.K >> 3); i += W * 64)
+      ss = sumsq8(*reinterpret_cast<const bf16x8*>(xr + 8 * i), ss);
+    ss = wave_sum(ss);
+    float* rs = &sm[0][0];  // (free until the softmax merge)
+    if (lane == 0) rs[w] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) tot += rs[ww];
+    const float rstd = rsqrtf(tot / (float)a.K + a.eps);
+    // ... then per dim pair (d, d + 64) of a head: the slices' partials summed in slice
+    // order, rstd, RoPE (q heads and k), this token's k / v to the cache
+    const u64* gb = a.gran + ((size_t)r * Hkv + h) * (G + 2) * a.ks * HD;
+    const int slot = a.slots[r];
+    const float2* csr = a.cs + (size_t)a.pos[r] * 64;
+    bf16* cb = reinterpret_cast<bf16*>(&cur[0][0]);
+    constexpr int KSM = 8;
+    for (int i = tid; i < (G + 2) * 64; i += W * 64) {
+      const int sl = i >> 6, d = i & 63;
+      const u64* base = gb + (size_t)sl * a.ks * HD;
+      u64 lo[KSM], hi[KSM];
+#pragma unroll
+      for (int k = 0; k < KSM; ++k)
+        if (k < a.ks) {
+          lo[k] = __hip_atomic_load(base + k * HD + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          hi[k] = __hip_atomic_load(base + k * HD + d + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      for (;;) {
+        bool stale = false;
+#pragma unroll
+        for (int k = 0; k < KSM; ++k)
+          if (k < a.ks) stale |= (unsigned)(lo[k] >> 32) != tag || (unsigned)(hi[k] >> 32) != tag;
+        if (!stale || failed) break;
+        if (wall_clock64() - t0 > a.spin_ticks) {
+          atomicOr(a.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+        for (int k = 0; k < KSM; ++k)
+          if (k < a.ks) {
+            if ((unsigned)(lo[k] >> 32) != tag)
+              lo[k] = __hip_atomic_load(base + k * HD + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(hi[k] >> 32) != tag)
+              hi[k] = __hip_atomic_load(base + k * HD + d + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
       }
-      __builtin_amdgcn_s_sleep(2);
-      x = __hip_atomic_load(gb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      float vlo = 0.f, vhi = 0.f;
+#pragma unroll
+      for (int k = 0; k < KSM; ++k)
+        if (k < a.ks) {
+          vlo += __uint_as_float((unsigned)lo[k]);
+          vhi += __uint_as_float((unsigned)hi[k]);
+        }
+      vlo *= rstd;
+      vhi *= rstd;
+      float ylo = vlo, yhi = vhi;
+      if (sl <= G) {  // q heads and k: rotate the pair (d, d + 64)
+        const float2 c = csr[d];
+        ylo = vlo * c.x - vhi * c.y;
+        yhi = vhi * c.x + vlo * c.y;
+      }
+      cb[sl * HD + d] = f2bf(ylo);
+      cb[sl * HD + d + 64] = f2bf(yhi);
+      if (sl >= G && slot >= 0) {  // k / v of the current token -> cache (later steps)
+        bf16* cache = sl == G ? a.kc : a.vc;
+        bf16* dst = cache + (((size_t)(slot / PAGE) * Hkv + h) * PAGE + slot % PAGE) * HD;
+        dst[d] = f2bf(ylo);
+        dst[d + 64] = f2bf(yhi);
+      }
     }
-    cur[i >> 6][i & 63] = (unsigned)x;
+  } else {
+    const u64* gb = a.gran + ((size_t)r * Hkv + h) * (G + 2) * 64;
+    for (int i = tid; i < (G + 2) * 64; i += W * 64) {
+      u64 x = __hip_atomic_load(gb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((unsigned)(x >> 32) != tag && !failed) {
+        if (wall_clock64() - t0 > a.spin_ticks) {
+          atomicOr(a.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        x = __hip_atomic_load(gb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      cur[i >> 6][i & 63] = (unsigned)x;
+    }
   }
   __syncthreads();
   if (a.probe & 2) {  // probe: hand-off only (no attention math)
@@ -578,6 +753,10 @@ __global__ __launch_bounds__(W * 64) void qkv_attn_kernel(QAArgs a) {
     consumer<G, W>(a, blockIdx.x, smem);
   } else {
     const int pg = blockIdx.x - a.n_cons;
+    if (!FO && a.ks > 1) {
+      producer_split<G, W>(a, pg, smem);
+      return;
+    }
     producer<G, W>(a, pg, smem);
     // FO: the first n_o producers go on to an o_proj column group, their registers free
     // once the qkv stream is done (no extra workgroups competing for residency).  Loading
@@ -595,7 +774,7 @@ __global__ __launch_bounds__(W * 64) void qkv_attn_kernel(QAArgs a) {
 
 template <int W, bool FO>
 int launch_qa(const QAArgs& a, int G, int groups, hipStream_t stream) {
-  const dim3 grid(a.n_cons + groups), block(W * 64);
+  const dim3 grid(a.n_cons + (FO ? groups : a.n_prod)), block(W * 64);
   switch (G) {
     case 1: hipLaunchKernelGGL((qkv_attn_kernel<1, W, FO>), grid, block, 0, stream, a); break;
     case 2: hipLaunchKernelGGL((qkv_attn_kernel<2, W, FO>), grid, block, 0, stream, a); break;
@@ -656,6 +835,32 @@ static long long qa_spin_ticks() {
   return t;
 }
 
+// k-slices per column group: whole groups where they already give every CU an equal share
+// (groups a multiple of the CU count, or >= 2 per CU), else the fewest slices that bring
+// the units to >= 2 per CU with <= 1/8 imbalance (8B qkv: 384 groups -> 2 = 768 units, 3 per
+// CU; the 70B TP=8 shard: 80 -> 7 = 560); P2P_QA_KSPLIT overrides.
+static int qa_ksplit(int groups, int K) {
+  static const int env = [] {
+    const char* e = std::getenv("P2P_QA_KSPLIT");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  if (env >= 1 && env <= 8) return env;
+  if (env == 0) return 1;  // (measurement pending: bench/qkv_attn_bench.py ks sweep)
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return 1;
+  if (groups % cus == 0 || groups >= 4 * cus) return 1;
+  for (int ks = 1; ks <= 8; ++ks) {
+    const int u = groups * ks;
+    if ((K / 32) / ks < 16) break;  // >= 16 k-steps per unit
+    if (u < 2 * cus) continue;
+    const int per = (u + cus - 1) / cus;  // the busiest CU's units vs the average
+    if (per * cus <= u + u / 8 || u % cus == 0) return ks;
+  }
+  return 1;
+}
+
 static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, int Hq, int Hkv,
                          const int* pos, const int* slots, const void* cos_sin, void* k_cache,
                          void* v_cache, const int* block_tables, int bt_stride,
@@ -692,11 +897,16 @@ static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, i
   a.probe = g_qa_probe;
   a.spin_ticks = qa_spin_ticks();
   const int groups = (Hq + 2 * Hkv) * (HD / 16);
-  a.n_prod = groups;
   // producer waves per block (split-K): 8 when the projection has few column groups (the
-  // 70B TP=8 shard: 80), as the skinny kernel's heuristic would pick; else 4
-  int W = waves;
-  if (W != 4 && W != 8) W = (groups * 8 * 2 <= 4096 && (K / 32) / 8 >= 8) ? 8 : 4;
+  // 70B TP=8 shard: 80), as the skinny kernel's heuristic would pick; else 4.
+  // Launch-code bits 8..15: k-slices per group (0 = qa_ksplit's pick; 1 = whole groups)
+  int ks = (waves >> 8) & 0xff;
+  int W = waves & 0xff;
+  if (ks == 0) ks = qa_ksplit(groups, K);
+  if (ks < 1 || ks > 8 || (K / 32) / ks < 4) return (int)hipErrorInvalidValue;
+  if (W != 4 && W != 8) W = (groups * ks * 8 * 2 <= 4096 && (K / 32) / ks / 8 >= 8) ? 8 : 4;
+  a.ks = Wo != nullptr ? 1 : ks;  // (the o_proj role keeps whole groups)
+  a.n_prod = groups * a.ks;
   if (Wo != nullptr) {
     a.Wo = (const bf16x8*)Wo;
     a.h = (bf16*)h;

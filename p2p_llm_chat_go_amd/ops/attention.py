@@ -95,12 +95,17 @@ def qkv_attn_ok(R: int, n_heads: int, n_kv: int, max_ctx: int) -> bool:
             and n_heads % n_kv == 0 and n_heads // n_kv in (1, 2, 4, 8))
 
 
+QKV_ATTN_MAX_KSPLIT = 8
+
+
 def qkv_attn_workspace(rows: int, n_heads: int, n_kv: int, device) -> tuple:
     """(granules u64 [rows][n_kv][G + 2][64], tag counters u32 [rows][n_kv],
     attention-output granules u64 [rows][n_heads * 64] + launch epoch u32 [2] for the
     fused o_proj role), zeroed."""
     G = n_heads // n_kv
-    gran = torch.zeros(rows * n_kv * (G + 2) * 64, dtype=torch.int64, device=device)
+    # (k-split producers publish one fp32 partial per dim and slice: up to 8 slices)
+    gran = torch.zeros(rows * n_kv * (G + 2) * 128 * QKV_ATTN_MAX_KSPLIT, dtype=torch.int64,
+                       device=device)
     cnt = torch.zeros(rows * n_kv, dtype=torch.int32, device=device)
     gran2 = torch.zeros(rows * n_heads * 64, dtype=torch.int64, device=device)
     epoch = torch.zeros(2, dtype=torch.int32, device=device)

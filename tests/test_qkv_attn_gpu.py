@@ -45,10 +45,15 @@ def _two_kernel(d, Hq, Hkv, kc, vc):
     return q, out
 
 
+@pytest.mark.parametrize("ks", [1, 2, 3, 6])
 @pytest.mark.parametrize("M,Hq,Hkv,K", [(1, 32, 8, 4096), (3, 32, 8, 1024), (16, 32, 8, 1024),
                                         (1, 8, 1, 8192), (5, 8, 1, 1024), (2, 4, 4, 512),
                                         (4, 16, 8, 512)])
-def test_qkv_attn_matches_two_kernels(M, Hq, Hkv, K):
+def test_qkv_attn_matches_two_kernels(M, Hq, Hkv, K, ks):
+    """ks > 1: k-split producers (fp32 partials, the consumer sums them in slice order and
+    applies rstd, RoPE and the KV write itself)."""
+    if (K // 32) // ks < 4:
+        pytest.skip("fewer than 4 k-steps per slice")
     d = _setup(M, Hq, Hkv, K, seed=M * 100 + Hq + K)
     kc1, vc1 = d["kc"].clone(), d["vc"].clone()
     q_ref, ref = _two_kernel(d, Hq, Hkv, kc1, vc1)
@@ -62,15 +67,17 @@ def test_qkv_attn_matches_two_kernels(M, Hq, Hkv, K):
         kc2, vc2 = d["kc"].clone(), d["vc"].clone()
         out = torch.full((M, Hq * 128), float("nan"), dtype=torch.bfloat16, device=DEV)
         ops.qkv_attn(d["wt"], d["x"], d["pos"], d["slots"], d["cs"], Hq, Hkv, kc2, vc2, d["bt"],
-                     d["ctx"], out, ws, err)
+                     d["ctx"], out, ws, err, waves=ks << 8)
         torch.cuda.synchronize()
         assert int(err.item()) == 0, "hand-off timed out"
         assert not out.isnan().any()
         # the current token's k / v reach the cache as the skinny epilogue writes them (the
-        # fp32 sums may round differently in the last bf16 bit: a handful of 1-ulp flips)
+        # fp32 sums may round differently in the last bf16 bit: a handful of 1-ulp flips;
+        # k-split sums slice partials in another order: up to 1/16 of the row's values)
         for name, a_, b_ in (("k", kc2, kc1), ("v", vc2, vc1)):
             assert torch.allclose(a_.float(), b_.float(), rtol=1e-2, atol=1e-3), (rep, name)
-            assert int((a_ != b_).sum()) <= 8, (rep, name, int((a_ != b_).sum()))
+            assert int((a_ != b_).sum()) <= (8 if ks == 1 else M * Hkv * 16), (
+                rep, name, int((a_ != b_).sum()))
         rel = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
         assert rel < 2e-2, (rep, rel)
         rel32 = ((out.cpu().float() - ref32).abs().max() / ref32.abs().max()).item()
