@@ -24,7 +24,7 @@
 // K-split producers (launch code bits 8..15 = ks > 1, round 5): a producer unit is one
 // k-slice of one column group -- groups x ks units, so the weight stream is spread evenly
 // over the CUs where whole groups are not (the 8B qkv: 384 groups = 1.5 per CU, 768 halves
-// = 3; the 70B TP=8 shard: 80 groups on 256 CUs, 480 sixths).  Units publish fp32 partial
+// = 3; the 70B TP=8 shard: 80 groups on 256 CUs, 160 halves; qa_ksplit picks).  Units publish fp32 partial
 // sums as {tag, fp32} granules; the consumer of (row, kv head) sums the slices in slice
 // order (deterministic), applies the row's rstd (it sums the squares of the row itself,
 // behind the weight stream), RoPE, writes this token's k / v to the cache and goes on with
@@ -835,30 +835,22 @@ static long long qa_spin_ticks() {
   return t;
 }
 
-// k-slices per column group: whole groups where they already give every CU an equal share
-// (groups a multiple of the CU count, or >= 2 per CU), else the fewest slices that bring
-// the units to >= 2 per CU with <= 1/8 imbalance (8B qkv: 384 groups -> 2 = 768 units, 3 per
-// CU; the 70B TP=8 shard: 80 -> 7 = 560); P2P_QA_KSPLIT overrides.
+// k-slices per column group.  Measured (bench/qkv_attn_bench.py, profiles/r5_qkv_attn_ksplit.jsonl):
+// the 70B TP=8 shard (80 groups on 256 CUs) runs 10.1 us with 2 slices against 11.4 with
+// whole groups (8 waves); the 8B qkv (384 groups) loses with any split (13.4 -> 15.7 us at 2:
+// 768 units no longer fit the device at once next to the consumers' LDS).  So: 2 slices
+// where whole groups leave more than half of the CUs without one; P2P_QA_KSPLIT overrides.
 static int qa_ksplit(int groups, int K) {
   static const int env = [] {
     const char* e = std::getenv("P2P_QA_KSPLIT");
     return e && *e ? std::atoi(e) : 0;
   }();
   if (env >= 1 && env <= 8) return env;
-  if (env == 0) return 1;  // (measurement pending: bench/qkv_attn_bench.py ks sweep)
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     return 1;
-  if (groups % cus == 0 || groups >= 4 * cus) return 1;
-  for (int ks = 1; ks <= 8; ++ks) {
-    const int u = groups * ks;
-    if ((K / 32) / ks < 16) break;  // >= 16 k-steps per unit
-    if (u < 2 * cus) continue;
-    const int per = (u + cus - 1) / cus;  // the busiest CU's units vs the average
-    if (per * cus <= u + u / 8 || u % cus == 0) return ks;
-  }
-  return 1;
+  return (2 * groups <= cus && (K / 32) / 2 >= 16) ? 2 : 1;
 }
 
 static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, int Hq, int Hkv,

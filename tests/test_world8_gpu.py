@@ -156,8 +156,13 @@ def _worker(rank, world, port, q, kind, mode, env):
 # box) and timed out whenever one rank started late (round 4: 5 of 5 runs on fresh boxes),
 # so the 8-rank fused epilogue is covered bit-exactly by test_fused_ar_gpu.py (world 8, one
 # launch per rank in lockstep) and here the 8-rank engine runs the unfused pair.
+# The TP=4 case also keeps whole-group qkv producers (P2P_QA_KSPLIT=1): k-split doubles the
+# qkv+attention grid (76 KB of LDS per workgroup), and four ranks' grids beside their peers'
+# spinning fused all-reduce launches no longer fit the one device (a rank on its own GPU
+# never shares it); the TP=8 case runs the k-split default.
 @pytest.mark.parametrize("kind,mode,world,env", [
-    ("dense", "tp", 8, {"P2P_TP_FUSED_AR": "0"}), ("dense", "tp", 4, {"P2P_FAR_MAX_WAVES": "2"}),
+    ("dense", "tp", 8, {"P2P_TP_FUSED_AR": "0"}),
+    ("dense", "tp", 4, {"P2P_FAR_MAX_WAVES": "2", "P2P_QA_KSPLIT": "1"}),
     ("moe", "allreduce", 8, {}), ("moe", "a2a", 8, {})])
 def test_world8_virtual_ranks_full_width(kind, mode, world, env):
     ctx = mp.get_context("spawn")
