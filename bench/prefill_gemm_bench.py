@@ -66,7 +66,16 @@ def main():
                 vs = [(v, c, 1) for v, c in vs]
             if a.only:
                 vs = [v for v in vs if v[0].rsplit("_deep", 1)[0] in a.only]
+            if name == "gate_up" and 64 < M <= 384:
+                vs = [("tall", "tall", 1)] + vs
             for vname, cfg, deep in vs:
+                ops.gemm.TALL_SILU = cfg == "tall"
+                if cfg == "tall":
+                    t = graph_time(lambda i: fn(W), n_inner=10)
+                    print(json.dumps({"M": M, "gemm": name, "variant": vname, "us": round(t, 1),
+                                      "TFLOPs": round(flops / (t * 1e-6) / 1e12, 1),
+                                      "TBps": round(N * K * 2 / (t * 1e-6) / 1e12, 2)}), flush=True)
+                    continue
                 set_tiled_min_m(65 if cfg is None else 1)
                 L.p2p_prefill_deep(deep)
                 if cfg is not None:

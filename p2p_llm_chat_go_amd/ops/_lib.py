@@ -41,6 +41,9 @@ _SIGS = {
     "p2p_flash_prefill2": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                            c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
     "p2p_flash_prefill_tile": [c_int, c_int],
+    "p2p_tall_silu": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_float,
+                      c_void_p],
+    "p2p_tall_silu_ok": [c_int, c_int, c_int],
     "p2p_car_alloc": [ctypes.c_size_t, c_void_p],
     "p2p_car_free": [c_void_p],
     "p2p_car_get_handle": [c_void_p, c_void_p],
@@ -242,7 +245,8 @@ _exp = None
 # experimental library (csrc/experimental: measured-negative fusions, hardware probes)
 _EXP_SIGS = ("p2p_attn_oproj", "p2p_attn_oproj_heads", "p2p_attn_oproj_heads_tune",
              "p2p_l3_prefetch", "p2p_persist_gemv_ok", "p2p_decode_engine_ok",
-             "p2p_decode_engine_grid", "p2p_decode_engine_trace", "p2p_decode_engine")
+             "p2p_decode_engine_grid", "p2p_decode_engine_trace", "p2p_decode_engine",
+             "p2p_tall_silu", "p2p_tall_silu_ok")
 
 
 def experimental():

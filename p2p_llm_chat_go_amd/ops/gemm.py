@@ -123,6 +123,17 @@ def set_tiled_min_m(m: int):
     TILED_MIN_M = int(m)
 
 
+# the tall SwiGLU kernel (csrc/experimental/tall_gemm.hip: every row of a batched prompt chunk
+# in one workgroup, weights streamed once) -- correct but SLOWER than the split-K tiled kernel
+# at every height measured (384 rows 152 vs 105 us, 128 rows 89 vs 54;
+# profiles/r5_tall_silu_negative.jsonl): opt-in P2P_TALL_SILU=1
+TALL_SILU = os.environ.get("P2P_TALL_SILU", "0") == "1"
+
+
+def tall_silu_ok(M: int, K: int, N: int) -> bool:
+    return bool(_lib.experimental().p2p_tall_silu_ok(M, K, N))
+
+
 def wide_ok(N, K, epi) -> bool:
     """Shapes the wide mid-M kernel tiles: 128 output columns per workgroup (SwiGLU: 64
     gate/up pairs), K in 256-wide chunks."""
@@ -304,6 +315,12 @@ def skinny_gemm(wt: torch.Tensor, x: torch.Tensor, epi: int = EPI_STORE, norm: b
     assert x.stride(1) == 1 and out.stride(1) == 1
     L = _lib.lib()
     s = _lib.stream_ptr(x.device)
+    if (epi == EPI_SILU and norm and M > SKINNY_MAX_M and TALL_SILU and not _is_f8(wt)
+            and not (waves & TILED_FLAG) and tall_silu_ok(M, K, N)):
+        # batched-prompt gate_up: all rows in one workgroup, weights streamed once (tall_gemm.hip)
+        _lib.check(_lib.experimental().p2p_tall_silu(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N,
+                                   out.data_ptr(), out.stride(0), float(eps), s), "tall_silu")
+        return out
     if _want_tiled(wt, M, N, K, epi, norm, waves):
         _lib.check(L.p2p_tiled_gemm(wt.data_ptr(), x.data_ptr(), x.stride(0), M, K, N, epi,
                                     int(norm), out.data_ptr(), out.stride(0), float(eps), s),

@@ -1112,3 +1112,32 @@ def test_moe_router_logits(R, E):
     got = torch.zeros(R, 16, device=DEV)
     M.moe_router_logits(h.to(DEV), wr.to(DEV), E, got)
     assert _rel(got.cpu()[:, :E], ref[:, :E]) < 1e-3
+
+
+@pytest.mark.parametrize("M", [65, 100, 128, 160, 192, 250, 288, 320, 352, 384])
+def test_tall_silu_gate_up(M):
+    """The tall SwiGLU kernel (csrc/experimental/tall_gemm.hip, opt-in: every row of a batched prompt chunk
+    in one workgroup, weights streamed once) against the fp32 PyTorch reference of
+    rmsnorm -> gate_up -> SwiGLU, at the 8B width (K 4096, 2 x 2048 columns) and ragged row
+    counts (rows past M are clamped duplicates, never stored)."""
+    from p2p_llm_chat_go_amd.ops import gemm as G
+
+    K, F = 4096, 2048
+    g = torch.Generator().manual_seed(M)
+    w = (torch.randn(2 * F, K, generator=g) * 0.02).to(torch.bfloat16)
+    wt = ops.tile_weight(w).to(DEV)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    assert G.tall_silu_ok(M, K, 2 * F)
+    out = torch.full((M + 3, F), float("nan"), dtype=torch.bfloat16, device=DEV)
+    G.TALL_SILU = True  # opt-in (measured slower than the tiled kernel; experimental library)
+    try:
+        ops.skinny_gemm(wt, x, ops.EPI_SILU, norm=True, out=out[:M])
+    finally:
+        G.TALL_SILU = False
+    torch.cuda.synchronize()
+    assert not out[M:].isnan().logical_not().any(), "rows past M written"
+    ref = torch.empty(M, F, dtype=torch.float32)
+    G._ref(wt.cpu(), x.cpu(), ops.EPI_SILU, True, ref, 1e-5)
+    got = out[:M].float().cpu()
+    rel = ((got - ref).abs().max() / ref.abs().max()).item()
+    assert rel < 1e-2, rel
