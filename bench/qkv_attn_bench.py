@@ -77,10 +77,15 @@ def run(name, Hq, Hkv, K, M, ctx_len, L=32, hidden=None):
     for wv in (4, 8):
         res["fused_w%d" % wv] = graph_time(lambda i: fused(i, wv), n_inner=L)
         # k-split producers (launch code bits 8..15: slices per column group)
-        for ks in (2, 3, 4, 6, 8):
-            if (K // 32) // ks >= 16:
+        for ks in (1, 2, 3, 4, 6, 8):
+            if (K // 32) // ks < 16:
+                continue
+            if ks > 1:
                 res["fused_w%d_ks%d" % (wv, ks)] = graph_time(lambda i: fused(i, wv | (ks << 8)),
                                                               n_inner=L)
+            if ctx_len <= 128 and ks <= 4:  # consumers with 2 key waves (contexts <= 128)
+                res["fused_w%d_ks%d_kw2" % (wv, ks)] = graph_time(
+                    lambda i: fused(i, wv | (ks << 8) | (2 << 16)), n_inner=L)
     res["two_kernels"] = graph_time(two, n_inner=L)
     res["qkv_only"] = graph_time(qkv_only, n_inner=L)
     for mode, label in ((0, "fused"), (1, "fused_producers_only"), (2, "fused_handoff_only")):

@@ -311,9 +311,11 @@ __device__ __forceinline__ void producer_split(const QAArgs& a, int pg, char* sm
 // not in the prefetched rows: its k row is patched into the K fragments and its v row
 // into the LDS V rows from the granules.
 constexpr int MKPW = 64;  // keys per wave = one page
-constexpr int KW = 4;     // key waves: 4 pages = 256 keys (waves >= KW only join the barriers)
-
-template <int G, int W>
+// key waves KW: one page of 64 keys each -- 4 (256 keys) by default, 2 (128 keys) when the
+// caller bounds the contexts (launch-code bits 16..23): half the consumer's LDS, so the
+// grid's workgroups (all sized for a consumer) fit the CUs 3-4 at a time instead of 2
+// (waves >= KW only join the barriers)
+template <int G, int W, int KW = 4>
 __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
   static_assert(G >= 1 && G <= 16, "query heads on the MFMA N axis");
   static_assert(W >= KW, "one page per key wave");
@@ -726,7 +728,7 @@ __device__ __forceinline__ void oproj(const QAArgs& a, int g, char* smem, const 
   }
 }
 
-template <int G>
+template <int G, int KW = 4>
 constexpr size_t consumer_lds() {
   const size_t v = sizeof(bf16) * KW * HD * VT;
   const size_t o = sizeof(float) * KW * G * HD;
@@ -744,13 +746,13 @@ size_t consumer_lds_for(int G) {
   return 0;
 }
 
-template <int G, int W, bool FO>
+template <int G, int W, bool FO, int KW = 4>
 __global__ __launch_bounds__(W * 64) void qkv_attn_kernel(QAArgs a) {
   constexpr size_t kProd = sizeof(float) * ((W - 1) * 4 * 64 + W * 16);
-  constexpr size_t kCons = consumer_lds<G>();
+  constexpr size_t kCons = consumer_lds<G, KW>();
   __shared__ __attribute__((aligned(16))) char smem[kCons > kProd ? kCons : kProd];
   if ((int)blockIdx.x < a.n_cons) {
-    consumer<G, W>(a, blockIdx.x, smem);
+    consumer<G, W, KW>(a, blockIdx.x, smem);
   } else {
     const int pg = blockIdx.x - a.n_cons;
     if (!FO && a.ks > 1) {
@@ -772,14 +774,14 @@ __global__ __launch_bounds__(W * 64) void qkv_attn_kernel(QAArgs a) {
   }
 }
 
-template <int W, bool FO>
+template <int W, bool FO, int KW = 4>
 int launch_qa(const QAArgs& a, int G, int groups, hipStream_t stream) {
   const dim3 grid(a.n_cons + (FO ? groups : a.n_prod)), block(W * 64);
   switch (G) {
-    case 1: hipLaunchKernelGGL((qkv_attn_kernel<1, W, FO>), grid, block, 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((qkv_attn_kernel<2, W, FO>), grid, block, 0, stream, a); break;
-    case 4: hipLaunchKernelGGL((qkv_attn_kernel<4, W, FO>), grid, block, 0, stream, a); break;
-    case 8: hipLaunchKernelGGL((qkv_attn_kernel<8, W, FO>), grid, block, 0, stream, a); break;
+    case 1: hipLaunchKernelGGL((qkv_attn_kernel<1, W, FO, KW>), grid, block, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((qkv_attn_kernel<2, W, FO, KW>), grid, block, 0, stream, a); break;
+    case 4: hipLaunchKernelGGL((qkv_attn_kernel<4, W, FO, KW>), grid, block, 0, stream, a); break;
+    case 8: hipLaunchKernelGGL((qkv_attn_kernel<8, W, FO, KW>), grid, block, 0, stream, a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -920,6 +922,9 @@ static int qkv_attn_impl(const void* Wt, const void* X, int ldx, int M, int K, i
     return W == 8 ? launch_qa<8, true>(a, Hq / Hkv, groups, stream)
                   : launch_qa<4, true>(a, Hq / Hkv, groups, stream);
   }
+  if (((waves >> 16) & 0xff) == 2)  // the caller bounds every context to 128 keys
+    return W == 8 ? launch_qa<8, false, 2>(a, Hq / Hkv, groups, stream)
+                  : launch_qa<4, false, 2>(a, Hq / Hkv, groups, stream);
   return W == 8 ? launch_qa<8, false>(a, Hq / Hkv, groups, stream)
                 : launch_qa<4, false>(a, Hq / Hkv, groups, stream);
 }

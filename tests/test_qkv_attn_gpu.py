@@ -16,14 +16,14 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _setup(M, Hq, Hkv, K, seed):
+def _setup(M, Hq, Hkv, K, seed, max_keys=256):
     g = torch.Generator().manual_seed(seed)
     N = (Hq + 2 * Hkv) * 128
     w = torch.randn(N, K, generator=g) * 0.05
     wt = ops.tile_weight(w.to(torch.bfloat16)).to(DEV)
     x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
-    ctx = torch.randint(1, 257, (M,), generator=g, dtype=torch.int32)
-    ctx[0] = 256
+    ctx = torch.randint(1, max_keys + 1, (M,), generator=g, dtype=torch.int32)
+    ctx[0] = max_keys
     if M > 1:
         ctx[1] = 1
     P = 1 + 4 * M
@@ -45,16 +45,17 @@ def _two_kernel(d, Hq, Hkv, kc, vc):
     return q, out
 
 
-@pytest.mark.parametrize("ks", [1, 2, 3, 6])
+@pytest.mark.parametrize("ks,kw", [(1, 4), (2, 4), (3, 4), (6, 4), (1, 2), (2, 2)])
 @pytest.mark.parametrize("M,Hq,Hkv,K", [(1, 32, 8, 4096), (3, 32, 8, 1024), (16, 32, 8, 1024),
                                         (1, 8, 1, 8192), (5, 8, 1, 1024), (2, 4, 4, 512),
                                         (4, 16, 8, 512)])
-def test_qkv_attn_matches_two_kernels(M, Hq, Hkv, K, ks):
+def test_qkv_attn_matches_two_kernels(M, Hq, Hkv, K, ks, kw):
     """ks > 1: k-split producers (fp32 partials, the consumer sums them in slice order and
-    applies rstd, RoPE and the KV write itself)."""
+    applies rstd, RoPE and the KV write itself); kw = 2: consumers with two key waves for
+    contexts <= 128 keys."""
     if (K // 32) // ks < 4:
         pytest.skip("fewer than 4 k-steps per slice")
-    d = _setup(M, Hq, Hkv, K, seed=M * 100 + Hq + K)
+    d = _setup(M, Hq, Hkv, K, seed=M * 100 + Hq + K, max_keys=64 * kw)
     kc1, vc1 = d["kc"].clone(), d["vc"].clone()
     q_ref, ref = _two_kernel(d, Hq, Hkv, kc1, vc1)
     # fp32 reference of the attention on the two-kernel path's q and cache
@@ -67,7 +68,7 @@ def test_qkv_attn_matches_two_kernels(M, Hq, Hkv, K, ks):
         kc2, vc2 = d["kc"].clone(), d["vc"].clone()
         out = torch.full((M, Hq * 128), float("nan"), dtype=torch.bfloat16, device=DEV)
         ops.qkv_attn(d["wt"], d["x"], d["pos"], d["slots"], d["cs"], Hq, Hkv, kc2, vc2, d["bt"],
-                     d["ctx"], out, ws, err, waves=ks << 8)
+                     d["ctx"], out, ws, err, waves=(ks << 8) | ((kw if kw == 2 else 0) << 16))
         torch.cuda.synchronize()
         assert int(err.item()) == 0, "hand-off timed out"
         assert not out.isnan().any()
