@@ -88,18 +88,26 @@ def main():
                 rows.append(s)
             nb = rows[0].shape[0]
             ph = {k: [] for k in ("skew", "first", "stream", "drain", "meet", "epi", "end")}
+            by_xcd = {k: [[] for _ in range(8)] for k in ("first", "arrive")}
+            by_split = [[] for _ in range(16)]
             for s in rows:
                 t0 = int(s[:, 0].min())
+                for b, r in enumerate(s.tolist()):  # blockIdx b runs on XCD b % 8
+                    by_xcd["first"][b % 8].append((r[1] - r[0]) * TICK_US)
+                    by_xcd["arrive"][b % 8].append((r[2] - t0) * TICK_US)
+                    by_split[int(r[7]) % 16].append((r[2] - t0) * TICK_US)
                 ends = [int(v) for v in s[:, 5] if v != 0]
                 ph["end"].append((max(ends) - t0) * TICK_US if ends else 0.0)
                 for r in s.tolist():
                     ph["skew"].append((r[0] - t0) * TICK_US)
                     ph["first"].append((r[1] - r[0]) * TICK_US)
                     ph["stream"].append((r[2] - r[1]) * TICK_US)
-                    if r[3]:
+                    if r[3]:  # split-K (r5 granule seam: 3 = granules stored, 4 = polls done;
+                        # blocks whose wave 0 finishes no unit stamp neither 4 nor 5)
                         ph["drain"].append((r[3] - r[2]) * TICK_US)
-                        ph["meet"].append((r[4] - r[3]) * TICK_US)
-                        if r[5]:
+                        if r[4]:
+                            ph["meet"].append((r[4] - r[3]) * TICK_US)
+                        if r[4] and r[5]:
                             ph["epi"].append((r[5] - r[4]) * TICK_US)
                     elif r[5]:
                         ph["epi"].append((r[5] - r[2]) * TICK_US)
@@ -109,6 +117,9 @@ def main():
             for k, v in ph.items():
                 if v:
                     out_row[k] = [round(q(v, p), 2) for p in (0.1, 0.5, 0.9, 1.0)]
+            for k, v in by_xcd.items():  # per-XCD median / max (straggler placement)
+                out_row[k + "_by_xcd"] = [[round(q(x, 0.5), 2), round(q(x, 1.0), 2)] for x in v if x]
+            out_row["arrive_by_split"] = [[round(q(x, 0.5), 2), round(q(x, 1.0), 2)] for x in by_split if x]
             print(json.dumps(out_row), flush=True)
         del wts
         torch.cuda.empty_cache()

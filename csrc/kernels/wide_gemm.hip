@@ -47,7 +47,25 @@ constexpr int NT = 512;   // 8 waves
 constexpr int KC = 8;     // k-steps per chunk: wave w DMA-loads k-step w of every m-tile
 constexpr int MAX_SPLIT = 16;  // K slices per tile (the rstd reduction unrolls over them)
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-using pgemm::SplitArgs;
+typedef unsigned long long u64;
+
+// Split-K seam (r5): the K slices of a tile meet through 8-byte tagged granules
+// {tag << 32 | fp32} (cdna_hip_programming.md R2: the data is the flag).  Each slice stores
+// its partials once and moves on; the wave finishing an (output group, m-tile) unit polls
+// the granules of every slice and needs no ticket, generation flip or second load.
+// Tags: a block takes ticket[tile] (64-bit, monotonic) BEFORE its weight stream; the
+// splitk blocks of launch L of a (splitk, tile) pair draw L*splitk .. L*splitk + splitk-1, so
+// tag = ticket / splitk + 1 is the same in all of them and new to every granule of the
+// tile's region (each splitk value owns its tickets and its regions; stale granules carry
+// older tags).  Replaces the write-through slabs + arrival ticket + generation flip, whose
+// ~6 serial round trips cost 4-5 us per launch at 48 rows (r5 stamps).
+struct GranArgs {
+  int splitk;
+  u64* gran;      // [tile][splitk][8 waves][4 m-tiles][4][64 lanes] partials
+  u64* ssg;       // [tile][splitk][64 rows] RMSNorm row sums of squares
+  u64* ticket;    // [tile]
+  int* err;       // set if a finishing wave waited past the spin bound (results invalid)
+};
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -68,7 +86,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
                                                        const bf16* __restrict__ X, int ldx, int M,
                                                        int K, int n_tiles, int up_off,
                                                        void* __restrict__ out, int ldo, float eps,
-                                                       EpiArgs ea, SplitArgs sp) {
+                                                       EpiArgs ea, GranArgs ga) {
   constexpr bool SILU = EPI == EPI_SILU;
   // pipeline depth: D chunks ahead (RS = D + 1 register sets of KC weight fragments: 128
   // VGPRs at D = 3), activation ring of D + 2 slots (<= 128 KiB of LDS at every MT)
@@ -81,7 +99,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   __shared__ __attribute__((aligned(16))) bf16x8 ring[NSLOT * SLOT];
   __shared__ float ss_l[2][4][16];
 
-  const int splitk = SPLIT ? sp.splitk : 1;
+  const int splitk = SPLIT ? ga.splitk : 1;
   const int b = xcd_remap(blockIdx.x, n_tiles * splitk);
   const int tile = b / splitk, split = b % splitk;  // a tile's slices are consecutive
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -92,6 +110,11 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   WSTAMP(0, wall_clock64());
   WSTAMP(6, tile);
   WSTAMP(7, split);
+  // this launch's tag: the ticket load is the oldest in flight, long landed at the seam
+  __shared__ unsigned tag_l;
+  u64 tkt = 0;
+  if constexpr (SPLIT)
+    if (tid == 0) tkt = __hip_atomic_fetch_add(&ga.ticket[tile], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   const int gw = SILU ? (w < 4 ? tile * 4 + w : tile * 4 + (w - 4) + up_off) : tile * 8 + w;
   const bf16x8* wsrc = Wt + (size_t)gw * S * 64 + lane;
@@ -128,10 +151,13 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     }
   };
 
-  // The output group this wave finishes, if any: group w (SILU: gate/up pair w < 4); under
-  // split-K only slice (w % splitk) finishes it.
+  // The units this wave finishes: output group w (SILU: gate/up pair w < 4) at m-tile i;
+  // under split-K unit (w, i) belongs to slice (w * MT + i) % splitk, so the 8 * MT units
+  // of a tile spread over all its slices' waves (at most one each from splitk >= MT).
   const int r = lane & 15, q = lane >> 4;
-  const bool fin = w < (SILU ? 4 : 8) && (!SPLIT || (w % splitk) == split);
+  auto owns = [&](int i) {
+    return w < (SILU ? 4 : 8) && (!SPLIT || (w * MT + i) % splitk == split);
+  };
   const int g = SILU ? tile * 4 + w : tile * 8 + w;
   // Epilogue operands, issued as ONE batch per lane BEFORE the weight stream (they are the
   // oldest loads in flight, so the counted chunk waits below still hold, and they have long
@@ -149,7 +175,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = 16 * i + 4 * q + j;
-      const bool ok = fin && m < M;
+      const bool ok = owns(i) && m < M;
       res[i][j] = 0.f;
       slotv[i][j] = -1;
       posv[i][j] = -1;
@@ -284,102 +310,124 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     WSTAMP(5, wall_clock64());
     return;
   } else {
-    // ---- parallel split-K: write-through slabs [tile][split][wave][MT] (f32x4 per lane) ----
-    const __amdgpu_buffer_rsrc_t rsl = pgemm::raw_rsrc(sp.slab);
-    const size_t tile_v = (size_t)tile * splitk * 8 * MT * 64;  // f32x4 index of slice 0
+    // ---- split-K seam over tagged granules (see GranArgs) ----
+    if (tid == 0) tag_l = (unsigned)(tkt / (u64)splitk) + 1u;
+    __syncthreads();  // ss_l complete, tag_l published
+    const unsigned tag = tag_l;
+    const u64 tg = (u64)tag << 32;
+    u64* gt = ga.gran + (size_t)tile * splitk * 8 * 4 * 256;  // this tile's region
+    auto gidx = [&](int s2, int wv, int i, int j) { return (((s2 * 8 + wv) * 4 + i) * 4 + j) * 64 + lane; };
 #pragma unroll
     for (int i = 0; i < MT; ++i)
-      pgemm::store_sc1(rsl, (int)((tile_v + (((size_t)split * 8 + w) * MT + i) * 64 + lane) * 16),
-                       acc[i]);
-    if constexpr (NORM) {
-      __syncthreads();  // ss_l complete
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __hip_atomic_store(gt + gidx(split, w, i, j), tg | __float_as_uint(acc[i][j]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    u64* st = ga.ssg + (size_t)tile * splitk * 64;
+    if constexpr (NORM)
       if (tid < 16 * MT) {
         const int i = tid >> 4, rr = tid & 15;
-        __hip_atomic_store(&sp.ss_slab[((size_t)tile * splitk + split) * 64 + 16 * i + rr],
-                           ss_l[0][i][rr] + ss_l[1][i][rr], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);  // write-through
+        __hip_atomic_store(st + split * 64 + tid, tg | __float_as_uint(ss_l[0][i][rr] + ss_l[1][i][rr]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     WSTAMP(3, wall_clock64());
-    if (tid == 0) {
-      const unsigned g0 = __hip_atomic_load(&sp.gen[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // read the generation BEFORE arriving
-      const unsigned t = __hip_atomic_fetch_add(&sp.counters[tile], 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      if (t == (unsigned)splitk - 1) {
-        (void)__hip_atomic_exchange(&sp.counters[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // re-armed before the flip
-        __hip_atomic_store(&sp.gen[tile], g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        const long long t0 = wall_clock64();
-        while (__hip_atomic_load(&sp.gen[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) any |= owns(i);
+    if (!any) return;
+    // Finish the owned units.  One poll sweep re-reads a batch of SB slices' granules (and,
+    // for the first batch, the rows' sum-of-squares granules) until every tag is this
+    // launch's; the partials are summed in slice order (deterministic).
+    constexpr int SB = SILU ? 4 : 8;
+    const long long t0 = wall_clock64();
+    bool failed = false;
+    auto ready = [&](u64 x) { return (unsigned)(x >> 32) == tag; };
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (!owns(i)) continue;
+      f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f}, upv = f32x4{0.f, 0.f, 0.f, 0.f};
+      float rowss = 0.f;  // NORM: lane l holds row 16 i + (l & 15) after the shuffles
+      for (int s0 = 0; s0 < splitk; s0 += SB) {
+        u64 pt[SB][4], pu[SB][4], sv[4];
+        for (;;) {
+          bool ok = true;
+#pragma unroll
+          for (int s = 0; s < SB; ++s) {
+            if (s0 + s >= splitk) break;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              pt[s][j] = __hip_atomic_load(gt + gidx(s0 + s, w, i, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if constexpr (SILU)
+                pu[s][j] = __hip_atomic_load(gt + gidx(s0 + s, w + 4, i, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+          if constexpr (NORM)
+            if (s0 == 0) {
+              // lane l: row 16 i + (l & 15), slices (l >> 4) + 4 k
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int s2 = q + 4 * k;
+                sv[k] = s2 < splitk ? __hip_atomic_load(st + s2 * 64 + 16 * i + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : tg;
+              }
+            }
+#pragma unroll
+          for (int s = 0; s < SB; ++s) {
+            if (s0 + s >= splitk) break;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              ok &= ready(pt[s][j]);
+              if constexpr (SILU) ok &= ready(pu[s][j]);
+            }
+          }
+          if constexpr (NORM)
+            if (s0 == 0) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) ok &= ready(sv[k]);
+            }
+          if (__all(ok) || failed) break;
           if (wall_clock64() - t0 > pgemm::SPLIT_SPIN_TICKS) {
-            __hip_atomic_store(sp.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
+            if (lane == 0) __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            failed = true;
           }
           __builtin_amdgcn_s_sleep(1);
         }
-      }
-    }
-    __syncthreads();
-    WSTAMP(4, wall_clock64());
-    // every slice's partials are visible.  Rows' rstd: one lane per row sums the slices'
-    // row sums (all loads issued before the first add) into LDS
-    __shared__ float rstd_l[64];
-    if constexpr (NORM) {
-      if (tid < 16 * MT) {
-        float pv[MAX_SPLIT];
 #pragma unroll
-        for (int s2 = 0; s2 < MAX_SPLIT; ++s2)
-          pv[s2] = __hip_atomic_load(&sp.ss_slab[((size_t)tile * splitk + min(s2, splitk - 1)) * 64 + tid],
-                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        float t2 = 0.f;
+        for (int s = 0; s < SB; ++s) {
+          if (s0 + s >= splitk) break;
 #pragma unroll
-        for (int s2 = 0; s2 < MAX_SPLIT; ++s2) t2 += s2 < splitk ? pv[s2] : 0.f;
-        rstd_l[tid] = rstd_from(t2);
-      }
-      __syncthreads();
-    }
-    if (!fin) return;
-    // the finished group's partials, summed in slice order; loads in batches of SB slices
-    // (clamped indices: straight-line code, one wait per batch).  SB = 8 covers the usual
-    // 5-8 slices in ONE round trip (batches of 4 cost a second one, ~1 us, r5 stamps); the
-    // SwiGLU form loads gate and up partials, so it keeps 4 (VGPRs)
-    constexpr int SB = SILU ? 4 : 8;
-    f32x4 tot[MT], up[MT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      tot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      up[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    for (int s0 = 0; s0 < splitk; s0 += SB) {
-      f32x4 pt[SB][MT], pu[SB][MT];
-#pragma unroll
-      for (int s = 0; s < SB; ++s) {
-        const int s2 = min(s0 + s, splitk - 1);
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          pt[s][i] = pgemm::load_sc1(rsl, (int)((tile_v + (((size_t)s2 * 8 + w) * MT + i) * 64 + lane) * 16));
-          if constexpr (SILU)
-            pu[s][i] = pgemm::load_sc1(rsl, (int)((tile_v + (((size_t)s2 * 8 + w + 4) * MT + i) * 64 + lane) * 16));
+          for (int j = 0; j < 4; ++j) {
+            tot[j] += __uint_as_float((unsigned)pt[s][j]);
+            if constexpr (SILU) upv[j] += __uint_as_float((unsigned)pu[s][j]);
+          }
         }
+        if constexpr (NORM)
+          if (s0 == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (q + 4 * k < splitk) rowss += __uint_as_float((unsigned)sv[k]);
+          }
+      }
+      WSTAMP(4, wall_clock64());
+      if constexpr (NORM) {
+        rowss += __shfl_xor(rowss, 16, 64);
+        rowss += __shfl_xor(rowss, 32, 64);
       }
 #pragma unroll
-      for (int s = 0; s < SB; ++s) {
-        if (s0 + s >= splitk) break;
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          tot[i] += pt[s][i];
-          if constexpr (SILU) up[i] += pu[s][i];
+      for (int j = 0; j < 4; ++j) {
+        const int m = 16 * i + 4 * q + j;
+        float sc = 1.f;
+        if constexpr (NORM) sc = rstd_from(__shfl(rowss, 4 * q + j, 64));
+        const float v = tot[j] * sc;
+        if constexpr (EPI == EPI_QKV_ROPE) {
+          epi_store<EPI>(m, m < M, g, r, v, 0.f, out, ldo, ea, csv[i][j], slotv[i][j]);
+        } else if constexpr (EPI == EPI_RESID) {
+          if (m < M) reinterpret_cast<bf16*>(out)[(size_t)m * ldo + g * 16 + r] = f2bf(res[i][j] + v);
+        } else {
+          epi_store<EPI>(m, m < M, g, r, v, upv[j] * sc, out, ldo, ea);
         }
       }
     }
-    epilogue(tot, up, [&](int i, int j) {
-      if constexpr (!NORM) return 1.f;
-      return rstd_l[16 * i + 4 * q + j];
-    });
 #ifdef WIDE_STAMP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -390,36 +438,68 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
 static int g_max_split = MAX_SPLIT;
 static int g_res = 1;  // RES variant where a slice's activations fit LDS (A/B: 0 = ring only)
 
+// Granule workspaces, one per K-slice count (GranArgs: tickets and granule regions of one
+// splitk value are never shared with another).  Sized for the most tiles that splitk allows
+// on this device (grid <= one block per CU), zeroed at allocation; a grown workspace never
+// frees the previous buffer (a captured hipGraph replays against it, see pgemm::split_ws).
+struct GranWs {
+  void* buf = nullptr;
+  int tiles = 0;
+};
+static GranWs g_gran_ws[MAX_SPLIT + 1];
+
+static bool gran_ws(int splitk, int n_tiles, hipStream_t st, GranArgs* ga) {
+  if (splitk < 2 || splitk > MAX_SPLIT) return false;
+  char* ws = nullptr;  // the fault word lives at the end of the split-K workspace
+  if (!pgemm::split_ws(0, st, &ws)) return false;
+  GranWs& g = g_gran_ws[splitk];
+  auto bytes_for = [&](int tiles) {
+    return (size_t)tiles * 8 + (size_t)tiles * splitk * 64 * 8 + (size_t)tiles * splitk * 8192 * 8 + 256;
+  };
+  if (g.tiles < n_tiles) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) return false;  // cannot allocate while capturing
+    const int tiles = std::max(n_tiles, pgemm::cu_count() / splitk);
+    void* buf = nullptr;
+    if (hipMalloc(&buf, bytes_for(tiles)) != hipSuccess) return false;
+    if (hipMemsetAsync(buf, 0, bytes_for(tiles), st) != hipSuccess) return false;
+    g.buf = buf;
+    g.tiles = tiles;
+  }
+  char* base = (char*)g.buf;
+  const size_t tk = ((size_t)g.tiles * 8 + 255) / 256 * 256;
+  ga->splitk = splitk;
+  ga->ticket = (u64*)base;
+  ga->ssg = (u64*)(base + tk);
+  ga->gran = (u64*)(base + tk + (size_t)g.tiles * splitk * 64 * 8);
+  ga->err = (int*)(ws + pgemm::g_split_ws.bytes - sizeof(unsigned));
+  return true;
+}
+
 template <int MT, int EPI, bool NORM, bool SPLIT, bool RES>
 int launch_v(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles, int up_off,
              void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st,
-             const SplitArgs& sp) {
-  hipLaunchKernelGGL((wide_gemm_kernel<MT, EPI, NORM, SPLIT, RES>), dim3(n_tiles * sp.splitk),
+             const GranArgs& ga) {
+  hipLaunchKernelGGL((wide_gemm_kernel<MT, EPI, NORM, SPLIT, RES>), dim3(n_tiles * ga.splitk),
                      dim3(NT), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, n_tiles, up_off,
-                     out, ldo, eps, ea, sp);
+                     out, ldo, eps, ea, ga);
   return (int)hipGetLastError();
 }
 
 template <int MT, int EPI, bool NORM>
 int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles, int up_off,
               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st, int splitk) {
-  using namespace pgemm;
   const int nc = K / (32 * KC);
   const bool res = g_res && (nc + splitk - 1) / splitk <= res_chunks<MT>();
   if (splitk > 1) {
-    const size_t slab = (size_t)n_tiles * splitk * 8 * MT * 64 * sizeof(f32x4);
-    const size_t ssb = (size_t)n_tiles * splitk * 64 * sizeof(float);
-    char* ws = nullptr;
-    if ((size_t)n_tiles * sizeof(unsigned) >= kCounterBytes / 2 || slab + ssb >= 0x7FFFFFFF ||
-        !split_ws(slab + ssb, st, &ws))  // (no workspace growth while a graph is captured)
+    GranArgs ga{};
+    if (!gran_ws(splitk, n_tiles, st, &ga))  // (no workspace growth while a graph is captured)
       return launch_mt<MT, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, 1);
-    unsigned* ctr = (unsigned*)(ws + g_split_ws.bytes - kCounterBytes);
-    constexpr size_t nw = kCounterBytes / sizeof(unsigned);
-    SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), ctr, ctr + nw / 2, (int*)(ctr + nw - 1), 1};
-    return res ? launch_v<MT, EPI, NORM, true, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, sp)
-               : launch_v<MT, EPI, NORM, true, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, sp);
+    return res ? launch_v<MT, EPI, NORM, true, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, ga)
+               : launch_v<MT, EPI, NORM, true, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, ga);
   }
-  SplitArgs none{1, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  GranArgs none{1, nullptr, nullptr, nullptr, nullptr};
   return res ? launch_v<MT, EPI, NORM, false, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none)
              : launch_v<MT, EPI, NORM, false, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none);
 }
