@@ -29,6 +29,8 @@
 // m-tile per wave pair); the row sums of the slices meet in the reduction.
 // Measured (docs/ARCHITECTURE.md "Wide mid-M family"): the autotuner's pick at 33-64 rows
 // for gate_up, down and qkv; the split-K seam (~5-6 us) is what it still pays on N <= 6144.
+#include <cstdlib>
+#include <type_traits>
 #define PGEMM_NO_DISPATCH
 #include "prefill_gemm.h"
 
@@ -53,18 +55,22 @@ typedef unsigned long long u64;
 // {tag << 32 | fp32} (cdna_hip_programming.md R2: the data is the flag).  Each slice stores
 // its partials once and moves on; the wave finishing an (output group, m-tile) unit polls
 // the granules of every slice and needs no ticket, generation flip or second load.
-// Tags: a block takes ticket[tile] (64-bit, monotonic) BEFORE its weight stream; the
-// splitk blocks of launch L of a (splitk, tile) pair draw L*splitk .. L*splitk + splitk-1, so
-// tag = ticket / splitk + 1 is the same in all of them and new to every granule of the
-// tile's region (each splitk value owns its tickets and its regions; stale granules carry
-// older tags).  Replaces the write-through slabs + arrival ticket + generation flip, whose
+// Tags: a block takes ticket[tile] (64-bit, monotonic) BEFORE its weight stream and shares
+// it through LDS at the chunk-0 barrier; the splitk blocks of launch L of a (splitk, tile)
+// pair draw L*splitk .. L*splitk + splitk-1, so tag = ticket / splitk + 1 is the same in all
+// of them and new to every granule of the tile's region (each splitk value owns its tickets
+// and its regions; stale granules carry older tags).  (A ticket per WAVE measured 2x slower:
+// 64 agent-scope atomics per address serialise at the memory side, and the first chunk's
+// loads queue behind them.)  No wave waits for the other waves of its block after its
+// stream: each publishes its partials and its k-parity's row sums of squares at once.  Replaces the write-through slabs + arrival ticket + generation flip, whose
 // ~6 serial round trips cost 4-5 us per launch at 48 rows (r5 stamps).
 struct GranArgs {
   int splitk;
   u64* gran;      // [tile][splitk][8 waves][4 m-tiles][4][64 lanes] partials
-  u64* ssg;       // [tile][splitk][64 rows] RMSNorm row sums of squares
+  u64* ssg;       // [tile][splitk][2 k parities][64 rows] RMSNorm row sums of squares
   u64* ticket;    // [tile]
   int* err;       // set if a finishing wave waited past the spin bound (results invalid)
+  int align;      // slice boundaries rounded to multiples of this many k-steps (1 or KC)
 };
 
 template <int N>
@@ -104,9 +110,14 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   const int tile = b / splitk, split = b % splitk;  // a tile's slices are consecutive
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int S = K >> 5;
-  const int nc_all = S / KC;
-  const int c0 = split * nc_all / splitk, c1 = (split + 1) * nc_all / splitk;
-  const int n = c1 - c0;
+  // K slices in k-step units (r5: chunk-unit slices left qkv's 16 chunks in 5 slices as
+  // 3/3/3/3/4 and the seam waited ~2.7 us for the long one); chunk c of the slice covers
+  // k-steps ks0 + 8c .. + kv(c) - 1, only the last one partial.  A partial chunk still issues
+  // full-count loads (clamped to its last k-step) so the counted vmcnt waits hold.
+  const int al = SPLIT ? ga.align : 1;
+  const int ks0 = split * (S / al) / splitk * al, nks = (split + 1) * (S / al) / splitk * al - ks0;
+  const int n = (nks + KC - 1) / KC;
+  auto kv_of = [&](int c) { return min(KC, nks - c * KC); };
   WSTAMP(0, wall_clock64());
   WSTAMP(6, tile);
   WSTAMP(7, split);
@@ -122,19 +133,21 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int row = min(16 * i + (lane & 15), M - 1);
-    asrc[i] = X + (size_t)row * ldx + 32 * w + 8 * (lane >> 4);
+    asrc[i] = X + (size_t)row * ldx + 8 * (lane >> 4);
   }
 
   auto issue_a = [&](int c) {
-    bf16x8* base = ring + ((c - c0) % NSLOT) * SLOT;
+    bf16x8* base = ring + (c % NSLOT) * SLOT;
+    const int kk = ks0 + c * KC + min(w, kv_of(c) - 1);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (size_t)c * KC * 32),
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (size_t)kk * 32),
                                        (lds_ptr_t)(base + (i * KC + w) * 64), 16, 0, 0);
   };
   auto issue_w = [&](int c, bf16x8(&wr)[KC]) {
+    const int kb = ks0 + c * KC, kl = kv_of(c) - 1;
 #pragma unroll
-    for (int k = 0; k < KC; ++k) wr[k] = __builtin_nontemporal_load(wsrc + (size_t)(c * KC + k) * 64);
+    for (int k = 0; k < KC; ++k) wr[k] = __builtin_nontemporal_load(wsrc + (size_t)(kb + min(k, kl)) * 64);
   };
   auto issue = [&](int c, bf16x8(&wr)[KC]) {
     if constexpr (!RES) issue_a(c);
@@ -195,10 +208,11 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   float ss = 0.f;  // NORM: rows of m-tile (w & 3), k-steps of parity (w >> 2), this lane's 8 k
   const int sq_mt = w & 3, sq_par = w >> 2;
 
-  auto compute = [&](int c, const bf16x8(&wr)[KC]) {
-    const bf16x8* base = ring + ((c - c0) % NSLOT) * SLOT;
+  auto compute_kv = [&](const bf16x8* base, const bf16x8(&wr)[KC], int kv, auto full) {
+    constexpr bool FULL = decltype(full)::value;
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
+      if (!FULL && k >= kv) break;
       bf16x8 a[MT];
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[i] = base[(i * KC + k) * 64 + lane];
@@ -210,10 +224,19 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       if (sq_mt < MT) {
 #pragma unroll
         for (int k = 0; k < KC; k += 2) {
+          if (!FULL && k + sq_par >= kv) break;
           ss = sumsq8(base[(sq_mt * KC + k + sq_par) * 64 + lane], ss);
         }
       }
     }
+  };
+  auto compute = [&](int c, const bf16x8(&wr)[KC]) {
+    const bf16x8* base = ring + (c % NSLOT) * SLOT;
+    const int kv = kv_of(c);
+    if (kv == KC)
+      compute_kv(base, wr, KC, std::true_type{});
+    else  // a slice's last chunk, partial
+      compute_kv(base, wr, kv, std::false_type{});
   };
 
   // D chunks (activation DMA + this wave's weights) are in flight ahead of the one being
@@ -221,23 +244,24 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   // the ring slot refilled at step t (chunk t+D's) was last read at t-2, before barrier t-1
   bf16x8 wr[RS][KC];
   if constexpr (RES)  // the whole slice's activations first (host: n <= res_chunks)
-    for (int c = 0; c < n; ++c) issue_a(c0 + c);
+    for (int c = 0; c < n; ++c) issue_a(c);
 #pragma unroll
   for (int j = 0; j < D; ++j)
-    if (j < n) issue(c0 + j, wr[j]);
+    if (j < n) issue(j, wr[j]);
   for (int tb = 0; tb < n; tb += RS) {
 #pragma unroll
     for (int j = 0; j < RS; ++j) {
       const int t = tb + j;
       if (t >= n) break;
-      if (t + D < n) issue(c0 + t + D, wr[(j + D) % RS]);
+      if (t + D < n) issue(t + D, wr[(j + D) % RS]);
       wait_chunks(min(D, n - 1 - t));
       if (!RES || t == 0) {  // RES: chunk 0's weights landed => this wave's DMA parts too
+        if (SPLIT && t == 0 && tid == 0) tag_l = (unsigned)(tkt / (u64)splitk) + 1u;  // landed (oldest load)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (t == 0) WSTAMP(1, wall_clock64());
       }
-      compute(c0 + t, wr[j]);
+      compute(t, wr[j]);
     }
   }
 
@@ -246,7 +270,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   if constexpr (NORM) {
     ss += __shfl_xor(ss, 16, 64);
     ss += __shfl_xor(ss, 32, 64);
-    if (sq_mt < MT && lane < 16) ss_l[sq_par][sq_mt][lane] = ss;
+    if (!SPLIT && sq_mt < MT && lane < 16) ss_l[sq_par][sq_mt][lane] = ss;
   }
   if constexpr (EPI == EPI_QKV_ROPE) {
     const int kk = g & 7;
@@ -311,9 +335,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     return;
   } else {
     // ---- split-K seam over tagged granules (see GranArgs) ----
-    if (tid == 0) tag_l = (unsigned)(tkt / (u64)splitk) + 1u;
-    __syncthreads();  // ss_l complete, tag_l published
-    const unsigned tag = tag_l;
+    const unsigned tag = tag_l;  // written before the chunk-0 barrier
     const u64 tg = (u64)tag << 32;
     u64* gt = ga.gran + (size_t)tile * splitk * 8 * 4 * 256;  // this tile's region
     auto gidx = [&](int s2, int wv, int i, int j) { return (((s2 * 8 + wv) * 4 + i) * 4 + j) * 64 + lane; };
@@ -323,13 +345,11 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       for (int j = 0; j < 4; ++j)
         __hip_atomic_store(gt + gidx(split, w, i, j), tg | __float_as_uint(acc[i][j]),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    u64* st = ga.ssg + (size_t)tile * splitk * 64;
+    u64* st = ga.ssg + (size_t)tile * splitk * 128;  // [split][parity][64 rows]
     if constexpr (NORM)
-      if (tid < 16 * MT) {
-        const int i = tid >> 4, rr = tid & 15;
-        __hip_atomic_store(st + split * 64 + tid, tg | __float_as_uint(ss_l[0][i][rr] + ss_l[1][i][rr]),
+      if (sq_mt < MT && lane < 16)
+        __hip_atomic_store(st + (split * 2 + sq_par) * 64 + 16 * sq_mt + lane, tg | __float_as_uint(ss),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
     WSTAMP(3, wall_clock64());
     bool any = false;
 #pragma unroll
@@ -348,7 +368,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f}, upv = f32x4{0.f, 0.f, 0.f, 0.f};
       float rowss = 0.f;  // NORM: lane l holds row 16 i + (l & 15) after the shuffles
       for (int s0 = 0; s0 < splitk; s0 += SB) {
-        u64 pt[SB][4], pu[SB][4], sv[4];
+        u64 pt[SB][4], pu[SB][4], sv[8];
         for (;;) {
           bool ok = true;
 #pragma unroll
@@ -363,12 +383,12 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
           }
           if constexpr (NORM)
             if (s0 == 0) {
-              // lane l: row 16 i + (l & 15), slices (l >> 4) + 4 k
+              // lane l: row 16 i + (l & 15), (slice, parity) pairs c = (l >> 4) + 4 k
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const int s2 = q + 4 * k;
-                sv[k] = s2 < splitk ? __hip_atomic_load(st + s2 * 64 + 16 * i + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                    : tg;
+              for (int k = 0; k < 8; ++k) {
+                const int c = q + 4 * k;
+                sv[k] = c < 2 * splitk ? __hip_atomic_load(st + c * 64 + 16 * i + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : tg;
               }
             }
 #pragma unroll
@@ -383,7 +403,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
           if constexpr (NORM)
             if (s0 == 0) {
 #pragma unroll
-              for (int k = 0; k < 4; ++k) ok &= ready(sv[k]);
+              for (int k = 0; k < 8; ++k) ok &= ready(sv[k]);
             }
           if (__all(ok) || failed) break;
           if (wall_clock64() - t0 > pgemm::SPLIT_SPIN_TICKS) {
@@ -404,8 +424,8 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
         if constexpr (NORM)
           if (s0 == 0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-              if (q + 4 * k < splitk) rowss += __uint_as_float((unsigned)sv[k]);
+            for (int k = 0; k < 8; ++k)
+              if (q + 4 * k < 2 * splitk) rowss += __uint_as_float((unsigned)sv[k]);
           }
       }
       WSTAMP(4, wall_clock64());
@@ -448,13 +468,22 @@ struct GranWs {
 };
 static GranWs g_gran_ws[MAX_SPLIT + 1];
 
+// P2P_WIDE_KSTEP=0: K slices on chunk boundaries (8 k-steps; r5 A/B against k-step slices)
+static int kstep_align() {
+  static int a = [] {
+    const char* e = std::getenv("P2P_WIDE_KSTEP");
+    return (e && e[0] == '0') ? KC : 1;
+  }();
+  return a;
+}
+
 static bool gran_ws(int splitk, int n_tiles, hipStream_t st, GranArgs* ga) {
   if (splitk < 2 || splitk > MAX_SPLIT) return false;
   char* ws = nullptr;  // the fault word lives at the end of the split-K workspace
   if (!pgemm::split_ws(0, st, &ws)) return false;
   GranWs& g = g_gran_ws[splitk];
   auto bytes_for = [&](int tiles) {
-    return (size_t)tiles * 8 + (size_t)tiles * splitk * 64 * 8 + (size_t)tiles * splitk * 8192 * 8 + 256;
+    return (size_t)tiles * 8 + (size_t)tiles * splitk * 128 * 8 + (size_t)tiles * splitk * 8192 * 8 + 256;
   };
   if (g.tiles < n_tiles) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -472,8 +501,9 @@ static bool gran_ws(int splitk, int n_tiles, hipStream_t st, GranArgs* ga) {
   ga->splitk = splitk;
   ga->ticket = (u64*)base;
   ga->ssg = (u64*)(base + tk);
-  ga->gran = (u64*)(base + tk + (size_t)g.tiles * splitk * 64 * 8);
+  ga->gran = (u64*)(base + tk + (size_t)g.tiles * splitk * 128 * 8);
   ga->err = (int*)(ws + pgemm::g_split_ws.bytes - sizeof(unsigned));
+  ga->align = kstep_align();
   return true;
 }
 
@@ -490,8 +520,9 @@ int launch_v(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles, 
 template <int MT, int EPI, bool NORM>
 int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles, int up_off,
               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st, int splitk) {
-  const int nc = K / (32 * KC);
-  const bool res = g_res && (nc + splitk - 1) / splitk <= res_chunks<MT>();
+  const int al = splitk > 1 ? kstep_align() : 1;
+  const int S = K / 32, slice_ks = ((S / al + splitk - 1) / splitk) * al;  // the longest slice's k-steps
+  const bool res = g_res && (slice_ks + KC - 1) / KC <= res_chunks<MT>();
   if (splitk > 1) {
     GranArgs ga{};
     if (!gran_ws(splitk, n_tiles, st, &ga))  // (no workspace growth while a graph is captured)
@@ -499,7 +530,7 @@ int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles,
     return res ? launch_v<MT, EPI, NORM, true, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, ga)
                : launch_v<MT, EPI, NORM, true, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, ga);
   }
-  GranArgs none{1, nullptr, nullptr, nullptr, nullptr};
+  GranArgs none{1, nullptr, nullptr, nullptr, nullptr, 1};
   return res ? launch_v<MT, EPI, NORM, false, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none)
              : launch_v<MT, EPI, NORM, false, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none);
 }
