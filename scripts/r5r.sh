@@ -13,7 +13,9 @@ prof() {  # prof <name> <timeout> <tokens> cmd...
   python3 scripts/kstats_db.py "$db" 30 --tokens "$tok" > gpurun_out/${T}_kstats_$name.md && rm -rf /tmp/prof_$name
 }
 run 300 ${T}_ttft.log python bench/ttft_breakdown.py --message 4 --pages 2 &&
+run 300 ${T}_ttft8.log python bench/ttft_breakdown.py --message 4 --pages 2 --peers 8 &&
 run 600 ${T}_bench.log python bench.py --steps 20 --warmup 5 &&
+prof ttft8 300 0 python3 bench/ttft_breakdown.py --message 4 --pages 2 --peers 8 --iters 20 &&
 prof ttft 300 0 python3 bench/ttft_breakdown.py --message 4 --pages 2 --iters 20 &&
-prof bench 600 256 python3 bench.py --steps 3 --warmup 1 &&
-prof proxy 600 256 python3 bench/tp_rank_proxy.py --steps 3 --warmup 1
+prof bench 600 0 python3 bench.py --steps 3 --warmup 1 &&
+prof proxy 600 0 python3 bench/tp_rank_proxy.py --steps 3 --warmup 1
