@@ -406,11 +406,15 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
               for (int k = 0; k < 8; ++k) ok &= ready(sv[k]);
             }
           if (__all(ok) || failed) break;
-          if (wall_clock64() - t0 > pgemm::SPLIT_SPIN_TICKS) {
+          const long long waited = wall_clock64() - t0;
+          if (waited > pgemm::SPLIT_SPIN_TICKS) {
             if (lane == 0) __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             failed = true;
           }
-          __builtin_amdgcn_s_sleep(1);
+          // a sweep re-reads up to 40 granules per lane: past ~5 us (a late slice, not the
+          // usual skew) back off so a long wait does not load the memory system
+          if (waited > 500) __builtin_amdgcn_s_sleep(32);
+          else __builtin_amdgcn_s_sleep(1);
         }
 #pragma unroll
         for (int s = 0; s < SB; ++s) {
@@ -537,11 +541,26 @@ int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles,
 
 // K slices: the grid must stay <= one block per CU (every slice of a tile resident for the
 // parallel reduction) and each slice keeps >= 2 chunks; otherwise as many as fill the CUs.
+// P2P_WIDE_SPLIT_CAP: hard cap on the K slices of every launch, requested ones included.  The
+// slices of a tile meet in the kernel, so they must be resident together: true for a grid of
+// at most one workgroup per CU on a device of its own, not for several processes sharing one
+// device (virtual-rank tests), where the other processes' spinning grids can hold the CUs a
+// late slice needs; those tests set the cap to 1.
+static int split_cap() {
+  static int c = [] {
+    const char* e = std::getenv("P2P_WIDE_SPLIT_CAP");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 ? v : MAX_SPLIT;
+  }();
+  return c;
+}
+
 static int pick_split(int n_tiles, int nc, int req) {
   const int cus = pgemm::cu_count();
   if (cus <= 0) return 1;
   int s = req > 0 ? std::min(std::min(req, nc), MAX_SPLIT)
                   : std::min(cus / n_tiles, std::min(g_max_split, nc / 2));
+  s = std::min(s, split_cap());
   while (s > 1 && n_tiles * s > cus) --s;
   return std::max(1, s);
 }

@@ -360,6 +360,10 @@ def _rank_main(spec, replica, rank, device, port, parent_conn, follower_conns, l
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
             # virtual ranks (tests: a whole group on ONE device) cannot share RCCL's device
             backend = "nccl" if device.startswith("cuda") and not spec.get("virtual") else "gloo"
+            if spec.get("virtual") and group > 1:
+                # the group's processes share the device's CUs: the wide kernel's K slices meet
+                # inside one launch and need each other resident (wide_gemm.hip split_cap)
+                os.environ.setdefault("P2P_WIDE_SPLIT_CAP", "1")
             kw = {"device_id": torch.device(device)} if backend == "nccl" else {}
             dist.init_process_group(backend, rank=rank, world_size=group,
                                     timeout=datetime.timedelta(seconds=spec.get("pg_timeout", 600)),

@@ -87,9 +87,9 @@ def test_group_native_loop_matches_python_lockstep(world):
     assert rep.get("k_graph_launches", 0) > 0, show  # and replayed as whole k-step graphs
     seq_p, _conc_p, mp = _serve(world, False, reqs)
     assert "mirror_frames" not in mp["per_replica"][0]
-    for a, b in zip(seq_n, seq_p):
+    for i, (a, b) in enumerate(zip(seq_n, seq_p)):
         assert a["eval_count"] == b["eval_count"]
-        assert a["response"] == b["response"], (a["response"], b["response"])
+        assert a["response"] == b["response"], (i, a["response"], b["response"])
     # concurrent (batched decode, riders in prompt chunks): every reply complete (the
     # batch shapes differ from the sequential run's, so bf16 rounding may flip near-ties)
     for a, b in zip(conc_n, seq_p):

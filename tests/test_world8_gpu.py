@@ -146,23 +146,21 @@ def _worker(rank, world, port, q, kind, mode, env):
         dist.destroy_process_group()
 
 
-# Fused all-reduce epilogue (default) at TP=4 and the unfused pair at TP=8.  The fused
-# GEMM's workgroups wait in place for the same workgroup of every peer: on 8 GPUs each
-# device runs only its own grid and in-order dispatch guarantees progress, but virtual
-# ranks on ONE device share its wave slots and LDS, so ranks whose grids are already
-# spinning can keep a late rank's earlier kernels from being scheduled at all (a deadlock
-# until the spin bound).  At 4 ranks with the split-K waves capped (P2P_FAR_MAX_WAVES) every
-# rank's grid fits; at 8 ranks it held only when the ranks happened to run in step (a warm
-# box) and timed out whenever one rank started late (round 4: 5 of 5 runs on fresh boxes),
-# so the 8-rank fused epilogue is covered bit-exactly by test_fused_ar_gpu.py (world 8, one
-# launch per rank in lockstep) and here the 8-rank engine runs the unfused pair.
-# The TP=4 case also keeps whole-group qkv producers (P2P_QA_KSPLIT=1): k-split doubles the
-# qkv+attention grid (76 KB of LDS per workgroup), and four ranks' grids beside their peers'
-# spinning fused all-reduce launches no longer fit the one device (a rank on its own GPU
-# never shares it); the TP=8 case runs the k-split default.
+# The unfused all-reduce pair at TP=8 and TP=4.  The fused GEMM's workgroups wait in place
+# for the same workgroup of every peer: on 8 GPUs each device runs only its own grid and
+# in-order dispatch guarantees progress, but virtual ranks on ONE device share its wave slots
+# and LDS, so ranks whose grids are already spinning can keep a late rank's earlier kernels
+# from being scheduled at all (a deadlock until the spin bound).  At 8 ranks that held only
+# when the ranks happened to run in step (round 4: 5 of 5 timeouts on fresh boxes); at 4
+# ranks, with the split-K waves capped and whole-group qkv producers, it held through round
+# 4 and stalled on 5 of 6 runs in round 5 (2-key-wave consumers and unsplit wide GEMMs did
+# not change that), with no kernel of the path changed.  So the fused epilogue is covered
+# bit-exactly by test_fused_ar_gpu.py (world 8, one launch per rank in lockstep) and inside
+# an engine by test_group_native_loop_gpu.py (TP 2 and 4, virtual ranks, replies equal to
+# the Python lockstep loop); here both engine widths run the unfused pair.
 @pytest.mark.parametrize("kind,mode,world,env", [
     ("dense", "tp", 8, {"P2P_TP_FUSED_AR": "0"}),
-    ("dense", "tp", 4, {"P2P_FAR_MAX_WAVES": "2", "P2P_QA_KSPLIT": "1"}),
+    ("dense", "tp", 4, {"P2P_TP_FUSED_AR": "0"}),
     ("moe", "allreduce", 8, {}), ("moe", "a2a", 8, {})])
 def test_world8_virtual_ranks_full_width(kind, mode, world, env):
     ctx = mp.get_context("spawn")
