@@ -22,6 +22,12 @@
 
 #include "gemm_epilogue.h"
 
+// The split-K fault word of the current device (tiled_gemm.hip): one int per device,
+// allocated with the first split-K workspace and never moved, so a captured graph, the
+// Python check (ops.gemm.tiled_split_fault) and the native loop (EngineLoop::set_aux_fault)
+// all see the same word.  nullptr while a capture is in progress and it does not exist yet.
+extern "C" int* p2p_split_fault_word_ptr(hipStream_t st);
+
 namespace pgemm {
 
 constexpr int BK = 64;
@@ -790,6 +796,7 @@ static bool split_ws(size_t bytes, hipStream_t st, char** out) {
     void* buf = nullptr;
     if (hipMalloc(&buf, want) != hipSuccess) return false;
     if (hipMemsetAsync(buf, 0, want, st) != hipSuccess) return false;
+    if (!p2p_split_fault_word_ptr(st)) return false;
     g_split_ws.buf = buf;  // the old buffer stays allocated (see above)
     g_split_ws.bytes = want;
   }
@@ -855,8 +862,9 @@ int launch_stages(const void* Wt, const void* X, int ldx, int M, int K, int m_ti
     // [0, n/2) arrival tickets, [n/2, n-1) generations, [n-1] the fault word.
     unsigned* ctr = (unsigned*)(ws + g_split_ws.bytes - kCounterBytes);
     constexpr size_t nw = kCounterBytes / sizeof(unsigned);
+    int* fw = p2p_split_fault_word_ptr(st);
     SplitArgs sp{splitk, (f32x4*)ws, (float*)(ws + slab), ctr, ctr + nw / 2,
-                 (int*)(ctr + nw - 1), par};
+                 fw ? fw : (int*)(ctr + nw - 1), par};
     hipLaunchKernelGGL((prefill_gemm_kernel<BM, BN, EPI, NORM, true, STAGES>),
                        dim3(tiles * splitk), dim3(NT), 0, st, (const bf16x8*)Wt,
                        (const bf16*)X, ldx, M, K, m_tiles, n_tiles, up_off, out, ldo, eps, ea, sp);
@@ -970,7 +978,10 @@ static int pick_tile(int M, int N) {
   // (one-m-tile 384 / 448-row tiles for 321-448 rows measured 1.1-1.3x SLOWER than the
   // 128x128 split-K / phased 256x256 picks below and were removed:
   // profiles/r3_prefill_tiles_384_448.jsonl)
-  if (N % 128 == 0 && ((M > 128 && M <= 192) || (M > 256 && M <= 320)))
+  // (257-320 rows: the one-m-tile 320x128 pays on the wide gate_up only; o_proj at 288 rows
+  // took 64 us with it and 39 with 128x128 split-K, cold weights:
+  // profiles/r5_prefill_gemm_cold_vs_hipblaslt.jsonl)
+  if (N % 128 == 0 && ((M > 128 && M <= 192) || (M > 256 && M <= 320 && N >= 16384)))
     return M <= 192 ? 7 : 6;
   const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};
   int best = 0;

@@ -214,15 +214,30 @@ P2P_API void p2p_prefill_deep(int mode) { pgemm::g_deep = (mode >= 0 && mode <= 
 // residency allows), 0 = serial (the last arriving slice reduces the whole tile).
 P2P_API void p2p_tiled_split_parallel(int on) { pgemm::g_split_parallel = on ? 1 : 0; }
 
-// Nonzero if a parallel split-K slice waited past its spin bound since the last call
-// (its tile's output is invalid); clears the word.  Synchronises the current device.
-extern "C" int p2p_wide_split_fault();  // wide_gemm.hip (its own split workspace)
+// The split-K fault word of each device (see prefill_gemm.h): allocated once, never moved.
+static int* g_fault_word[64];
 
+extern "C" int* p2p_split_fault_word_ptr(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!g_fault_word[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
+    int* p = nullptr;
+    if (hipMalloc(&p, 256) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, 256, st) != hipSuccess) return nullptr;
+    g_fault_word[dev] = p;
+  }
+  return g_fault_word[dev];
+}
+
+// Nonzero if a parallel split-K slice (tiled or wide kernel) waited past its spin bound since
+// the last call (its tile's output is invalid); clears the word.  Synchronises the device.
 P2P_API int p2p_tiled_split_fault() {
-  const int wv = p2p_wide_split_fault();
-  if (wv) return wv;
-  if (!pgemm::g_split_ws.buf) return 0;
-  int* w = (int*)((char*)pgemm::g_split_ws.buf + pgemm::g_split_ws.bytes - sizeof(unsigned));
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_fault_word[dev]) return 0;
+  int* w = g_fault_word[dev];
   int v = 0;
   if (hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   if (v) {

@@ -506,7 +506,8 @@ static bool gran_ws(int splitk, int n_tiles, hipStream_t st, GranArgs* ga) {
   ga->ticket = (u64*)base;
   ga->ssg = (u64*)(base + tk);
   ga->gran = (u64*)(base + tk + (size_t)g.tiles * splitk * 128 * 8);
-  ga->err = (int*)(ws + pgemm::g_split_ws.bytes - sizeof(unsigned));
+  int* fw = p2p_split_fault_word_ptr(st);
+  ga->err = fw ? fw : (int*)(ws + pgemm::g_split_ws.bytes - sizeof(unsigned));
   ga->align = kstep_align();
   return true;
 }
@@ -618,18 +619,10 @@ extern "C" int p2p_wide_dispatch(const void* Wt, const void* X, int ldx, int M, 
 }
 
 // Nonzero if a split slice of the wide kernel waited past its spin bound since the last call
-// (that tile's output is invalid); clears the word.  Synchronises the current device.
-extern "C" int p2p_wide_split_fault() {
-  if (!pgemm::g_split_ws.buf) return 0;
-  int* w = (int*)((char*)pgemm::g_split_ws.buf + pgemm::g_split_ws.bytes - sizeof(unsigned));
-  int v = 0;
-  if (hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (v) {
-    const int z = 0;
-    (void)hipMemcpy(w, &z, sizeof(int), hipMemcpyHostToDevice);
-  }
-  return v;
-}
+// (that tile's output is invalid); clears the word.  The wide and tiled kernels share the
+// device's split-K fault word (p2p_split_fault_word_ptr), so this is p2p_tiled_split_fault.
+extern "C" int p2p_tiled_split_fault();
+extern "C" int p2p_wide_split_fault() { return p2p_tiled_split_fault(); }
 
 // Benchmarks: cap on the K-slice count of the heuristic (1 = never split).
 // A/B: 1 = activations resident in LDS where a slice fits (default), 0 = the ring always.

@@ -24,7 +24,8 @@ enum Slot : int {
   kSampI = 9,
   kSampP = 10,
   kSampS = 11,
-  kSlots = 12,
+  kAux0 = 12,  // kAux0, kAux0 + 1: split-K fault word per decode buffer; kAux0 + 2 prefill
+  kSlots = 15,
 };
 
 }  // namespace
@@ -626,8 +627,11 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
     hip_check(h.memcpyAsync(f, g->first, nseq * 4, kD2H, stream_), "first tokens D2H");
     int32_t* ew = (int32_t*)pinned(kErr0 + 2, 4);
     if (g->err) hip_check(h.memcpyAsync(ew, g->err, 4, kD2H, stream_), "fault word D2H");
+    int32_t* ea = (int32_t*)pinned(kAux0 + 2, 4);
+    if (aux_err_) hip_check(h.memcpyAsync(ea, aux_err_, 4, kD2H, stream_), "split fault D2H");
     hip_check(h.streamSynchronize(stream_), "prefill sync");
     if (g->err && *ew != 0) on_fault(g->err, "prefill");
+    if (aux_err_ && *ea != 0) on_fault(aux_err_, "prefill (split-K)");
     for (int b = 0; b < nseq; ++b) first[b] = f[b];
   }
   const int64_t t1 = now_ns();
@@ -753,6 +757,8 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
             "hist D2H");
   if (g->err)
     hip_check(h.memcpyAsync(pinned(kErr0 + c.buf, 4), g->err, 4, kD2H, stream_), "fault D2H");
+  if (aux_err_)
+    hip_check(h.memcpyAsync(pinned(kAux0 + c.buf, 4), aux_err_, 4, kD2H, stream_), "split fault D2H");
   c.ev = events_[c.buf];
   hip_check(h.eventRecord(c.ev, stream_), "hipEventRecord");
   loaded_steps_ += k;
@@ -768,6 +774,10 @@ void EngineLoop::collect() {
   if (c.g->err && *(int32_t*)pinned_[kErr0 + c.buf].first != 0) {
     flight_.clear();  // chunks behind a faulted one ran on its invalid state
     on_fault(c.g->err, "decode");
+  }
+  if (aux_err_ && *(int32_t*)pinned_[kAux0 + c.buf].first != 0) {
+    flight_.clear();
+    on_fault(aux_err_, "decode (split-K)");
   }
   faults_in_row_ = 0;  // a clean decode chunk: whatever faulted before was transient
   const int32_t* hist = (const int32_t*)pinned_[kHist0 + c.buf].first;

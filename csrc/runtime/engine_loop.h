@@ -134,6 +134,9 @@ class EngineLoop {
   // resets, graph replays, eager prefills) is also sent to the followers' EngineMirror over
   // these channel fds (owned by the caller), one frame per step (runtime/mirror.h)
   void set_mirror(const std::vector<int>& fds);
+  // A second device fault word checked with every graph's own: the kernels' split-K word
+  // (p2p_split_fault_word_ptr), which the graphs' split-K GEMMs set when a slice gives up.
+  void set_aux_fault(uintptr_t word) { aux_err_ = reinterpret_cast<int32_t*>(word); }
   // a graph provider about to capture (kind, a, b, greedy): the followers capture it too
   void mirror_provide(const std::string& kind, int a, int b, bool greedy);
   void start();
@@ -220,6 +223,7 @@ class EngineLoop {
   int hist_buf_ = 0;
   static constexpr int kMaxFaultsInRow = 3;
   int faults_in_row_ = 0;  // consecutive steps that ended with a kernel fault word set
+  int32_t* aux_err_ = nullptr;  // set_aux_fault
 
   // metrics
   std::atomic<long> n_requests_{0}, n_tokens_{0}, n_prefill_calls_{0}, n_decode_calls_{0},

@@ -84,6 +84,12 @@ class NativeEngineServer(EngineServer):
             # TP / EP group leader (engine.cluster): the followers' EngineMirror threads
             # replay every device operation of this loop (runtime/mirror.h)
             self.loop.set_mirror([int(f) for f in mirror_fds])
+        if dev.type == "cuda":
+            # the kernels' split-K fault word: a split-K slice that gave up inside a graph
+            # fails the step like the graph's own fault word does
+            from ..ops.gemm import split_fault_word
+
+            self.loop.set_aux_fault(split_fault_word(dev))
         self.group = 1 + len(mirror_fds or ())
         self.loop.set_provider(self._provide)
         self.loop.set_eager_prefill(self._eager_prefill)

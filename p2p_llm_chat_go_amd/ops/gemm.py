@@ -236,6 +236,23 @@ def tiled_split_parallel(on: bool = True):
     _lib.lib().p2p_tiled_split_parallel(int(bool(on)))
 
 
+def split_fault_word(device=None) -> int:
+    """Device address of the kernels' split-K fault word on the current device (one int,
+    allocated on first use and never moved; the wide and tiled split-K GEMMs set it when a
+    slice gives up waiting).  The native loop checks it with every graph's own fault word."""
+    import ctypes
+
+    L = _lib.lib()
+    fn = L.p2p_split_fault_word_ptr
+    fn.argtypes = [ctypes.c_void_p]
+    fn.restype = ctypes.c_void_p
+    p = fn(_lib.stream_ptr(device))
+    if not p:
+        raise _lib.KernelError("split-K fault word: allocation failed")
+    torch.cuda.synchronize(device)  # its zeroing is done before any loop stream reads it
+    return int(p)
+
+
 def tiled_split_fault() -> int:
     """Nonzero if a parallel split-K slice gave up waiting for its tile (output invalid);
     clears the flag.  Synchronises the device."""

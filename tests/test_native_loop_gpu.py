@@ -89,6 +89,37 @@ def test_native_loop_matches_static_greedy():
         srv.close()
 
 
+def test_native_loop_split_fault_word_fails_the_step():
+    """A split-K slice that gave up sets the kernels' split-K fault word
+    (ops.gemm.split_fault_word), not the graph's own: the native loop checks it beside every
+    graph's word, fails the requests of that step with the reason, clears it, and serves the
+    next request normally (the Python path raises in check_faults the same way)."""
+    import ctypes
+
+    from p2p_llm_chat_go_amd.engine.native_loop import NativeEngineServer
+    from p2p_llm_chat_go_amd.ops.gemm import split_fault_word, tiled_split_fault
+
+    eng, w, cfg = _engine()
+    p = _prompts(2)[1]
+    ref = eng.generate([p], 12, stop_on_eos=False)[0].tokens
+    srv = NativeEngineServer(eng, max_batch=4, decode_chunk=4)
+    try:
+        word = split_fault_word(eng.device)
+        one = torch.ones(1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        hip = ctypes.CDLL("libamdhip64.so")
+        assert hip.hipMemcpy(ctypes.c_void_p(word), ctypes.c_void_p(one.data_ptr()),
+                             ctypes.c_size_t(4), 3) == 0  # device to device
+        with pytest.raises(RuntimeError, match="split-K"):
+            srv.generate(p, SamplingParams(max_tokens=12, stop_on_eos=False))
+        assert tiled_split_fault() == 0  # the loop cleared it
+        r = srv.generate(p, SamplingParams(max_tokens=12, stop_on_eos=False))
+        assert r["done"] and r["tokens"] == ref, r
+        assert srv.metrics()["errors"] >= 1
+    finally:
+        srv.close()
+
+
 def test_native_loop_full_batch_replays_k_step_graphs():
     """A full batch (running == max_batch) with decode_chunk=8: the loop's decode chunks are
     8 steps long, so it replays the whole 8-step graph (exec_k, engine_loop.cc) instead of
