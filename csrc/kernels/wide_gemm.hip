@@ -22,11 +22,11 @@
 //     first version was latency-bound at ~2.6 TB/s);
 //   * the grid is column blocks x K slices, with the slice count picked so the grid is
 //     <= one block per CU and close to the CU count (qkv at 8B: 48 x 5 = 240 blocks);
-//     the K slices of a tile meet through write-through slabs and a generation flip
-//     (the parallel split-K reduction of prefill_gemm.h), and slice s finishes the
-//     waves w with w % splitk == s, summing the slices in slice order (deterministic).
+//     the K slices of a tile meet through tagged 8-byte granules (GranArgs below): unit
+//     (column group w, m-tile i) is finished by slice (w * MT + i) % splitk, summing the
+//     slices in slice order (deterministic);
 // RMSNorm: the block squares the activation fragments it already holds in LDS (one
-// m-tile per wave pair); the row sums of the slices meet in the reduction.
+// m-tile per wave pair); the row sums of the slices meet as granules too.
 // Measured (docs/ARCHITECTURE.md "Wide mid-M family"): the autotuner's pick at 33-64 rows
 // for gate_up, down and qkv; the split-K seam (~5-6 us) is what it still pays on N <= 6144.
 #include <cstdlib>
@@ -38,7 +38,9 @@ namespace wide {
 
 #ifdef WIDE_STAMP
 // probe builds only (csrc/experimental/wide_stamp.hip): per-block wall-clock stamps
-// [entry, first chunk ready, main loop done, slabs drained, slices met, end, tile, split]
+// [entry, first chunk ready, main loop done, granules stored (split) / -, polls done (split,
+//  wave 0 only where it finishes a unit), end, tile, split]; the stores before a stamp
+//  wait for completion in this build only (the stamp's own global load)
 __device__ long long* wide_stamp_buf;
 #define WSTAMP(i, v) do { if (wide_stamp_buf && threadIdx.x == 0) wide_stamp_buf[(size_t)blockIdx.x * 8 + (i)] = (v); } while (0)
 #else
@@ -62,8 +64,9 @@ typedef unsigned long long u64;
 // and its regions; stale granules carry older tags).  (A ticket per WAVE measured 2x slower:
 // 64 agent-scope atomics per address serialise at the memory side, and the first chunk's
 // loads queue behind them.)  No wave waits for the other waves of its block after its
-// stream: each publishes its partials and its k-parity's row sums of squares at once.  Replaces the write-through slabs + arrival ticket + generation flip, whose
-// ~6 serial round trips cost 4-5 us per launch at 48 rows (r5 stamps).
+// stream: each publishes its partials and its k-parity's row sums of squares at once.
+// Replaces the write-through slabs + arrival ticket + generation flip, whose ~6 serial
+// round trips cost 4-5 us per launch at 48 rows (r5 stamps).
 struct GranArgs {
   int splitk;
   u64* gran;      // [tile][splitk][8 waves][4 m-tiles][4][64 lanes] partials
