@@ -1,4 +1,5 @@
-# world-8 virtual-rank tests with the wide split cap, the group native loop, then the rest.
+# End-of-session GPU validation: virtual-rank / group-loop / wide-kernel tests, the rest of the
+# GPU tier, smoke and the headline bench (logs: gpurun_out/r5g3_*).
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
