@@ -33,6 +33,11 @@ from .kv_cache import KVCache, pages_for
 
 BATCH_BUCKETS = (1, 2, 4, 8, 16, 32, 64)
 CTX_BUCKETS = (256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 131072)
+# decode graphs also come in a 128-key bucket: a suggest-reply (a chat message + 64 new
+# tokens) fits it, and its qkv+attention launch then runs 2-key-wave consumers (half the
+# LDS, csrc/kernels/qkv_attn.hip launch-code bits 16..23): bench.py 364.4-365.3 ->
+# 367.0-367.1 tok/s, alternating runs on one box (round 5)
+DECODE_CTX_BUCKETS = (128,) + CTX_BUCKETS
 
 
 def bucket(x, buckets):
@@ -138,7 +143,7 @@ class Engine:
         return ws
 
     def decode_graph(self, B: int, ctx: int, greedy: bool = True) -> DecodeGraph:
-        key = (bucket(B, BATCH_BUCKETS), bucket(ctx, CTX_BUCKETS), greedy)
+        key = (bucket(B, BATCH_BUCKETS), bucket(ctx, DECODE_CTX_BUCKETS), greedy)
         g = self._graphs.get(key)
         if g is None:
             st = DecodeState(self.model, key[0], key[1] // PAGE, key[1], key[1])

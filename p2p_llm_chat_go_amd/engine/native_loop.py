@@ -26,7 +26,7 @@ import os
 import time
 
 from ..native import load as load_native
-from .engine import BATCH_BUCKETS, CTX_BUCKETS, Engine
+from .engine import BATCH_BUCKETS, CTX_BUCKETS, DECODE_CTX_BUCKETS, Engine
 from .graph import PREFILL_ROW_BUCKETS
 from .sampling import SamplingParams
 from .server import EngineServer, EngineTimeout
@@ -75,7 +75,7 @@ class NativeEngineServer(EngineServer):
             # (profiles/r4_serve_native_vs_python.jsonl)
             "riders_all": os.environ.get("ENGINE_RIDERS", "all") == "all",
             "device": dev.index or 0, "batch_buckets": list(BATCH_BUCKETS),
-            "ctx_buckets": list(CTX_BUCKETS),
+            "ctx_buckets": list(DECODE_CTX_BUCKETS),  # the loop's decode graph buckets
             "row_buckets": [r for r in PREFILL_ROW_BUCKETS
                             if r <= min(engine.max_prefill_tokens, engine.prefill_graph_max_rows)],
             "prefill_max_pages": self.prefill_ctx // 64,

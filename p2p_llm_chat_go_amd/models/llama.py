@@ -222,12 +222,16 @@ class LlamaModel:
         qa_o = (qa and self.fuse_qkv_attn_oproj and self.tp == 1
                 and ops.qkv_attn_oproj_ok(self.w.layers[0].o, self.nq, self.nkv, rows=R,
                                           hidden=cfg.hidden))
+        # contexts bounded by 128 keys (the 128-key decode graphs): 2 key waves per consumer
+        qa_waves = None
+        if qa and max_ctx <= 128 and not (ops.attention.QKV_ATTN_WAVES >> 16) & 0xff:
+            qa_waves = ops.attention.QKV_ATTN_WAVES | (2 << 16)
         for i, lw in enumerate(self.w.layers):
             kc, vc = self.kv.layer(i)
             if qa:
                 ops.qkv_attn(lw.qkv, h, pos[:R], slots[:R], self.rope, self.nq, self.nkv, kc, vc,
                              block_tables, ctx_lens[:R], attn, ws.qa, ws.err, eps=cfg.eps,
-                             oproj=(lw.o, h) if qa_o else None)
+                             oproj=(lw.o, h) if qa_o else None, waves=qa_waves)
                 if not qa_o:
                     self._row_parallel(lw.o, attn, h, ws, R)
                 self._mlp(lw, ws, R)
