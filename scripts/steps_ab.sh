@@ -1,0 +1,9 @@
+# A/B: decode-graph steps per replay (P2P_DECODE_GRAPH_STEPS 8 default vs 16) on the headline bench
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/st8_$i.log 2>&1 || exit 1
+  P2P_DECODE_GRAPH_STEPS=16 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/st16_$i.log 2>&1 || exit 1
+done
+for f in gpurun_out/st*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"ttft_p50_ms": [0-9.]*' $f)"; done
