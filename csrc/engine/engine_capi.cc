@@ -18,6 +18,8 @@
 #include <string.h>
 #include <time.h>
 
+#include <cmath>
+
 #include <atomic>
 #include <chrono>
 #include <memory>
@@ -219,7 +221,9 @@ bool parse_params(const Json& req, int default_max, Params* p) {
       static thread_local std::mt19937_64 rng{std::random_device{}()};
       p->seed = (int64_t)(rng() >> 2);  // random.getrandbits(62)
     } else {
-      if (!as_double(sd, &v)) return false;
+      // int(seed) & (2**63 - 1) exactly: beyond 2**53 a JSON number has lost its low bits
+      // in the double, so those seeds (and non-numbers) take the Python path
+      if (!as_double(sd, &v) || !(std::fabs(v) < 9007199254740992.0)) return false;
       p->seed = (int64_t)v & INT64_MAX;
     }
   }
@@ -230,9 +234,11 @@ bool parse_params(const Json& req, int default_max, Params* p) {
 bool native_ids(const Front& f, const Json& req, std::vector<int>* ids) {
   if (!f.tok.ok) return false;
   if (req.get_string("endpoint") == "chat") return f.tok.messages_ids(req.get("messages"), ids);
+  // a missing prompt is ""; an explicit null (or any non-string) goes to Python, which
+  // raises on it as it always did
   const Json& pr = req.get("prompt");
-  if (!pr.is_null() && !pr.is_string()) return false;
-  const std::string prompt = pr.is_null() ? "" : pr.str();
+  if (req.has("prompt") && !pr.is_string()) return false;
+  const std::string prompt = pr.is_string() ? pr.str() : "";
   if (truthy(req.get("raw"))) {
     ids->push_back(f.tok.bos);
     return f.tok.encode(prompt, ids);
@@ -573,7 +579,11 @@ void p2p_engine_destroy(p2p_engine* e) {
 char* p2p_engine_tok_probe(const char* spec_json, const char* request_json, const char* ids_json) {
   try {
     Front f;
-    f.tok.load(spec_json);
+    try {
+      f.tok.load(spec_json);
+    } catch (const std::exception&) {  // a tokenizer.json the native side does not cover
+      f.tok = p2p::NativeTok();
+    }
     Json out = Json::object();
     std::vector<int> ids;
     const bool ok = native_ids(f, Json::parse(request_json), &ids);

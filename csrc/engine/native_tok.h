@@ -1,20 +1,25 @@
-// Native form of the engine's offline tokenizer (engine/tokenizer.py SyntheticTokenizer)
-// and of the Ollama prompt templates, so the engine C ABI turns a request into prompt ids
-// and generated ids into text without the interpreter.
+// Native form of the engine's tokenizers (engine/tokenizer.py: SyntheticTokenizer, and
+// HFTokenizer over a byte-level BPE tokenizer.json such as Llama-3's, bpe_tok.h) and of the
+// Ollama prompt templates, so the engine C ABI turns a request into prompt ids and
+// generated ids into text without the interpreter.
 //
 // Encoding splits text with the pattern  \s*\w+ | \s*[^\w\s] | \s+  and maps each piece to
 // lo + crc32(piece) % (hi - lo), exactly as the Python class does; the native side handles
 // printable ASCII (plus \t \n \r) and reports anything else as "not native", in which case
 // the caller asks Python (Unicode \w / \s classes are not re-implemented here).  Decoding
 // uses the built-in table exported by Python (`native_spec`) and recomputes the
-// pseudo-words of other ids.
+// pseudo-words of other ids.  A "bpe" spec (HFTokenizer.native_spec) names the
+// tokenizer.json; encoding and decoding then follow the HF library exactly (bpe_tok.h),
+// for any UTF-8 text.
 #pragma once
 #include <stdint.h>
 
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
+#include "engine/bpe_tok.h"
 #include "net/json.h"
 
 namespace p2p {
@@ -27,10 +32,23 @@ class NativeTok {
   std::vector<int> eos;
   std::map<std::string, int> special;
   std::map<int, std::string> pieces;
+  std::shared_ptr<BpeTok> bpe;  // "bpe" specs
 
-  // spec: SyntheticTokenizer.native_spec() as JSON; anything else leaves ok = false
+  // spec: SyntheticTokenizer / HFTokenizer .native_spec() as JSON; anything else (or a
+  // tokenizer.json with parts bpe_tok.h does not cover: it throws) leaves ok = false
   void load(const std::string& spec_json) {
     Json s = Json::parse(spec_json);
+    if (s.get_string("kind") == "bpe") {
+      auto b = std::make_shared<BpeTok>();
+      b->load_file(s.get_string("path"));
+      llama3 = s.get_bool("llama3", false);
+      bos = (int)s.get("bos").integer();
+      for (auto& e : s.get("eos").items()) eos.push_back((int)e.integer());
+      for (auto& kv : s.get("special").fields()) special[kv.first] = (int)kv.second.integer();
+      bpe = b;
+      ok = true;
+      return;
+    }
     if (s.get_string("kind") != "synthetic") return;
     llama3 = s.get_bool("llama3", false);
     lo = (int)s.get("lo").integer();
@@ -64,8 +82,9 @@ class NativeTok {
     return c ^ 0xFFFFFFFFu;
   }
 
-  // false if the text needs Python (non-ASCII)
+  // false if the text needs Python (synthetic: non-ASCII; bpe: not UTF-8)
   bool encode(const std::string& t, std::vector<int>* out) const {
+    if (bpe) return bpe->encode(t, out);
     if (!ascii_text(t)) return false;
     auto sp = [](unsigned char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; };
     auto wd = [](unsigned char c) { return isalnum(c) || c == '_'; };
@@ -113,15 +132,18 @@ class NativeTok {
   }
 
   // tokenizer._render_messages (Ollama /api/chat); false if a message is not plain strings
+  // (an explicit null role / content included: Python renders str(None) = "None"; only a
+  // missing key takes the default)
   bool messages_ids(const Json& msgs, std::vector<int>* ids) const {
     if (!msgs.is_null() && !msgs.is_array()) return false;
     std::vector<std::pair<std::string, std::string>> ms;
     for (auto& m : msgs.items()) {
       if (!m.is_object()) continue;
+      const bool hr = m.has("role"), hc = m.has("content");
       const Json& r = m.get("role");
       const Json& c = m.get("content");
-      if (!(r.is_null() || r.is_string()) || !(c.is_null() || c.is_string())) return false;
-      ms.emplace_back(r.is_null() ? "user" : r.str(), c.is_null() ? "" : c.str());
+      if ((hr && !r.is_string()) || (hc && !c.is_string())) return false;
+      ms.emplace_back(hr ? r.str() : "user", hc ? c.str() : "");
     }
     ids->push_back(bos);
     if (llama3) {
@@ -176,7 +198,19 @@ class NativeTok {
     return out;
   }
 
+  // HFTokenizer.decode: tokenizers' decode, then Python's str.strip()
+  static std::string py_strip(const std::string& s) {
+    std::vector<uint32_t> cps;
+    std::vector<size_t> offs;
+    if (!uni::utf8_decode(s, &cps, &offs)) return s;
+    size_t a = 0, b = cps.size();
+    while (a < b && uni::py_space(cps[a])) ++a;
+    while (b > a && uni::py_space(cps[b - 1])) --b;
+    return s.substr(offs[a], offs[b] - offs[a]);
+  }
+
   std::string decode(const std::vector<int>& ids) const {
+    if (bpe) return py_strip(bpe->decode(ids));
     std::string out;
     for (int i : ids) {
       bool skip = i == bos;

@@ -177,6 +177,7 @@ class HFTokenizer:
 
         if os.path.isdir(path):
             path = os.path.join(path, "tokenizer.json")
+        self.path = os.path.abspath(path)
         self.tok = Tokenizer.from_file(path)
         self.vocab = self.tok.get_vocab_size()
         self.llama3 = self.tok.token_to_id("<|begin_of_text|>") is not None
@@ -208,8 +209,14 @@ class HFTokenizer:
         return _render_messages(self, messages, self.tok.token_to_id)
 
     def native_spec(self) -> dict:
-        # a real BPE / SentencePiece model: the C ABI asks Python to encode and decode
-        return {"kind": "hf"}
+        """The engine C ABI reads the same tokenizer.json natively (csrc/engine/bpe_tok.h:
+        byte-level BPE with the Llama-3 or GPT-2 pre-tokenizer, as Llama-3's); a file with
+        parts it does not implement (a SentencePiece-style model such as Mixtral's, a
+        normalizer, ...) is refused there and every request asks Python to encode / decode."""
+        special = {k: self.tok.token_to_id(k) for k in LLAMA3_SPECIAL}
+        return {"kind": "bpe", "path": self.path, "llama3": bool(self.llama3),
+                "bos": int(self.bos_id), "eos": [int(e) for e in self.eos_ids],
+                "special": {k: int(v) for k, v in special.items() if v is not None}}
 
 
 def get_tokenizer(cfg=None, path: str | None = None):

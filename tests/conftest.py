@@ -1,3 +1,5 @@
+import ctypes
+import json
 import os
 import sys
 
@@ -22,3 +24,27 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+ENGINE_LIB = os.path.join(ROOT, "p2p_llm_chat_go_amd", "_lib", "libp2p_engine.so")
+
+
+@pytest.fixture(scope="module")
+def probe():
+    """The engine C ABI's tokenizer probe: (native spec, Ollama request, ids) -> its
+    {"native", "ids", "text"} (tests of csrc/engine/native_tok.h and bpe_tok.h)."""
+    if not os.path.exists(ENGINE_LIB):
+        pytest.skip("engine C ABI not built")
+    L = ctypes.CDLL(ENGINE_LIB)
+    L.p2p_engine_tok_probe.restype = ctypes.c_void_p
+    L.p2p_engine_tok_probe.argtypes = [ctypes.c_char_p] * 3
+    L.p2p_engine_free.argtypes = [ctypes.c_void_p]
+
+    def run(spec, req, ids=()):
+        p = L.p2p_engine_tok_probe(json.dumps(spec).encode(), json.dumps(req).encode(),
+                                   json.dumps(list(ids)).encode())
+        assert p, "probe failed"
+        out = json.loads(ctypes.string_at(p).decode())
+        L.p2p_engine_free(p)
+        return out
+    return run

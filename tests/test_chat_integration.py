@@ -462,12 +462,16 @@ def test_upnp_igd_port_mapping(procs):
         web.shutdown()
 
 
-@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
-def test_node_daemon_hosts_engine_in_process(procs, dev):
+@pytest.mark.parametrize("dev,tokfile", [("cpu", False), pytest.param("cuda:0", False, marks=pytest.mark.gpu),
+                                         pytest.param("cuda:0", True, marks=pytest.mark.gpu)],
+                         ids=["cpu", "gpu", "gpu-bpe"])
+def test_node_daemon_hosts_engine_in_process(procs, dev, tokfile, tmp_path):
     """ENGINE=inproc: the C++ node daemon loads the engine C ABI (libp2p_engine.so,
     csrc/engine/engine_capi.h) and serves /api/generate (plain and streaming NDJSON)
     and /suggest from the engine in its own process -- the node links the engine the
-    way the BASELINE north star's Go node links it through cgo (CPU tiny-llama here)."""
+    way the BASELINE north star's Go node links it through cgo (CPU tiny-llama here).
+    gpu-bpe: with TOKENIZER_PATH naming a Llama-3-style tokenizer.json the native BPE
+    tokenizer (csrc/engine/bpe_tok.h) serves it, still with no interpreter entry."""
     lib = os.path.join(os.path.dirname(BIN), "p2p_llm_chat_go_amd", "_lib", "libp2p_engine.so")
     if not os.path.exists(lib):
         pytest.skip("engine C ABI not built")
@@ -476,6 +480,10 @@ def test_node_daemon_hosts_engine_in_process(procs, dev):
     env = {"MYNAMEIS": "A", "HTTP_ADDR": "127.0.0.1:%d" % port, "DIRECTORY_URL": d,
            "KEY_TYPE": "ed25519", "LISTEN_ADDRS": "/ip4/127.0.0.1/tcp/0", "ENGINE": "inproc",
            "ENGINE_MODEL": "tiny-llama", "ENGINE_DEVICE": dev}
+    if tokfile:  # ids < tiny-llama's 512-token vocab: 500 BPE tokens + the 6 specials
+        from tokutil import train_bpe_tokenizer
+
+        env["TOKENIZER_PATH"] = train_bpe_tokenizer(tmp_path, vocab=500)
     procs.spawn("p2p-node", env)
     a = "http://127.0.0.1:%d" % port
     wait_http(a + "/me", timeout=120)
@@ -505,6 +513,17 @@ def test_node_daemon_hosts_engine_in_process(procs, dev):
         assert m.get("p2p_engine_capi_python_tokenize") == 0, m
         assert m.get("p2p_engine_capi_python_decode") == 0, m
         assert m.get("p2p_engine_capi_gil_entries") == 1, m
+        st, body, _ = http("POST", a + "/api/generate", {"model": "llama3.1", "stream": False,
+                                                          "prompt": "Grüße — 日本語? 😀",
+                                                          "options": {"num_predict": 4}})
+        assert st == 200 and json.loads(body)["eval_count"] == 4
+        m2 = {}
+        for line in http("GET", a + "/metrics")[1].splitlines():
+            k, _, v = line.partition(" ")
+            m2[k] = float(v) if v else 0.0
+        # non-ASCII text: native with a tokenizer.json, Python's with the synthetic tokenizer
+        assert (m2.get("p2p_engine_capi_python_tokenize") == 0) == tokfile, m2
+        assert m2.get("p2p_engine_capi_python_decode") == 0, m2
 
 
 def test_connection_manager_trims_to_low_watermark(procs):

@@ -4,9 +4,6 @@ tokenizer's (engine/tokenizer.py) -- the C ABI serves requests without the inter
 only if the two agree bit for bit.  Non-ASCII text must report "not native" (the request
 then takes Python's tokenisation).  The reference sends the same prompt to Ollama
 (`web/streamlit_app.py:91-95`); this is the in-process replacement's front end."""
-import ctypes
-import json
-import os
 import random
 
 import pytest
@@ -14,28 +11,6 @@ import pytest
 from p2p_llm_chat_go_amd.engine.tokenizer import SAMPLE_MESSAGES, get_tokenizer, suggest_prompt
 from p2p_llm_chat_go_amd.models import TINY_LLAMA
 from p2p_llm_chat_go_amd.models.config import LLAMA31_8B
-
-LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                   "p2p_llm_chat_go_amd", "_lib", "libp2p_engine.so")
-
-
-@pytest.fixture(scope="module")
-def probe():
-    if not os.path.exists(LIB):
-        pytest.skip("engine C ABI not built")
-    L = ctypes.CDLL(LIB)
-    L.p2p_engine_tok_probe.restype = ctypes.c_void_p
-    L.p2p_engine_tok_probe.argtypes = [ctypes.c_char_p] * 3
-    L.p2p_engine_free.argtypes = [ctypes.c_void_p]
-
-    def run(spec, req, ids=()):
-        p = L.p2p_engine_tok_probe(json.dumps(spec).encode(), json.dumps(req).encode(),
-                                   json.dumps(list(ids)).encode())
-        assert p, "probe failed"
-        out = json.loads(ctypes.string_at(p).decode())
-        L.p2p_engine_free(p)
-        return out
-    return run
 
 
 def _texts():
@@ -86,3 +61,4 @@ def test_non_ascii_and_odd_requests_fall_back_to_python(probe):
     assert not probe(spec, {"prompt": 42})["native"]
     assert not probe(spec, {"endpoint": "chat", "messages": [{"role": "user", "content": 3}]})["native"]
     assert not probe({"kind": "hf"}, {"prompt": "hello"})["native"]
+    assert not probe(spec, {"endpoint": "chat", "messages": [{"role": None, "content": "x"}]})["native"]
