@@ -54,6 +54,9 @@ constexpr int kSlots = 256;
 std::function<int()> g_slot[kSlots];
 std::atomic<int> g_next{0};
 std::atomic<int> g_bad{0};
+// fault injection on a follower rank (run_group_faults): the next follower decode replay
+// sets its graph's fault word; the next follower eager prefill raises
+std::atomic<int> g_follower_fault{0}, g_follower_eager_fail{0};
 
 template <int I>
 int tramp() { return g_slot[I](); }
@@ -76,12 +79,14 @@ void* exec_of(std::function<int()> f) {
 uint64_t mix(uint64_t h, uint64_t v) { return (h ^ v) * 0x100000001B3ull; }
 
 struct DecodeGraph {
-  std::vector<int32_t> meta, hist, step{0};
+  std::vector<int32_t> meta, hist, step{0}, errw{0};
   std::vector<int64_t> keys{0};
   DecodeGraphDesc d;
   uint64_t trace = 1469598103934665603ull;  // FNV over (step, meta) at every replay
   long launches = 0;
-  DecodeGraph(int B, int ctx) : meta((size_t)B * (4 + ctx / PAGE)), hist((size_t)B * ctx) {
+  DecodeGraph(int B, int ctx, bool follower = false)
+      : meta((size_t)B * (4 + ctx / PAGE)), hist((size_t)B * ctx) {
+    if (follower) d.err = errw.data();
     d.B = B;
     d.max_pages = ctx / PAGE;
     d.ctx = ctx;
@@ -92,9 +97,10 @@ struct DecodeGraph {
     d.step = step.data();
     d.keys = keys.data();
     d.keys_bytes = sizeof(int64_t);
-    auto one = [this] {
+    auto one = [this, follower] {
       const int B = d.B, S = d.max_steps, s = step[0];
       launches++;
+      if (follower && g_follower_fault.exchange(0)) errw[0] = 1;
       trace = mix(trace, (uint64_t)s);
       for (int32_t v : meta) trace = mix(trace, (uint64_t)(uint32_t)v);
       if (s >= S) {
@@ -419,6 +425,99 @@ int run_group() {
              : 1;
 }
 
+// Faults on a follower rank: a follower whose graph fault word is set, or whose
+// eager-prefill callback raises, answers that frame with its status bits; the leader must
+// fail exactly that step (the request gets the reason), clear every rank's words, and go
+// on serving -- the follower stays alive.
+int run_group_faults() {
+  LoopConfig c;
+  c.num_pages = 256;
+  c.max_batch = 4;
+  c.max_prefill_tokens = 256;
+  c.max_ctx = 2048;
+  c.eos = {EOS};
+  c.decode_chunk = 4;
+  c.row_buckets = {16, 32, 48, 64};
+  c.prefill_max_pages = PREFILL_PAGES;
+  c.prefill_graph_after = 1;
+  EngineLoop loop(c);
+  int sv[2];
+  if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return 1;
+  loop.set_mirror({sv[0]});
+  std::map<std::tuple<int, int>, std::unique_ptr<DecodeGraph>> ld, fd_;
+  std::map<std::tuple<int, int>, std::unique_ptr<PrefillGraph>> lp, fp;
+  loop.set_provider([&](const std::string& kind, int a, int b, bool greedy) {
+    loop.mirror_provide(kind, a, b, greedy);
+    if (kind == "decode") {
+      ld[{a, b}].reset(new DecodeGraph(a, b));
+      loop.add_decode_graph(ld[{a, b}]->d);
+    } else {
+      lp[{a, b}].reset(new PrefillGraph(a, b));
+      loop.add_prefill_graph(lp[{a, b}]->d);
+    }
+  });
+  auto eager = [](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>&,
+                  const std::vector<int>&, const std::vector<LoopSampling>&) {
+    std::vector<int> f;
+    for (const auto& p : prompts) f.push_back(nxt(p.back(), (int)p.size() - 1));
+    return f;
+  };
+  loop.set_eager_prefill(eager);
+  EngineMirror m(sv[1], 0);
+  m.set_provider([&](const std::string& kind, int a, int b, bool) {
+    if (kind == "decode") {
+      fd_[{a, b}].reset(new DecodeGraph(a, b, true));
+      m.add_decode_graph(fd_[{a, b}]->d);
+    } else {
+      fp[{a, b}].reset(new PrefillGraph(a, b));
+      m.add_prefill_graph(fp[{a, b}]->d);
+    }
+  });
+  m.set_eager_prefill([&](const std::vector<std::vector<int>>& p, const std::vector<std::vector<int>>& pg,
+                          const std::vector<int>& st, const std::vector<LoopSampling>& sm) {
+    if (g_follower_eager_fail.exchange(0)) throw std::runtime_error("injected eager failure");
+    return eager(p, pg, st, sm);
+  });
+  std::string fres = "?";
+  std::thread fth([&] { fres = m.run(); });
+  loop.start();
+  int failures = 0;
+  auto ask = [&](int L, std::string* err) {
+    std::vector<int> prompt(L);
+    for (int i = 0; i < L; ++i) prompt[i] = (i * 13 + 5) % (V - 1);
+    const int64_t id = loop.submit(prompt, 12, false, LoopSampling());
+    LoopResult r;
+    loop.wait(id, 30.0, &r);
+    loop.release(id);
+    *err = r.error;
+    return r.error.empty() && r.tokens == expected(prompt, 12, false);
+  };
+  std::string e;
+  if (!ask(20, &e)) failures++, std::fprintf(stderr, "faults: clean request failed: %s\n", e.c_str());
+  g_follower_fault = 1;
+  if (ask(20, &e) || e.find("follower") == std::string::npos)
+    failures++, std::fprintf(stderr, "faults: follower fault not reported (err '%s')\n", e.c_str());
+  if (!ask(20, &e)) failures++, std::fprintf(stderr, "faults: request after the fault failed: %s\n", e.c_str());
+  g_follower_eager_fail = 1;
+  if (ask(300, &e) || e.find("failed on a follower") == std::string::npos)
+    failures++, std::fprintf(stderr, "faults: follower eager failure not reported (err '%s')\n", e.c_str());
+  if (!ask(300, &e)) failures++, std::fprintf(stderr, "faults: eager request after the failure failed: %s\n", e.c_str());
+  for (auto& kv : fd_)
+    if (kv.second->errw[0] != 0) failures++, std::fprintf(stderr, "faults: follower word not cleared\n");
+  auto lm = loop.metrics();
+  auto mm = m.metrics();
+  loop.shutdown();
+  fth.join();
+  m.shutdown();
+  close(sv[0]);
+  close(sv[1]);
+  if (!fres.empty()) failures++, std::fprintf(stderr, "faults: follower ended with '%s'\n", fres.c_str());
+  std::printf("group faults: failures=%d follower_faults=%ld fault_reports=%ld host_failures=%ld dead='%s'\n",
+              failures, (long)lm["mirror_follower_faults"], (long)mm["mirror_fault_reports"],
+              (long)mm["mirror_host_failures"], loop.dead().c_str());
+  return failures == 0 && lm["mirror_follower_faults"] >= 2 && mm["mirror_host_failures"] == 1 ? 0 : 1;
+}
+
 }  // namespace
 
 int main() {
@@ -428,6 +527,7 @@ int main() {
   rc |= run(false, true);
   rc |= run(true, true);
   rc |= run_group();
+  rc |= run_group_faults();
   if (rc == 0) std::printf("LOOP_SELFTEST_OK\n");
   return rc;
 }

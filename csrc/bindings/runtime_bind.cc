@@ -154,7 +154,11 @@ EngineLoop::GraphProvider py_provider(py::function f) {
   auto fn = std::make_shared<py::function>(std::move(f));
   return [fn](const std::string& kind, int a, int b, bool greedy) {
     py::gil_scoped_acquire gil;
-    (*fn)(kind, a, b, greedy);
+    try {
+      (*fn)(kind, a, b, greedy);
+    } catch (py::error_already_set& e) {  // formatted here, with the GIL held
+      throw std::runtime_error(std::string("graph provider raised: ") + e.what());
+    }
   };
 }
 
@@ -163,9 +167,13 @@ EngineLoop::EagerPrefill py_eager(py::function f) {
   return [fn](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>& pages,
               const std::vector<int>& starts, const std::vector<LoopSampling>& samp) {
     py::gil_scoped_acquire gil;
-    py::list sp;
-    for (auto& s : samp) sp.append(py::make_tuple(s.temperature, s.top_k, s.top_p, s.seed));
-    return py::cast<std::vector<int>>((*fn)(prompts, pages, starts, sp));
+    try {
+      py::list sp;
+      for (auto& s : samp) sp.append(py::make_tuple(s.temperature, s.top_k, s.top_p, s.seed));
+      return py::cast<std::vector<int>>((*fn)(prompts, pages, starts, sp));
+    } catch (py::error_already_set& e) {
+      throw std::runtime_error(std::string("eager prefill raised: ") + e.what());
+    }
   };
 }
 
@@ -248,6 +256,7 @@ void bind_engine_loop(py::module_& m) {
       .def("add_prefill_graph", [](EngineMirror& M, py::dict d) { M.add_prefill_graph(prefill_desc(d)); })
       .def("set_provider", [](EngineMirror& M, py::function f) { M.set_provider(py_provider(f)); })
       .def("set_eager_prefill", [](EngineMirror& M, py::function f) { M.set_eager_prefill(py_eager(f)); })
+      .def("set_aux_fault", &EngineMirror::set_aux_fault, py::arg("word"))
       .def("run", &EngineMirror::run, py::call_guard<py::gil_scoped_release>())
       .def("metrics", &EngineMirror::metrics)
       .def("shutdown", &EngineMirror::shutdown, py::call_guard<py::gil_scoped_release>());

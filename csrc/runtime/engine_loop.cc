@@ -302,6 +302,7 @@ std::map<std::string, double> EngineLoop::metrics() {
   if (mirror_) {
     m["mirror_frames"] = mirror_->frames();
     m["mirror_bytes"] = mirror_->bytes();
+    m["mirror_follower_faults"] = mirror_->follower_faults();
   }
   return m;
 }
@@ -530,13 +531,15 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
     }
     riders.clear();
     const int64_t te = now_ns();
+    uint32_t mseq = 0;
     if (mirror_) {  // the followers run the same eager prefill (its collectives pair up)
       mirror_->eager(prompts, pages, starts, samp);
-      mirror_->flush();
+      mseq = mirror_->flush();
     }
     first = eager_(prompts, pages, starts, samp);
     eager_ns_ += now_ns() - te;
     n_eager_prefill_++;
+    follower_check(mseq, "eager prefill");
   } else {
     // chunk metadata (PrefillGraph.host_meta, engine/graph.py)
     int32_t* m = (int32_t*)pinned(kPrefillMeta, g->meta_len * 4);
@@ -610,6 +613,7 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
       hip_check(h.memcpyAsync(g->topp, tp, S * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->seeds, sd, S * 8, kH2D, stream_), "samp H2D");
     }
+    uint32_t pf_seq = 0;
     if (mirror_) {
       const char K = 'P';
       mirror_->h2d(K, g->rows, g->n_seq, g->greedy, kFMeta, m, g->meta_len * 4);
@@ -620,7 +624,7 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
         mirror_->h2d(K, g->rows, g->n_seq, g->greedy, kFSeeds, pinned_[kSampS].first, S * 8);
       }
       mirror_->launch(K, g->rows, g->n_seq, g->greedy, 0, 1);
-      mirror_->flush();
+      pf_seq = mirror_->flush();
     }
     hip_check(h.graphLaunch(g->exec, stream_), "prefill graph launch");
     int32_t* f = (int32_t*)pinned(kFirst, S * 4);
@@ -632,6 +636,7 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
     hip_check(h.streamSynchronize(stream_), "prefill sync");
     if (g->err && *ew != 0) on_fault(g->err, "prefill");
     if (aux_err_ && *ea != 0) on_fault(aux_err_, "prefill (split-K)");
+    follower_check(pf_seq, "prefill");
     for (int b = 0; b < nseq; ++b) first[b] = f[b];
   }
   const int64_t t1 = now_ns();
@@ -732,10 +737,11 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
   // the next launch of the prompt-chunk graph pays: ~8 us per launch, bench/graph_switch_probe.py)
   const int nk = (g->exec_k && g->k_steps > 1) ? k / g->k_steps : 0;
   const int n1 = k - nk * g->k_steps;
+  uint32_t mseq = 0;
   if (mirror_) {  // the followers replay the same graphs (their collectives pair with ours)
     if (nk) mirror_->launch('D', g->B, g->ctx, g->greedy, 1, (uint32_t)nk);
     if (n1) mirror_->launch('D', g->B, g->ctx, g->greedy, 0, (uint32_t)n1);
-    mirror_->flush();
+    mseq = mirror_->flush();
   }
   for (int i = 0; i < nk; ++i) {
     hip_check(h.graphLaunch(g->exec_k, stream_), "decode graph launch");
@@ -748,6 +754,7 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
   c.s0 = loaded_steps_;
   c.k = k;
   c.buf = hist_buf_;
+  c.mseq = mseq;
   hist_buf_ ^= 1;
   // this chunk's k columns of every row: [B, k] packed
   const size_t hb = (size_t)g->B * k * 4;
@@ -779,6 +786,10 @@ void EngineLoop::collect() {
     flight_.clear();
     on_fault(aux_err_, "decode (split-K)");
   }
+  if (mirror_ && c.mseq && mirror_->await(c.mseq)) {
+    flight_.clear();
+    on_fault(nullptr, "decode (on a follower rank)");
+  }
   faults_in_row_ = 0;  // a clean decode chunk: whatever faulted before was transient
   const int32_t* hist = (const int32_t*)pinned_[kHist0 + c.buf].first;
   std::vector<std::vector<int>> toks(c.ids.size());
@@ -800,15 +811,30 @@ void EngineLoop::collect() {
 // check_faults -- so one transient timeout fails only the requests in this step;
 // kMaxFaultsInRow faulted steps in a row mark the replica dead, and the router stops
 // sending it traffic.
+// Group followers report their own fault words per frame (mirror.h status back channel):
+// a fault on any rank fails the step here like a local one.
+void EngineLoop::follower_check(uint32_t seq, const char* where) {
+  if (!mirror_ || !seq) return;
+  const uint32_t bits = mirror_->await(seq);
+  if (bits) on_fault(nullptr, (std::string(where) + (bits & 2 ? " (failed on a follower rank)"
+                                                               : " (on a follower rank)")).c_str());
+}
+
 void EngineLoop::on_fault(int32_t* err, const char* where) {
   const HipApi& h = hip_api();
-  (void)h.memsetAsync(err, 0, 4, stream_);
+  if (err) (void)h.memsetAsync(err, 0, 4, stream_);
   (void)h.streamSynchronize(stream_);
-  if (mirror_) {  // a group's fault words are set together (a peer's spin gave up too)
+  if (mirror_) {
+    // every rank's words back to 0 ('F'), and the followers' reports of the frames before it
+    // (chunks in flight behind the faulted one: still faulted) consumed here, so the next
+    // step starts clean
     try {
       mirror_->faults();
-      mirror_->flush();
-    } catch (...) {
+      const uint32_t fs = mirror_->flush();
+      if (fs) (void)mirror_->await(fs);
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> lk(mu_);
+      dead_ = std::string("group follower lost after a fault: ") + e.what();
     }
   }
   loaded_ = nullptr;

@@ -171,6 +171,7 @@ class EngineLoop {
     int s0 = 0, k = 0;  // hist columns [s0, s0 + k)
     int buf = 0;        // pinned hist buffer index
     void* ev = nullptr;
+    uint32_t mseq = 0;  // the group frame that launched it (follower status, mirror.h)
   };
 
   void run();
@@ -182,6 +183,7 @@ class EngineLoop {
   void drain();    // read every chunk in flight
   void fail_all(const std::string& why);
   [[noreturn]] void on_fault(int32_t* err, const char* where);
+  void follower_check(uint32_t seq, const char* where);
   const DecodeGraphDesc* decode_graph(int B, int ctx, bool greedy);
   const PrefillGraphDesc* find_prefill_graph(int rows, int nseq, bool greedy);
   const PrefillGraphDesc* prefill_graph(int rows, int nseq, bool greedy);

@@ -2,9 +2,14 @@
 #include "runtime/mirror.h"
 
 #include <errno.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -141,9 +146,9 @@ void MirrorSender::stop() {
   flush();
 }
 
-void MirrorSender::flush() {
+uint32_t MirrorSender::flush() {
   std::lock_guard<std::recursive_mutex> lk(mu_);
-  if (buf_.empty()) return;
+  if (buf_.empty()) return 0;
   const uint32_t n = (uint32_t)buf_.size();
   std::string frame(reinterpret_cast<const char*>(&n), 4);
   frame += buf_;
@@ -151,14 +156,65 @@ void MirrorSender::flush() {
   for (int fd : fds_) write_all(fd, frame.data(), frame.size());
   frames_++;
   bytes_ += (long)frame.size();
+  return (uint32_t)frames_.load();
+}
+
+uint32_t MirrorSender::await(uint32_t seq, double timeout_s) {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  if (acked_.size() != fds_.size()) acked_.assign(fds_.size(), 0);
+  uint32_t bits = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t f = 0; f < fds_.size(); ++f) {
+    while (acked_[f] < seq) {
+      const double left =
+          timeout_s - std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      pollfd pf{fds_[f], POLLIN, 0};
+      const int r = left > 0 ? poll(&pf, 1, (int)(left * 1000) + 1) : 0;
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0)
+        throw std::runtime_error("group follower " + std::to_string(f + 1) +
+                                 " did not report frame " + std::to_string(seq));
+      uint32_t rep[2];
+      if (!read_exact(fds_[f], (char*)rep, sizeof rep))
+        throw std::runtime_error("group follower " + std::to_string(f + 1) + " is gone");
+      acked_[f] = rep[0];
+      bits |= rep[1];
+    }
+  }
+  if (bits) follower_faults_++;
+  return bits;
 }
 
 // ------------------------------------------------------------------ follower
-EngineMirror::~EngineMirror() {}
+EngineMirror::EngineMirror(int fd, int device) : fd_(fd), device_(device) {
+  const char* e = std::getenv("P2P_MIRROR_INJECT_FAULT");
+  inject_at_ = e ? std::atol(e) : 0;
+}
+
+EngineMirror::~EngineMirror() {
+  {
+    std::lock_guard<std::mutex> lk(rmu_);
+    rstop_ = true;
+  }
+  rcv_.notify_all();
+  if (rth_.joinable()) rth_.join();
+}
 
 void EngineMirror::shutdown() {
+  {
+    std::lock_guard<std::mutex> lk(rmu_);
+    rstop_ = true;
+  }
+  rcv_.notify_all();
+  if (rth_.joinable()) rth_.join();
   const HipApi& h = hip_api();
   if (!h.ok) return;
+  for (int i = 0; i < kRep; ++i) {
+    if (rep_ev_[i]) h.eventDestroy(rep_ev_[i]);
+    rep_ev_[i] = nullptr;
+  }
+  if (rep_words_) h.hostFree(rep_words_);
+  rep_words_ = nullptr;
   for (int i = 0; i < 2; ++i) {
     if (stage_[i]) h.hostFree(stage_[i]);
     if (stage_ev_[i]) h.eventDestroy(stage_ev_[i]);
@@ -236,91 +292,167 @@ std::map<std::string, double> EngineMirror::metrics() {
   m["mirror_launches"] = n_launches_;
   m["mirror_provides"] = n_provides_;
   m["mirror_eager"] = n_eager_;
+  m["mirror_fault_reports"] = n_faults_;
+  m["mirror_host_failures"] = n_host_fail_;
   std::lock_guard<std::mutex> lk(gmu_);
   m["mirror_graphs"] = (double)graphs_.size();
   return m;
 }
 
-void EngineMirror::apply(const std::string& frame) {
+uint32_t EngineMirror::apply(const std::string& frame, std::vector<int32_t*>* launched) {
   const HipApi& h = hip_api();
   // h2d payloads of this frame go through one pinned staging buffer (copied up front)
   char* st = (char*)staging(frame.size());
   memcpy(st, frame.data(), frame.size());
   Reader r{frame};
   bool used_stage = false;
-  while (r.i < frame.size()) {
-    const char op = r.get<char>();
-    if (op == 'S') {
-      throw std::string("");  // stop: handled by run()
-    }
-    if (op == 'F') {
-      std::lock_guard<std::mutex> lk(gmu_);
-      for (auto& kv : graphs_)
-        if (kv.second.err) hip_check(h.memsetAsync(kv.second.err, 0, 4, stream_), "mirror fault reset");
-      continue;
-    }
-    if (op == 'E') {
-      const uint32_t n = r.get<uint32_t>();
-      std::vector<std::vector<int>> prompts, pages;
-      std::vector<int> starts;
-      std::vector<LoopSampling> samp;
-      for (uint32_t i = 0; i < n; ++i) {
-        prompts.push_back(r.ints());
-        pages.push_back(r.ints());
-        starts.push_back(r.get<int32_t>());
-        LoopSampling s;
-        s.temperature = r.get<float>();
-        s.top_k = r.get<int32_t>();
-        s.top_p = r.get<float>();
-        s.seed = r.get<int64_t>();
-        samp.push_back(s);
+  uint32_t host_bits = 0;
+  try {
+    while (r.i < frame.size()) {
+      const char op = r.get<char>();
+      if (op == 'S') {
+        throw std::string("");  // stop: handled by run()
       }
-      if (!eager_) throw std::runtime_error("mirror: no eager prefill callback");
-      hip_check(h.streamSynchronize(stream_), "mirror sync");  // the model code runs on its stream
-      eager_(prompts, pages, starts, samp);
-      n_eager_++;
-      continue;
+      if (op == 'F') {  // the leader failed a step: every fault word of this rank back to 0
+        std::lock_guard<std::mutex> lk(gmu_);
+        for (auto& kv : graphs_)
+          if (kv.second.err) hip_check(h.memsetAsync(kv.second.err, 0, 4, stream_), "mirror fault reset");
+        if (aux_err_) hip_check(h.memsetAsync(aux_err_, 0, 4, stream_), "mirror split fault reset");
+        continue;
+      }
+      if (op == 'E') {
+        const uint32_t n = r.get<uint32_t>();
+        std::vector<std::vector<int>> prompts, pages;
+        std::vector<int> starts;
+        std::vector<LoopSampling> samp;
+        for (uint32_t i = 0; i < n; ++i) {
+          prompts.push_back(r.ints());
+          pages.push_back(r.ints());
+          starts.push_back(r.get<int32_t>());
+          LoopSampling s;
+          s.temperature = r.get<float>();
+          s.top_k = r.get<int32_t>();
+          s.top_p = r.get<float>();
+          s.seed = r.get<int64_t>();
+          samp.push_back(s);
+        }
+        if (!eager_) throw std::runtime_error("mirror: no eager prefill callback");
+        hip_check(h.streamSynchronize(stream_), "mirror sync");  // the model code runs on its stream
+        eager_(prompts, pages, starts, samp);
+        n_eager_++;
+        continue;
+      }
+      const char kind = r.get<char>();
+      const int a = r.get<int32_t>(), b = r.get<int32_t>();
+      const bool greedy = r.get<uint8_t>() != 0;
+      if (op == 'V') {
+        if (!provider_) throw std::runtime_error("mirror: no graph provider");
+        hip_check(h.streamSynchronize(stream_), "mirror sync");
+        provider_(kind == 'D' ? "decode" : "prefill", a, b, greedy);
+        n_provides_++;
+        (void)find(kind, a, b, greedy);  // the provider must have registered it
+        continue;
+      }
+      Graph* g = find(kind, a, b, greedy);
+      if (op == 'H') {
+        const uint8_t f = r.get<uint8_t>();
+        const uint32_t n = r.get<uint32_t>();
+        const size_t off = r.i;
+        (void)r.bytes(n);
+        if (f > kFSeeds || !g->fields[f]) throw std::runtime_error("mirror: bad h2d field");
+        hip_check(h.memcpyAsync(g->fields[f], st + off, n, kH2D, stream_), "mirror h2d");
+        used_stage = true;
+      } else if (op == 'M') {
+        const uint8_t f = r.get<uint8_t>();
+        const uint32_t n = r.get<uint32_t>();
+        if (f > kFSeeds || !g->fields[f]) throw std::runtime_error("mirror: bad memset field");
+        hip_check(h.memsetAsync(g->fields[f], 0, n, stream_), "mirror memset");
+      } else if (op == 'L') {
+        const uint8_t which = r.get<uint8_t>();
+        const uint32_t count = r.get<uint32_t>();
+        void* ex = which ? g->exec_k : g->exec;
+        if (!ex) throw std::runtime_error("mirror: graph has no such exec");
+        for (uint32_t i = 0; i < count; ++i) hip_check(h.graphLaunch(ex, stream_), "mirror launch");
+        n_launches_ += count;
+        if (g->err && std::find(launched->begin(), launched->end(), g->err) == launched->end())
+          launched->push_back(g->err);
+      } else {
+        throw std::runtime_error(std::string("mirror: unknown op ") + op);
+      }
     }
-    const char kind = r.get<char>();
-    const int a = r.get<int32_t>(), b = r.get<int32_t>();
-    const bool greedy = r.get<uint8_t>() != 0;
-    if (op == 'V') {
-      if (!provider_) throw std::runtime_error("mirror: no graph provider");
-      hip_check(h.streamSynchronize(stream_), "mirror sync");
-      provider_(kind == 'D' ? "decode" : "prefill", a, b, greedy);
-      n_provides_++;
-      (void)find(kind, a, b, greedy);  // the provider must have registered it
-      continue;
-    }
-    Graph* g = find(kind, a, b, greedy);
-    if (op == 'H') {
-      const uint8_t f = r.get<uint8_t>();
-      const uint32_t n = r.get<uint32_t>();
-      const size_t off = r.i;
-      (void)r.bytes(n);
-      if (f > kFSeeds || !g->fields[f]) throw std::runtime_error("mirror: bad h2d field");
-      hip_check(h.memcpyAsync(g->fields[f], st + off, n, kH2D, stream_), "mirror h2d");
-      used_stage = true;
-    } else if (op == 'M') {
-      const uint8_t f = r.get<uint8_t>();
-      const uint32_t n = r.get<uint32_t>();
-      if (f > kFSeeds || !g->fields[f]) throw std::runtime_error("mirror: bad memset field");
-      hip_check(h.memsetAsync(g->fields[f], 0, n, stream_), "mirror memset");
-    } else if (op == 'L') {
-      const uint8_t which = r.get<uint8_t>();
-      const uint32_t count = r.get<uint32_t>();
-      void* ex = which ? g->exec_k : g->exec;
-      if (!ex) throw std::runtime_error("mirror: graph has no such exec");
-      for (uint32_t i = 0; i < count; ++i) hip_check(h.graphLaunch(ex, stream_), "mirror launch");
-      n_launches_ += count;
-    } else {
-      throw std::runtime_error(std::string("mirror: unknown op ") + op);
-    }
+  } catch (const std::exception& e) {
+    // a callback that raised, an unknown graph, a bad record: this frame fails (reported to
+    // the leader, which fails its step); the mirror keeps serving the next frames.  (A
+    // broken stream or HIP error shows up again on the next frame's own calls.)
+    host_bits = 2;
+    n_host_fail_++;
+    fprintf(stderr, "[mirror] frame failed on this rank: %s\n", e.what());
   }
   if (used_stage) {
     if (!stage_ev_[cur_]) hip_check(h.eventCreateWithFlags(&stage_ev_[cur_], 2), "mirror event");
     hip_check(h.eventRecord(stage_ev_[cur_], stream_), "mirror event");
     cur_ ^= 1;
+  }
+  return host_bits;
+}
+
+// Queue the frame's status: its launched graphs' fault words and the split-K word are
+// copied to a pinned slot behind the frame's work; reporter() answers once that landed.
+void EngineMirror::report(uint32_t seq, const std::vector<int32_t*>& launched, uint32_t host_bits) {
+  const HipApi& h = hip_api();
+  std::unique_lock<std::mutex> lk(rmu_);
+  const int slot = rep_next_;
+  rcv_.wait(lk, [&] { return !rep_busy_[slot] || rstop_; });
+  if (rstop_) return;
+  rep_next_ = (rep_next_ + 1) % kRep;
+  rep_busy_[slot] = true;
+  lk.unlock();
+  if (!rep_words_) {
+    hip_check(h.hostMalloc((void**)&rep_words_, (size_t)kRep * kRepWords * 4, 0), "mirror status");
+    memset(rep_words_, 0, (size_t)kRep * kRepWords * 4);
+  }
+  if (!rep_ev_[slot]) hip_check(h.eventCreateWithFlags(&rep_ev_[slot], 2), "mirror status event");
+  int32_t* w = rep_words_ + (size_t)slot * kRepWords;
+  int nw = 0;
+  for (int32_t* e : launched) {
+    if (nw >= kRepWords - 1) break;
+    hip_check(h.memcpyAsync(w + nw++, e, 4, kD2H, stream_), "mirror status D2H");
+  }
+  if (aux_err_) hip_check(h.memcpyAsync(w + nw++, aux_err_, 4, kD2H, stream_), "mirror status D2H");
+  hip_check(h.eventRecord(rep_ev_[slot], stream_), "mirror status event");
+  lk.lock();
+  rq_.push_back(Report{seq, host_bits, slot, nw});
+  lk.unlock();
+  rcv_.notify_all();
+}
+
+void EngineMirror::reporter() {
+  const HipApi& h = hip_api();
+  (void)h.setDevice(device_);
+  while (true) {
+    Report rp;
+    {
+      std::unique_lock<std::mutex> lk(rmu_);
+      rcv_.wait(lk, [&] { return rstop_ || !rq_.empty(); });
+      if (rq_.empty()) return;  // stopping, nothing left to answer
+      rp = rq_.front();
+      rq_.pop_front();
+    }
+    uint32_t bits = rp.host_bits;
+    if (h.eventSynchronize(rep_ev_[rp.slot]) != 0) bits |= 2;
+    for (int i = 0; i < rp.nwords; ++i)
+      if (rep_words_[(size_t)rp.slot * kRepWords + i] != 0) bits |= 1;
+    if (bits & 1) n_faults_++;
+    {
+      std::lock_guard<std::mutex> lk(rmu_);
+      rep_busy_[rp.slot] = false;
+    }
+    rcv_.notify_all();
+    const uint32_t msg[2] = {rp.seq, bits};
+    try {
+      write_all(fd_, (const char*)msg, sizeof msg);
+    } catch (const std::exception&) {  // the leader is gone: nothing to tell
+    }
   }
 }
 
@@ -330,19 +462,32 @@ std::string EngineMirror::run() {
     if (!h.ok) throw std::runtime_error("mirror: " + h.error);
     hip_check(h.setDevice(device_), "hipSetDevice");
     if (!stream_) hip_check(h.streamCreateWithFlags(&stream_, 1), "hipStreamCreate");
+    {
+      std::lock_guard<std::mutex> lk(rmu_);
+      rstop_ = false;
+    }
+    if (!rth_.joinable()) rth_ = std::thread([this] { reporter(); });
     std::string frame;
+    uint32_t seq = 0;
+    std::vector<int32_t*> launched;
     while (true) {
       uint32_t n = 0;
       if (!read_exact(fd_, (char*)&n, 4)) throw std::runtime_error("group channel closed (leader gone)");
       frame.resize(n);
       if (n && !read_exact(fd_, &frame[0], n)) throw std::runtime_error("group channel closed");
       n_frames_++;
+      ++seq;
+      launched.clear();
+      uint32_t host_bits;
       try {
-        apply(frame);
+        host_bits = apply(frame, &launched);
       } catch (const std::string&) {  // stop
         hip_check(h.streamSynchronize(stream_), "mirror drain");
         return "";
       }
+      if (!launched.empty() && ++launch_frames_ == inject_at_ && aux_err_)
+        hip_check(h.memsetAsync(aux_err_, 1, 4, stream_), "mirror fault injection");
+      report(seq, launched, host_bits);
     }
   } catch (const std::exception& e) {
     return e.what();

@@ -28,14 +28,27 @@
 //   'E' eager    n_seq {prompt, pages, start, sampling} x n_seq
 //   'S' stop
 // kind: 'D' decode graph (B, ctx bucket), 'P' prefill graph (rows, seq bucket).
+//
+// Status back channel (a kernel fault is local to the rank that saw it): for
+// every frame a follower answers on the same socket, once the device work the frame
+// enqueued has completed, with {u32 frame seq, u32 bits}: bit 0 = a fault word of a graph
+// the frame launched, or the follower device's split-K word, was set; bit 1 = a host-side
+// failure applying the frame (a provider / eager-prefill callback raised, an unknown
+// graph) -- the rest of that frame is skipped and the mirror stays alive.  The leader
+// reads the answers of every frame up to a step's before it hands that step's tokens out
+// (MirrorSender::await), so a fault on any rank fails the step on the leader too; its
+// fault record ('F') clears every graph word and the split-K word on the followers.
 #pragma once
 #include <stdint.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -65,9 +78,15 @@ class MirrorSender {
              const std::vector<std::vector<int>>& pages, const std::vector<int>& starts,
              const std::vector<LoopSampling>& samp);
   void stop();
-  void flush();  // one frame to every follower; throws if a channel is broken
+  // one frame to every follower; returns its sequence number (1, 2, ...; 0 if nothing was
+  // pending); throws if a channel is broken
+  uint32_t flush();
+  // the OR of every follower's status bits over the frames up to `seq` (blocks until each
+  // follower answered them; throws if a follower is gone or silent past timeout_s)
+  uint32_t await(uint32_t seq, double timeout_s = 120.0);
   long frames() const { return frames_; }
   long bytes() const { return bytes_; }
+  long follower_faults() const { return follower_faults_; }
 
  private:
   void head(char op, char kind, int a, int b, bool greedy);
@@ -76,14 +95,17 @@ class MirrorSender {
     buf_.append(reinterpret_cast<const char*>(&v), sizeof(T));
   }
   std::vector<int> fds_;
+  std::vector<uint32_t> acked_;  // per follower: the last frame it answered
   std::string buf_;
   std::recursive_mutex mu_;
-  std::atomic<long> frames_{0}, bytes_{0};
+  std::atomic<long> frames_{0}, bytes_{0}, follower_faults_{0};
 };
 
 class EngineMirror {
  public:
-  EngineMirror(int fd, int device) : fd_(fd), device_(device) {}
+  // P2P_MIRROR_INJECT_FAULT=N (tests): after the N-th frame that launches graphs, this rank
+  // sets its split-K fault word, as a slice that gave up on this rank only would
+  EngineMirror(int fd, int device);
   ~EngineMirror();
   EngineMirror(const EngineMirror&) = delete;
   EngineMirror& operator=(const EngineMirror&) = delete;
@@ -92,6 +114,9 @@ class EngineMirror {
   void add_prefill_graph(const PrefillGraphDesc& d);
   void set_provider(EngineLoop::GraphProvider p) { provider_ = std::move(p); }
   void set_eager_prefill(EngineLoop::EagerPrefill f) { eager_ = std::move(f); }
+  // this device's split-K fault word (p2p_split_fault_word_ptr): reported and cleared like
+  // the graphs' own words
+  void set_aux_fault(uintptr_t word) { aux_err_ = reinterpret_cast<int32_t*>(word); }
   // Applies frames until the leader's stop ("" returned) or a failure (its description:
   // a closed channel, an unknown graph, a HIP error).  Blocking; call without the GIL.
   std::string run();
@@ -109,8 +134,11 @@ class EngineMirror {
     int32_t* err = nullptr;
   };
   Graph* find(char kind, int a, int b, bool greedy);
-  void apply(const std::string& frame);
+  // applies one frame; returns the host failure bit (the frame's remaining records skipped)
+  uint32_t apply(const std::string& frame, std::vector<int32_t*>* launched);
   void* staging(size_t n);
+  void report(uint32_t seq, const std::vector<int32_t*>& launched, uint32_t host_bits);
+  void reporter();
 
   int fd_, device_;
   void* stream_ = nullptr;
@@ -124,7 +152,25 @@ class EngineMirror {
   size_t stage_n_[2] = {0, 0};
   void* stage_ev_[2] = {nullptr, nullptr};
   int cur_ = 0;
-  std::atomic<long> n_frames_{0}, n_launches_{0}, n_provides_{0}, n_eager_{0};
+  int32_t* aux_err_ = nullptr;
+  long inject_at_ = 0, launch_frames_ = 0;
+  // status reports: a ring of pinned word slots + events, drained in order by reporter()
+  static constexpr int kRep = 32, kRepWords = 16;
+  struct Report {
+    uint32_t seq, host_bits;
+    int slot, nwords;
+  };
+  int32_t* rep_words_ = nullptr;  // [kRep][kRepWords] pinned
+  void* rep_ev_[kRep] = {};
+  bool rep_busy_[kRep] = {};
+  int rep_next_ = 0;
+  std::deque<Report> rq_;
+  std::mutex rmu_;
+  std::condition_variable rcv_;
+  bool rstop_ = false;
+  std::thread rth_;
+  std::atomic<long> n_frames_{0}, n_launches_{0}, n_provides_{0}, n_eager_{0}, n_faults_{0},
+      n_host_fail_{0};
 };
 
 }  // namespace p2p

@@ -317,6 +317,10 @@ def run_follower_mirror(engine: Engine, fd: int, prefill_ctx: int) -> None:
 
     m.set_provider(provide)
     m.set_eager_prefill(eager)
+    if dev.type == "cuda":  # reported to the leader with the graphs' own words (mirror.h)
+        from ..ops.gemm import split_fault_word
+
+        m.set_aux_fault(split_fault_word(dev))
     err = m.run()
     import torch
 

@@ -102,3 +102,27 @@ def test_group_native_loop_matches_python_lockstep(world):
     # batch shapes differ from the sequential run's, so bf16 rounding may flip near-ties)
     for a, b in zip(conc_n, seq_p):
         assert a is not None and a["done"] and a["eval_count"] == b["eval_count"]
+
+
+def test_group_follower_fault_fails_the_step():
+    """a kernel fault is local to the rank that saw it.  A follower whose split-K
+    fault word is set (P2P_MIRROR_INJECT_FAULT: after its 3rd launching frame, inside the
+    first request) reports it on the group channel's status back channel (runtime/mirror.h);
+    the leader fails exactly that request with the reason, every rank's words are cleared,
+    and the next request's reply equals a clean group's."""
+    os.environ["P2P_MIRROR_INJECT_FAULT"] = "3"
+    try:
+        cs = ClusterServer("tiny-llama-gqa", gpus=2, tp=2, device="cuda", sd_seed=3, max_batch=2,
+                           warmup=False, virtual_ranks=True, start_timeout=600, kv_pages=256)
+    finally:
+        os.environ.pop("P2P_MIRROR_INJECT_FAULT", None)
+    try:
+        with pytest.raises(RuntimeError, match="follower rank"):
+            cs.handle_json(_req(0))
+        after = json.loads(cs.handle_json(_req(0)))
+        m = cs.metrics()["per_replica"][0]
+    finally:
+        cs.close()
+    assert m.get("mirror_follower_faults", 0) >= 1, m
+    clean, _conc, _m = _serve(2, True, [_req(0)])
+    assert after["response"] == clean[0]["response"] and after["eval_count"] == 24
