@@ -28,6 +28,7 @@
 
 #include "runtime/engine_loop.h"
 #include "runtime/hip_dyn.h"
+#include "runtime/loop_remote.h"
 #include "runtime/mirror.h"
 
 using namespace p2p;
@@ -518,6 +519,117 @@ int run_group_faults() {
   return failures == 0 && lm["mirror_follower_faults"] >= 2 && mm["mirror_host_failures"] == 1 ? 0 : 1;
 }
 
+// The cross-process request path (runtime/loop_remote.h) in one process: two loops serve
+// on abstract unix sockets, a RemoteLoops table routes concurrent submitters (blocking
+// waits, streaming waits, cancellations) to them; every reply must be exact, both replicas
+// must be used, and a replica whose socket is gone must be skipped, not fail requests.
+int run_remote() {
+  LoopConfig c;
+  c.num_pages = 256;
+  c.max_batch = 4;
+  c.max_prefill_tokens = 256;
+  c.max_ctx = 2048;
+  c.eos = {EOS};
+  c.decode_chunk = 4;
+  c.row_buckets = {16, 32, 48, 64, 96, 128, 192, 256};
+  c.prefill_max_pages = PREFILL_PAGES;
+  c.prefill_graph_after = 1;
+  std::vector<std::unique_ptr<EngineLoop>> loops;
+  std::vector<std::unique_ptr<DecodeGraph>> dg;
+  std::vector<std::unique_ptr<PrefillGraph>> pg;
+  std::mutex gm;
+  std::vector<std::string> names;
+  for (int r = 0; r < 2; ++r) {
+    loops.emplace_back(new EngineLoop(c));
+    EngineLoop* L = loops.back().get();
+    L->set_provider([&gm, &dg, &pg, L](const std::string& kind, int a, int b, bool) {
+      std::lock_guard<std::mutex> lk(gm);
+      if (kind == "decode") {
+        dg.emplace_back(new DecodeGraph(a, b));
+        L->add_decode_graph(dg.back()->d);
+      } else {
+        pg.emplace_back(new PrefillGraph(a, b));
+        L->add_prefill_graph(pg.back()->d);
+      }
+    });
+    L->set_eager_prefill([](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>&,
+                            const std::vector<int>&, const std::vector<LoopSampling>&) {
+      std::vector<int> f;
+      for (const auto& p : prompts) f.push_back(nxt(p.back(), (int)p.size() - 1));
+      return f;
+    });
+    names.push_back("p2p-selftest-" + std::to_string(getpid()) + "-" + std::to_string(r));
+    L->serve(names.back());
+    L->start();
+  }
+  names.push_back("p2p-selftest-nobody-" + std::to_string(getpid()));  // no server there
+  const P2PLoopApi* api = remote_loop_api();
+  void* rl = remote_loops_create(names);
+  std::atomic<int> failures{0}, checked{0};
+  auto peer = [&](int k) {
+    std::mt19937 rng(300 + k);
+    for (int n = 0; n < 8; ++n) {
+      const int Lp = std::vector<int>{3, 17, 44, 64, 120, 300}[rng() % 6];
+      std::vector<int32_t> prompt(Lp);
+      for (auto& t : prompt) t = (int32_t)(rng() % (V - 1));
+      const int max_new = 1 + (int)(rng() % 30);
+      char err[256] = {0};
+      const int64_t h = api->submit(rl, prompt.data(), Lp, max_new, 0, 0.f, 40, 0.9f, 0, err, sizeof err);
+      if (h < 0) {
+        std::fprintf(stderr, "remote: submit refused: %s\n", err);
+        failures++;
+        continue;
+      }
+      const std::vector<int> want = expected(std::vector<int>(prompt.begin(), prompt.end()), max_new, false);
+      if (n % 3 == 2) {  // cancelled right away: released without waiting
+        api->cancel(rl, h);
+        api->release(rl, h);
+        continue;
+      }
+      std::vector<int> streamed;
+      if (n % 2) {  // streaming waits
+        int done = 0;
+        while (!done) {
+          int32_t* t = nullptr;
+          int m = 0;
+          api->wait_tokens(rl, h, streamed.size(), 0.05, &t, &m, &done);
+          streamed.insert(streamed.end(), t, t + m);
+          api->free_mem(t);
+        }
+      }
+      P2PLoopResult r;
+      api->wait(rl, h, 30.0, &r);
+      std::vector<int> got(r.tokens, r.tokens + r.n_tokens);
+      if (r.error || !r.done || got != want || (n % 2 && streamed != want)) {
+        std::fprintf(stderr, "remote: reply mismatch (err %s)\n", r.error ? r.error : "-");
+        failures++;
+      }
+      api->free_mem(r.tokens);
+      api->free_mem(r.error);
+      api->release(rl, h);
+      checked++;
+    }
+  };
+  std::vector<std::thread> ths;
+  for (int k = 0; k < 6; ++k) ths.emplace_back(peer, k);
+  for (auto& t : ths) t.join();
+  const std::vector<long> routed = remote_loops_routed(rl);
+  char dead[256];
+  const int dl = api->dead(rl, dead, sizeof dead);
+  for (auto& L : loops) L->shutdown();
+  // every loop gone: submissions now fail with a reason instead of hanging
+  std::vector<int32_t> p{1, 2, 3};
+  char err[256] = {0};
+  const int64_t h = api->submit(rl, p.data(), 3, 4, 0, 0.f, 40, 0.9f, 0, err, sizeof err);
+  remote_loops_destroy(rl);
+  std::printf("remote: checked=%d failures=%d routed=%ld/%ld/%ld dead_len=%d after_shutdown=%lld '%s'\n",
+              checked.load(), failures.load(), routed[0], routed[1], routed[2], dl, (long long)h, err);
+  return failures.load() == 0 && checked.load() >= 30 && routed[0] > 0 && routed[1] > 0 &&
+                 routed[2] == 0 && dl == 0 && h < 0
+             ? 0
+             : 1;
+}
+
 }  // namespace
 
 int main() {
@@ -528,6 +640,7 @@ int main() {
   rc |= run(true, true);
   rc |= run_group();
   rc |= run_group_faults();
+  rc |= run_remote();
   if (rc == 0) std::printf("LOOP_SELFTEST_OK\n");
   return rc;
 }

@@ -192,6 +192,7 @@ void bind_engine_loop(py::module_& m) {
       // TP / EP group leader: record every device operation for the followers (mirror.h)
       .def("set_mirror", &EngineLoop::set_mirror)
       .def("set_aux_fault", &EngineLoop::set_aux_fault, py::arg("word"))
+      .def("serve", &EngineLoop::serve, py::arg("name"))
       .def("mirror_provide", &EngineLoop::mirror_provide, py::call_guard<py::gil_scoped_release>())
       .def("start", &EngineLoop::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &EngineLoop::stop, py::call_guard<py::gil_scoped_release>())

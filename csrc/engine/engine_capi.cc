@@ -31,6 +31,7 @@
 #include "engine/native_tok.h"
 #include "net/json.h"
 #include "runtime/loop_capi.h"
+#include "runtime/loop_remote.h"
 
 using p2p::Json;
 
@@ -40,6 +41,7 @@ namespace {
 struct Front {
   const P2PLoopApi* api = nullptr;
   void* loop = nullptr;
+  bool remote = false;  // loop is a RemoteLoops over the replicas' sockets (loop_remote.h)
   p2p::NativeTok tok;
   std::string model;
   int default_max = 128;
@@ -450,6 +452,19 @@ void attach_front(p2p_engine* e) {
   auto item = [&](const char* k) { return PyDict_GetItemString(d, k); };  // borrowed
   if (PyObject* v = item("api")) f->api = (const P2PLoopApi*)PyLong_AsVoidPtr(v);
   if (PyObject* v = item("loop")) f->loop = PyLong_AsVoidPtr(v);
+  if (PyObject* v = item("cluster")) {  // multi-GPU node: the replica leaders' loop sockets
+    std::vector<std::string> names;
+    const Py_ssize_t n = PyList_Check(v) ? PyList_Size(v) : 0;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      const char* c = PyUnicode_AsUTF8(PyList_GetItem(v, i));
+      if (c) names.push_back(c);
+    }
+    if (!names.empty() && (Py_ssize_t)names.size() == n) {
+      f->api = p2p::remote_loop_api();
+      f->loop = p2p::remote_loops_create(names);
+      f->remote = true;
+    }
+  }
   if (PyObject* v = item("model")) f->model = PyUnicode_AsUTF8(v) ? PyUnicode_AsUTF8(v) : "";
   if (PyObject* v = item("default_max_tokens")) f->default_max = (int)PyLong_AsLong(v);
   if (PyObject* v = item("timeout_s")) f->timeout_s = PyFloat_AsDouble(v);
@@ -526,6 +541,13 @@ char* p2p_engine_generate(p2p_engine* e, const char* request_json) {
         m.set("capi_python_decode", (long long)f.python_decode.load());
         m.set("capi_gil_entries", (long long)g_gil_entries.load());
         m.set("capi_native_tokenizer", f.tok.ok ? 1 : 0);
+        if (f.remote) {  // requests the C ABI routed to each replica's loop socket
+          Json per = Json::array();
+          long tot = 0;
+          for (long r : p2p::remote_loops_routed(f.loop)) per.push(Json(r)), tot += r;
+          m.set("capi_remote_routed", per);
+          m.set("capi_remote_requests", (long long)tot);
+        }
         return strdup(m.dump().c_str());
       }
     } catch (const std::exception&) {
@@ -565,6 +587,7 @@ const char* p2p_engine_error(void) { return t_err.c_str(); }
 
 void p2p_engine_destroy(p2p_engine* e) {
   if (!e) return;
+  if (e->front && e->front->remote) p2p::remote_loops_destroy(e->front->loop);
   PyGILState_STATE g = PyGILState_Ensure();
   PyObject* r = PyObject_CallMethod(e->server, "close", nullptr);
   if (!r) PyErr_Clear();

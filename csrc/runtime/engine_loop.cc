@@ -1,4 +1,5 @@
 #include "runtime/engine_loop.h"
+#include "runtime/loop_remote.h"
 
 #include <algorithm>
 #include <chrono>
@@ -39,9 +40,19 @@ EngineLoop::EngineLoop(const LoopConfig& cfg)
 
 // The thread only: HIP resources are released by shutdown() (a destructor running at
 // interpreter exit may find the HIP runtime already torn down).
-EngineLoop::~EngineLoop() { stop(); }
+EngineLoop::~EngineLoop() {
+  if (server_) server_->stop();
+  stop();
+}
+
+void EngineLoop::serve(const std::string& name) {
+  if (server_) throw std::runtime_error("loop already serving");
+  server_.reset(new LoopServer(this, name));
+  server_->start();
+}
 
 void EngineLoop::shutdown() {
+  if (server_) server_->stop();  // no new requests; open ones are cancelled
   stop();
   const HipApi& h = hip_api();
   if (!h.ok) return;

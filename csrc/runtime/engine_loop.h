@@ -39,6 +39,7 @@
 namespace p2p {
 
 class MirrorSender;  // runtime/mirror.h
+class LoopServer;    // runtime/loop_remote.h
 
 struct LoopSampling {
   float temperature = 0.f;  // <= 0: greedy
@@ -139,6 +140,9 @@ class EngineLoop {
   void set_aux_fault(uintptr_t word) { aux_err_ = reinterpret_cast<int32_t*>(word); }
   // a graph provider about to capture (kind, a, b, greedy): the followers capture it too
   void mirror_provide(const std::string& kind, int a, int b, bool greedy);
+  // serve requests from other processes on the abstract unix socket @name (the node of a
+  // multi-GPU cluster routes to this replica natively: runtime/loop_remote.h)
+  void serve(const std::string& name);
   void start();
   void stop();
   void shutdown();  // stop + release the loop's HIP resources (stream, events, pinned memory)
@@ -212,6 +216,7 @@ class EngineLoop {
   GraphProvider provider_;
   EagerPrefill eager_;
   std::unique_ptr<MirrorSender> mirror_;
+  std::unique_ptr<LoopServer> server_;
   bool mirror_stopped_ = false;
 
   // device-side state of the loop thread

@@ -442,7 +442,15 @@ def _leader_main(spec, replica, eng, parent_conn, follower_conns):
         finally:
             cancelled.discard(rid)
 
-    send(("ready", replica))
+    sock = None
+    if hasattr(server, "serve_socket"):
+        # the node's engine C ABI reaches this replica's native loop directly over this
+        # socket (runtime/loop_remote.h): no pickled pipe, no Python on either side
+        try:
+            sock = server.serve_socket("p2p-loop-%d-r%d" % (os.getpid(), replica))
+        except Exception as e:  # noqa: BLE001 -- the pipe path still serves
+            print("replica %d: native socket unavailable: %s" % (replica, e), flush=True)
+    send(("ready", replica, sock))
 
     def watchdog():  # a fatal engine error ends the replica loudly
         while server.dead is None:
@@ -476,6 +484,7 @@ class _Replica:
         self.idx = idx
         self.conn = conn
         self.procs = procs
+        self.socket = None  # the leader loop's native request socket (loop_remote.h)
         self.outstanding = 0
         self.served = 0
         self.alive = True
@@ -500,6 +509,10 @@ class ClusterServer:
             raise ValueError("ENGINE_GPUS=%d is not a multiple of TP*EP=%d" % (gpus, group))
         self.n_replicas = gpus // group
         self.group = group
+        self.model = model
+        self.model_name = model_name
+        self.max_tokens = max_tokens
+        self.tokenizer_path = tokenizer or checkpoint
         spec = dict(model=model, tp=tp, ep=ep, max_batch=max_batch, max_tokens=max_tokens,
                     model_name=model_name, weights=weights, tokenizer=tokenizer, sd_seed=sd_seed,
                     kv_pages=kv_pages, warmup=warmup, world=gpus, checkpoint=checkpoint or None,
@@ -538,6 +551,7 @@ class ClusterServer:
             if msg[0] != "ready":
                 self.close()
                 raise RuntimeError("engine replica %d failed to start:\n%s" % (rep.idx, msg[1]))
+            rep.socket = msg[2] if len(msg) > 2 else None
         for rep in self._replicas:
             threading.Thread(target=self._reader, args=(rep,), daemon=True,
                              name="replica-%d-reader" % rep.idx).start()
@@ -663,6 +677,33 @@ class ClusterServer:
                 from None
 
     # ------------------------------------------------------------- hooks
+    def native_front(self) -> dict | None:
+        """The engine C ABI's native request path over this cluster (csrc/engine/
+        engine_capi.cc + runtime/loop_remote.h): every replica leader's loop socket, and the
+        tokenizer's native spec (requests are tokenised here, in the node process, exactly
+        as a leader would).  None when a replica has no native loop (EP a2a groups, CPU
+        engines): requests then go through handle_json and the replica pipes."""
+        if not self._replicas or not all(r.socket for r in self._replicas):
+            return None
+        import json as _json
+
+        from .tokenizer import get_tokenizer
+
+        if self.tokenizer_path and os.path.isdir(self.tokenizer_path) \
+                and os.path.exists(os.path.join(self.tokenizer_path, "config.json")):
+            from ..models.weights import config_from_hf
+
+            cfg = config_from_hf(self.tokenizer_path)
+        else:
+            from ..models.config import get_config
+
+            cfg = get_config(self.model)
+        tok = get_tokenizer(cfg, self.tokenizer_path)
+        return {"cluster": [r.socket for r in self._replicas], "model": self.model_name,
+                "default_max_tokens": int(self.max_tokens),
+                "timeout_s": float(os.environ.get("ENGINE_TIMEOUT", "60")),
+                "tokenizer": _json.dumps(tok.native_spec())}
+
     def handle_json(self, req_text: str) -> str:
         req = json.loads(req_text)
         if req.get("endpoint") == "metrics":
@@ -739,4 +780,7 @@ def from_env(device: str | None = None):
                          warmup=os.environ.get("ENGINE_WARMUP", "1") != "0",
                          first_gpu=int(os.environ.get("ENGINE_FIRST_GPU", "0")),
                          checkpoint=os.environ.get("ENGINE_CHECKPOINT") or None,
-                         ep_mode=os.environ.get("ENGINE_EP_MODE", "allreduce"))
+                         ep_mode=os.environ.get("ENGINE_EP_MODE", "allreduce"),
+                         kv_pages=int(os.environ["ENGINE_KV_PAGES"]) if os.environ.get("ENGINE_KV_PAGES") else None,
+                         # tests: every rank process on the one GPU of the box
+                         virtual_ranks=os.environ.get("ENGINE_VIRTUAL_RANKS", "0") == "1")

@@ -181,6 +181,12 @@ class NativeEngineServer(EngineServer):
                 "model": self.model_name, "default_max_tokens": int(self.default_max_tokens),
                 "timeout_s": float(self.request_timeout_s), "tokenizer": json.dumps(spec)}
 
+    def serve_socket(self, name: str) -> str:
+        """Serve requests of other processes on the abstract unix socket @name (the node
+        of a multi-GPU cluster routes to this replica without Python: runtime/loop_remote.h)."""
+        self.loop.serve(name)
+        return name
+
     def encode_request(self, req_text: str) -> list:
         """Prompt ids of an Ollama request (the C ABI's fallback tokenisation)."""
         req = json.loads(req_text)

@@ -462,16 +462,28 @@ def test_upnp_igd_port_mapping(procs):
         web.shutdown()
 
 
-@pytest.mark.parametrize("dev,tokfile", [("cpu", False), pytest.param("cuda:0", False, marks=pytest.mark.gpu),
-                                         pytest.param("cuda:0", True, marks=pytest.mark.gpu)],
-                         ids=["cpu", "gpu", "gpu-bpe"])
-def test_node_daemon_hosts_engine_in_process(procs, dev, tokfile, tmp_path):
+_CLUSTER_DP2 = {"ENGINE_GPUS": "2", "ENGINE_VIRTUAL_RANKS": "1", "ENGINE_KV_PAGES": "256",
+                "ENGINE_WARMUP": "0", "ENGINE_SD_SEED": "3"}
+_CLUSTER_TP2 = dict(_CLUSTER_DP2, ENGINE_TP="2", ENGINE_MODEL="tiny-llama-gqa")
+
+
+@pytest.mark.parametrize("dev,tokfile,cluster", [
+    ("cpu", False, None), pytest.param("cuda:0", False, None, marks=pytest.mark.gpu),
+    pytest.param("cuda:0", True, None, marks=pytest.mark.gpu),
+    pytest.param("cuda:0", True, _CLUSTER_DP2, marks=pytest.mark.gpu),
+    pytest.param("cuda:0", False, _CLUSTER_TP2, marks=pytest.mark.gpu)],
+    ids=["cpu", "gpu", "gpu-bpe", "gpu-dp2-bpe", "gpu-tp2"])
+def test_node_daemon_hosts_engine_in_process(procs, dev, tokfile, cluster, tmp_path):
     """ENGINE=inproc: the C++ node daemon loads the engine C ABI (libp2p_engine.so,
     csrc/engine/engine_capi.h) and serves /api/generate (plain and streaming NDJSON)
     and /suggest from the engine in its own process -- the node links the engine the
     way the BASELINE north star's Go node links it through cgo (CPU tiny-llama here).
     gpu-bpe: with TOKENIZER_PATH naming a Llama-3-style tokenizer.json the native BPE
-    tokenizer (csrc/engine/bpe_tok.h) serves it, still with no interpreter entry."""
+    tokenizer (csrc/engine/bpe_tok.h) serves it, still with no interpreter entry.
+    gpu-dp2-bpe / gpu-tp2: a multi-GPU node (ENGINE_GPUS=2 replicas, or one ENGINE_TP=2
+    group; virtual ranks: every rank process on the box's one GPU) -- the C ABI routes each
+    request to a replica leader's native loop over its socket (runtime/loop_remote.h), so
+    these serve with no interpreter entry either."""
     lib = os.path.join(os.path.dirname(BIN), "p2p_llm_chat_go_amd", "_lib", "libp2p_engine.so")
     if not os.path.exists(lib):
         pytest.skip("engine C ABI not built")
@@ -484,9 +496,11 @@ def test_node_daemon_hosts_engine_in_process(procs, dev, tokfile, tmp_path):
         from tokutil import train_bpe_tokenizer
 
         env["TOKENIZER_PATH"] = train_bpe_tokenizer(tmp_path, vocab=500)
+    if cluster:
+        env.update(cluster)
     procs.spawn("p2p-node", env)
     a = "http://127.0.0.1:%d" % port
-    wait_http(a + "/me", timeout=120)
+    wait_http(a + "/me", timeout=600 if cluster else 120)
     st, body, _ = http("POST", a + "/api/generate", {"model": "llama3.1", "prompt": "hello",
                                                       "stream": False,
                                                       "options": {"num_predict": 5}})
@@ -524,6 +538,8 @@ def test_node_daemon_hosts_engine_in_process(procs, dev, tokfile, tmp_path):
         # non-ASCII text: native with a tokenizer.json, Python's with the synthetic tokenizer
         assert (m2.get("p2p_engine_capi_python_tokenize") == 0) == tokfile, m2
         assert m2.get("p2p_engine_capi_python_decode") == 0, m2
+        if cluster:  # served by the replica leaders' loops over their sockets
+            assert m2.get("p2p_engine_capi_remote_requests", 0) >= 4, m2
 
 
 def test_connection_manager_trims_to_low_watermark(procs):
