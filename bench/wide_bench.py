@@ -66,10 +66,12 @@ def main():
             from p2p_llm_chat_go_amd.ops import _lib
             for res in (1, 0) if os.environ.get("WIDE_AB_RES", "0") == "1" else (1,):
                 _lib.lib().p2p_wide_resident(res)
-                for s in splits:
-                    code = G.WIDE_FLAG | (s << 8)
-                    t = _graph_time(lambda: [fn(wt, code) for wt in wts]) * 1000 / len(wts)
-                    row["wide%s_s%s" % ("" if res else "ring", s if s else "auto")] = round(t, 2)
+                for nw in [int(v) for v in os.environ.get("WIDE_NWS", "8,16").split(",")]:
+                    for s in splits:
+                        code = G.WIDE_FLAG | (s << 8) | (G.WIDE16 if nw == 16 else 0)
+                        t = _graph_time(lambda: [fn(wt, code) for wt in wts]) * 1000 / len(wts)
+                        row["wide%s%s_s%s" % ("16" if nw == 16 else "", "" if res else "ring",
+                                             s if s else "auto")] = round(t, 2)
             _lib.lib().p2p_wide_resident(1)
             assert ops.tiled_split_fault() == 0
             print(json.dumps(row), flush=True)

@@ -46,7 +46,8 @@ int skinny_unit_argmax(SKINNY_UNIT_ARGS);
 int skinny_unit_ar(SKINNY_UNIT_ARGS);
 
 constexpr int MIDM_FLAG = 1 << 25;  // launch-code bit (ops.gemm.MIDM_FLAG)
-constexpr int WIDE_FLAG = 1 << 26;  // launch-code bit (ops.gemm.WIDE_FLAG), K slices in bits 8..15
+constexpr int WIDE_FLAG = 1 << 26;  // launch-code bit (ops.gemm.WIDE_FLAG), K slices in bits 8..15,
+                                     // bit 16: 16 waves per workgroup (ops.gemm.WIDE16)
 constexpr int PERSIST_FLAG = 1 << 28;  // ops.gemm.PERSIST_FLAG: persist_gemv.hip, CU multiple in 8..15
 // the persistent GEMV lives in the experimental library (measured slower than the skinny
 // launches, profiles/r4_persist_gemv_negative.jsonl): resolved when that library is loaded
@@ -98,7 +99,7 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
   }
   // bit 26: the wide mid-M kernel (wide_gemm.hip; bf16 dense weights, K % 256 == 0)
   if ((waves & WIDE_FLAG) && epi != EPI_AR)
-    return p2p_wide_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, &ea, (waves >> 8) & 0xff,
+    return p2p_wide_dispatch(Wt, X, ldx, M, K, N, epi, norm, out, ldo, eps, &ea, (waves >> 8) & 0x1ff,
                              stream);
   // bit 25: the mid-M LDS-DMA kernel (midm_gemm.h; bf16 dense weights, K % 128 == 0)
   if ((waves & MIDM_FLAG) && !ea.wscale && !ea.moe_cnt && K % 128 == 0) {

@@ -47,7 +47,6 @@ __device__ long long* wide_stamp_buf;
 #define WSTAMP(i, v) do { } while (0)
 #endif
 
-constexpr int NT = 512;   // 8 waves
 constexpr int KC = 8;     // k-steps per chunk: wave w DMA-loads k-step w of every m-tile
 constexpr int MAX_SPLIT = 16;  // K slices per tile (the rstd reduction unrolls over them)
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -90,28 +89,41 @@ constexpr int res_chunks() { return 18 / MT; }
 // RES: the slice's whole activation block is DMA'd into LDS up front (one barrier), so the
 // waves never meet again in the k loop and each streams its weights at its own pace;
 // otherwise the activations stream through a ring with a barrier per chunk.
-template <int MT, int EPI, bool NORM, bool SPLIT, bool RES>
-__global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict__ Wt,
-                                                       const bf16* __restrict__ X, int ldx, int M,
-                                                       int K, int n_tiles, int up_off,
-                                                       void* __restrict__ out, int ldo, float eps,
-                                                       EpiArgs ea, GranArgs ga) {
+// NW = 16 (r6): two waves per column group, splitting every chunk's k-steps by parity (wave
+// w and w + 8 stream group w & 7, k-steps of parity w >> 3), summed through LDS after the k
+// loop.  A pure weight stream of these sizes reaches ~6.4 TB/s with 16 waves per CU and only
+// ~5.3 with 8 (bench/stream_probe.py, profiles/r6_stream_probe.md): the 8-wave grid, one
+// workgroup per CU, could not feed HBM however many bytes each wave kept in flight.
+template <int MT, int EPI, bool NORM, bool SPLIT, bool RES, int NW>
+__global__ __launch_bounds__(NW * 64) void wide_gemm_kernel(const bf16x8* __restrict__ Wt,
+                                                            const bf16* __restrict__ X, int ldx, int M,
+                                                            int K, int n_tiles, int up_off,
+                                                            void* __restrict__ out, int ldo, float eps,
+                                                            EpiArgs ea, GranArgs ga) {
   constexpr bool SILU = EPI == EPI_SILU;
-  // pipeline depth: D chunks ahead (RS = D + 1 register sets of KC weight fragments: 128
-  // VGPRs at D = 3), activation ring of D + 2 slots (<= 128 KiB of LDS at every MT)
-  constexpr int D = MT >= 4 ? 2 : 3;
+  constexpr int NPAR = NW / 8;   // waves per column group (k-step parities)
+  constexpr int KW = KC / NPAR;  // k-steps of a chunk per wave
+  constexpr int NQ = NW / 4;     // NORM: k-step classes (mod NQ) x 4 m-tiles = NW waves
+  constexpr int NQ2 = 2;         // classes left after the pair exchange (NW = 16: 2 + 2 -> 2)
+  // pipeline depth: D chunks ahead (RS = D + 1 register sets of KW weight fragments: 128
+  // VGPRs at NW = 8, D = 3; 48 at NW = 16, D = 2), activation ring of D + 2 slots (<= 128 KiB)
+  constexpr int D = NW == 16 ? (MT >= 4 ? 1 : 2) : (MT >= 4 ? 2 : 3);
   constexpr int RS = D + 1;
   constexpr int RING = D + 2;
   constexpr int SLOT = MT * KC * 64;  // bf16x8 per ring slot
-  constexpr int PER_CHUNK = MT + KC;  // vmem instructions per thread per chunk
+  constexpr int AD = (MT + NPAR - 1) / NPAR;  // activation DMA instructions per wave per chunk
+  constexpr int PER_CHUNK = AD + KW;  // vmem instructions per thread per chunk
   constexpr int NSLOT = RES ? res_chunks<MT>() : RING;
+  constexpr int NSV = NQ2 * MAX_SPLIT / 4;  // row-sum granules polled per lane (split-K NORM)
   __shared__ __attribute__((aligned(16))) bf16x8 ring[NSLOT * SLOT];
-  __shared__ float ss_l[2][4][16];
+  __shared__ float ss_l[NQ2][4][16];
+  __shared__ int slot_l[64], pos_l[64];  // EPI_QKV_ROPE: the rows' KV slots and positions
 
   const int splitk = SPLIT ? ga.splitk : 1;
   const int b = xcd_remap(blockIdx.x, n_tiles * splitk);
   const int tile = b / splitk, split = b % splitk;  // a tile's slices are consecutive
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wg = w & 7, par = w >> 3;  // column group of the tile, k-step parity
   const int S = K >> 5;
   // K slices in k-step units (r5: chunk-unit slices left qkv's 16 chunks in 5 slices as
   // 3/3/3/3/4 and the seam waited ~2.7 us for the long one); chunk c of the slice covers
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   if constexpr (SPLIT)
     if (tid == 0) tkt = __hip_atomic_fetch_add(&ga.ticket[tile], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-  const int gw = SILU ? (w < 4 ? tile * 4 + w : tile * 4 + (w - 4) + up_off) : tile * 8 + w;
+  const int gw = SILU ? (wg < 4 ? tile * 4 + wg : tile * 4 + (wg - 4) + up_off) : tile * 8 + wg;
   const bf16x8* wsrc = Wt + (size_t)gw * S * 64 + lane;
   const bf16* asrc[MT];
 #pragma unroll
@@ -139,42 +151,49 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     asrc[i] = X + (size_t)row * ldx + 8 * (lane >> 4);
   }
 
+  // chunk c's activations: wave w loads k-step w & 7 of the m-tiles of its parity (NW = 16:
+  // the odd wave of a pair repeats its last m-tile when MT is odd, so every wave issues AD
+  // instructions -- the same bytes to the same LDS place -- and the counted waits hold)
   auto issue_a = [&](int c) {
     bf16x8* base = ring + (c % NSLOT) * SLOT;
-    const int kk = ks0 + c * KC + min(w, kv_of(c) - 1);
+    const int kk = ks0 + c * KC + min(wg, kv_of(c) - 1);
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int a = 0; a < AD; ++a) {
+      const int i = min(par + NPAR * a, MT - 1);
       __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (size_t)kk * 32),
-                                       (lds_ptr_t)(base + (i * KC + w) * 64), 16, 0, 0);
+                                       (lds_ptr_t)(base + (i * KC + wg) * 64), 16, 0, 0);
+    }
   };
-  auto issue_w = [&](int c, bf16x8(&wr)[KC]) {
+  auto issue_w = [&](int c, bf16x8(&wr)[KW]) {
     const int kb = ks0 + c * KC, kl = kv_of(c) - 1;
 #pragma unroll
-    for (int k = 0; k < KC; ++k) wr[k] = __builtin_nontemporal_load(wsrc + (size_t)(kb + min(k, kl)) * 64);
+    for (int j = 0; j < KW; ++j)
+      wr[j] = __builtin_nontemporal_load(wsrc + (size_t)(kb + min(par + NPAR * j, kl)) * 64);
   };
-  auto issue = [&](int c, bf16x8(&wr)[KC]) {
+  auto issue = [&](int c, bf16x8(&wr)[KW]) {
     if constexpr (!RES) issue_a(c);
     issue_w(c, wr);
   };
 
-  constexpr int PC = RES ? KC : PER_CHUNK;  // vmem instructions per chunk in the k loop
+  constexpr int PC = RES ? KW : PER_CHUNK;  // vmem instructions per chunk in the k loop
   auto wait_chunks = [&](int k) {  // at most k chunks of this thread's loads in flight
     switch (k) {
       case 0: wait_vmcnt<0>(); break;
       case 1: wait_vmcnt<PC>(); break;
       case 2: wait_vmcnt<2 * PC>(); break;
-      default: wait_vmcnt<(D >= 3 ? 3 : 2) * PC>(); break;
+      default: wait_vmcnt<(D >= 3 ? 3 : D) * PC>(); break;
     }
   };
 
-  // The units this wave finishes: output group w (SILU: gate/up pair w < 4) at m-tile i;
-  // under split-K unit (w, i) belongs to slice (w * MT + i) % splitk, so the 8 * MT units
-  // of a tile spread over all its slices' waves (at most one each from splitk >= MT).
+  // The units this wave finishes: output group wg (SILU: gate/up pair wg < 4) at m-tile i;
+  // under split-K unit (wg, i) belongs to slice (wg * MT + i) % splitk, so the 8 * MT units
+  // of a tile spread over all its slices' waves (at most one each from splitk >= MT).  Only
+  // the even wave of a parity pair finishes (it holds the pair's sum).
   const int r = lane & 15, q = lane >> 4;
   auto owns = [&](int i) {
-    return w < (SILU ? 4 : 8) && (!SPLIT || (w * MT + i) % splitk == split);
+    return par == 0 && wg < (SILU ? 4 : 8) && (!SPLIT || (wg * MT + i) % splitk == split);
   };
-  const int g = SILU ? tile * 4 + w : tile * 8 + w;
+  const int g = SILU ? tile * 4 + wg : tile * 8 + wg;
   // Epilogue operands, issued as ONE batch per lane BEFORE the weight stream (they are the
   // oldest loads in flight, so the counted chunk waits below still hold, and they have long
   // landed when the epilogue runs): the residual values (EPI_RESID), the rows' KV slots and
@@ -182,10 +201,10 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   // after the main loop).  Issued after the main loop, the residual loads held up the slab
   // drain of the split-K seam by ~1.6 us (bench/wide_stamp_probe.py, r5); loaded element by
   // element in the epilogue they were a chain of MT x 4 dependent round trips per lane.
+  // (r6: the rows' slots / positions land in LDS by DMA from wave 0, not in 24 VGPRs per lane
+  // held across the k loop -- the 16-wave variant has 128 VGPRs per lane in all)
   float res[MT][4];
   float2 csv[MT][4];
-  int slotv[MT][4];
-  int posv[MT][4];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -193,47 +212,47 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
       const int m = 16 * i + 4 * q + j;
       const bool ok = owns(i) && m < M;
       res[i][j] = 0.f;
-      slotv[i][j] = -1;
-      posv[i][j] = -1;
       csv[i][j] = float2{1.f, 0.f};
-      if constexpr (EPI == EPI_RESID)
+      if constexpr (EPI == EPI_RESID && !(SPLIT && NW == 16))
         if (ok) res[i][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + g * 16 + r];
-      if constexpr (EPI == EPI_QKV_ROPE)
-        if (ok) {
-          slotv[i][j] = ea.slots[m];
-          posv[i][j] = ea.pos[m];
-        }
+    }
+  if constexpr (EPI == EPI_QKV_ROPE)
+    if (w == 0) {
+      const int mm = min(lane, M - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(ea.slots + mm), (lds_ptr_t)slot_l, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(ea.pos + mm), (lds_ptr_t)pos_l, 4, 0, 0);
     }
 
   f32x4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ss = 0.f;  // NORM: rows of m-tile (w & 3), k-steps of parity (w >> 2), this lane's 8 k
-  const int sq_mt = w & 3, sq_par = w >> 2;
+  float ss = 0.f;  // NORM: rows of m-tile (w & 3), k-steps = (w >> 2) mod NQ, this lane's 8 k
+  const int sq_mt = w & 3, sq_q = w >> 2;
 
-  auto compute_kv = [&](const bf16x8* base, const bf16x8(&wr)[KC], int kv, auto full) {
+  auto compute_kv = [&](const bf16x8* base, const bf16x8(&wr)[KW], int kv, auto full) {
     constexpr bool FULL = decltype(full)::value;
 #pragma unroll
-    for (int k = 0; k < KC; ++k) {
+    for (int j = 0; j < KW; ++j) {
+      const int k = par + NPAR * j;
       if (!FULL && k >= kv) break;
       bf16x8 a[MT];
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[i] = base[(i * KC + k) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < MT; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], wr[k], acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], wr[j], acc[i], 0, 0, 0);
     }
     if constexpr (NORM) {
       if (sq_mt < MT) {
 #pragma unroll
-        for (int k = 0; k < KC; k += 2) {
-          if (!FULL && k + sq_par >= kv) break;
-          ss = sumsq8(base[(sq_mt * KC + k + sq_par) * 64 + lane], ss);
+        for (int k = 0; k < KC; k += NQ) {
+          if (!FULL && k + sq_q >= kv) break;
+          ss = sumsq8(base[(sq_mt * KC + k + sq_q) * 64 + lane], ss);
         }
       }
     }
   };
-  auto compute = [&](int c, const bf16x8(&wr)[KC]) {
+  auto compute = [&](int c, const bf16x8(&wr)[KW]) {
     const bf16x8* base = ring + (c % NSLOT) * SLOT;
     const int kv = kv_of(c);
     if (kv == KC)
@@ -245,7 +264,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   // D chunks (activation DMA + this wave's weights) are in flight ahead of the one being
   // computed; the counted wait + barrier makes chunk t complete (every wave's DMA part), and
   // the ring slot refilled at step t (chunk t+D's) was last read at t-2, before barrier t-1
-  bf16x8 wr[RS][KC];
+  bf16x8 wr[RS][KW];
   if constexpr (RES)  // the whole slice's activations first (host: n <= res_chunks)
     for (int c = 0; c < n; ++c) issue_a(c);
 #pragma unroll
@@ -269,20 +288,56 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   }
 
   WSTAMP(2, wall_clock64());
-  // ---- this slice's row sums of squares: wave pair (w, w ^ 4) holds m-tile w & 3 ----
+  // ---- this wave's row sums of squares: the NQ waves w = sq_mt + 4 x hold m-tile sq_mt ----
   if constexpr (NORM) {
     ss += __shfl_xor(ss, 16, 64);
     ss += __shfl_xor(ss, 32, 64);
-    if (!SPLIT && sq_mt < MT && lane < 16) ss_l[sq_par][sq_mt][lane] = ss;
   }
-  if constexpr (EPI == EPI_QKV_ROPE) {
-    const int kk = g & 7;
-    const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+  if constexpr (NPAR > 1) {
+    // the odd wave of each pair hands its partial sums (and its row sums of squares: k
+    // classes 2, 3 -> 0, 1) to the even one through LDS (the activation buffer is free once
+    // every wave is past its last read of it)
+    float* xp = reinterpret_cast<float*>(ring);
+    float* xs = xp + 8 * MT * 4 * 64;
+    __syncthreads();
+    if (par == 1) {
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (posv[i][j] >= 0) csv[i][j] = ea.cs[(size_t)posv[i][j] * 64 + dd];
+        for (int j = 0; j < 4; ++j) xp[((wg * MT + i) * 4 + j) * 64 + lane] = acc[i][j];
+      if constexpr (NORM) xs[(w - 8) * 64 + lane] = ss;
+    }
+    __syncthreads();
+    if (par == 0) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += xp[((wg * MT + i) * 4 + j) * 64 + lane];
+      if constexpr (NORM) ss += xs[w * 64 + lane];
+    }
+  }
+  if constexpr (NORM)
+    if (!SPLIT && par == 0 && sq_mt < MT && lane < 16) ss_l[sq_q & 1][sq_mt][lane] = ss;
+  int slotv[MT][4];
+  // EPI_QKV_ROPE: unit (i)'s KV slots and (cos, sin) -- issued right before the unit's poll
+  // (split-K) or its stores; the slots / positions DMA was wave 0's first load, landed at the
+  // chunk-0 barrier
+  auto rope_operands = [&](int i) {
+    if constexpr (EPI == EPI_QKV_ROPE) {
+      const int kk = g & 7;
+      const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = 16 * i + 4 * q + j;
+        const bool ok = owns(i) && m < M;
+        slotv[i][j] = ok ? slot_l[m] : -1;
+        if (ok) csv[i][j] = ea.cs[(size_t)pos_l[m] * 64 + dd];
+      }
+    }
+  };
+  if constexpr (!SPLIT) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) rope_operands(i);
   }
 
   auto epilogue = [&](const f32x4 (&v)[MT], const f32x4 (&u)[MT], auto&& rstd_of) {
@@ -309,22 +364,23 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
   if constexpr (!SPLIT) {
     // the up waves hand their accumulators to the gate waves through LDS (ring is free)
     float* xch = reinterpret_cast<float*>(ring);
-    __syncthreads();  // every wave is past its last ring read; ss_l complete
+    __syncthreads();  // every wave is past its last ring read (and the pair sums); ss_l complete
     if constexpr (SILU) {
-      if (w >= 4) {
+      if (par == 0 && wg >= 4) {
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) xch[(((w - 4) * MT + i) * 4 + j) * 64 + lane] = acc[i][j];
+          for (int j = 0; j < 4; ++j) xch[(((wg - 4) * MT + i) * 4 + j) * 64 + lane] = acc[i][j];
       }
       __syncthreads();
-      if (w >= 4) return;
+      if (wg >= 4) return;
     }
+    if (par != 0) return;
     f32x4 up[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) up[i][j] = SILU ? xch[((w * MT + i) * 4 + j) * 64 + lane] : 0.f;
+      for (int j = 0; j < 4; ++j) up[i][j] = SILU ? xch[((wg * MT + i) * 4 + j) * 64 + lane] : 0.f;
     }
     epilogue(acc, up, [&](int i, int j) {
       if constexpr (!NORM) return 1.f;
@@ -342,16 +398,18 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     const u64 tg = (u64)tag << 32;
     u64* gt = ga.gran + (size_t)tile * splitk * 8 * 4 * 256;  // this tile's region
     auto gidx = [&](int s2, int wv, int i, int j) { return (((s2 * 8 + wv) * 4 + i) * 4 + j) * 64 + lane; };
+    if (par == 0) {
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        __hip_atomic_store(gt + gidx(split, w, i, j), tg | __float_as_uint(acc[i][j]),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    u64* st = ga.ssg + (size_t)tile * splitk * 128;  // [split][parity][64 rows]
+        for (int j = 0; j < 4; ++j)
+          __hip_atomic_store(gt + gidx(split, wg, i, j), tg | __float_as_uint(acc[i][j]),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    u64* st = ga.ssg + (size_t)tile * splitk * NQ2 * 64;  // [split][k class][64 rows]
     if constexpr (NORM)
-      if (sq_mt < MT && lane < 16)
-        __hip_atomic_store(st + (split * 2 + sq_par) * 64 + 16 * sq_mt + lane, tg | __float_as_uint(ss),
+      if (par == 0 && sq_mt < MT && lane < 16)
+        __hip_atomic_store(st + (split * NQ2 + (sq_q & 1)) * 64 + 16 * sq_mt + lane, tg | __float_as_uint(ss),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     WSTAMP(3, wall_clock64());
     bool any = false;
@@ -361,17 +419,24 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
     // Finish the owned units.  One poll sweep re-reads a batch of SB slices' granules (and,
     // for the first batch, the rows' sum-of-squares granules) until every tag is this
     // launch's; the partials are summed in slice order (deterministic).
-    constexpr int SB = SILU ? 4 : 8;
+    constexpr int SB = NW == 16 ? (SILU ? 2 : 4) : (SILU ? 4 : 8);  // (NW = 16: 128 VGPRs)
     const long long t0 = wall_clock64();
     bool failed = false;
     auto ready = [&](u64 x) { return (unsigned)(x >> 32) == tag; };
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       if (!owns(i)) continue;
+      rope_operands(i);
+      if constexpr (EPI == EPI_RESID && NW == 16)  // (16 waves: loaded here, behind the poll)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = 16 * i + 4 * q + j;
+          if (m < M) res[i][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + g * 16 + r];
+        }
       f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f}, upv = f32x4{0.f, 0.f, 0.f, 0.f};
       float rowss = 0.f;  // NORM: lane l holds row 16 i + (l & 15) after the shuffles
       for (int s0 = 0; s0 < splitk; s0 += SB) {
-        u64 pt[SB][4], pu[SB][4], sv[8];
+        u64 pt[SB][4], pu[SB][4], sv[NSV];
         for (;;) {
           bool ok = true;
 #pragma unroll
@@ -379,19 +444,19 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
             if (s0 + s >= splitk) break;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              pt[s][j] = __hip_atomic_load(gt + gidx(s0 + s, w, i, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              pt[s][j] = __hip_atomic_load(gt + gidx(s0 + s, wg, i, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               if constexpr (SILU)
-                pu[s][j] = __hip_atomic_load(gt + gidx(s0 + s, w + 4, i, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pu[s][j] = __hip_atomic_load(gt + gidx(s0 + s, wg + 4, i, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           }
           if constexpr (NORM)
             if (s0 == 0) {
-              // lane l: row 16 i + (l & 15), (slice, parity) pairs c = (l >> 4) + 4 k
+              // lane l: row 16 i + (l & 15), (slice, k class) pairs c = (l >> 4) + 4 k
 #pragma unroll
-              for (int k = 0; k < 8; ++k) {
+              for (int k = 0; k < NSV; ++k) {
                 const int c = q + 4 * k;
-                sv[k] = c < 2 * splitk ? __hip_atomic_load(st + c * 64 + 16 * i + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : tg;
+                sv[k] = c < NQ2 * splitk ? __hip_atomic_load(st + c * 64 + 16 * i + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : tg;
               }
             }
 #pragma unroll
@@ -406,7 +471,7 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
           if constexpr (NORM)
             if (s0 == 0) {
 #pragma unroll
-              for (int k = 0; k < 8; ++k) ok &= ready(sv[k]);
+              for (int k = 0; k < NSV; ++k) ok &= ready(sv[k]);
             }
           if (__all(ok) || failed) break;
           const long long waited = wall_clock64() - t0;
@@ -431,8 +496,8 @@ __global__ __launch_bounds__(NT) void wide_gemm_kernel(const bf16x8* __restrict_
         if constexpr (NORM)
           if (s0 == 0) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if (q + 4 * k < 2 * splitk) rowss += __uint_as_float((unsigned)sv[k]);
+            for (int k = 0; k < NSV; ++k)
+              if (q + 4 * k < NQ2 * splitk) rowss += __uint_as_float((unsigned)sv[k]);
           }
       }
       WSTAMP(4, wall_clock64());
@@ -489,8 +554,9 @@ static bool gran_ws(int splitk, int n_tiles, hipStream_t st, GranArgs* ga) {
   char* ws = nullptr;  // the fault word lives at the end of the split-K workspace
   if (!pgemm::split_ws(0, st, &ws)) return false;
   GranWs& g = g_gran_ws[splitk];
+  // tickets | row sums of squares [tile][split][<= 4 k classes][64] | partials
   auto bytes_for = [&](int tiles) {
-    return (size_t)tiles * 8 + (size_t)tiles * splitk * 128 * 8 + (size_t)tiles * splitk * 8192 * 8 + 256;
+    return (size_t)tiles * 8 + (size_t)tiles * splitk * 256 * 8 + (size_t)tiles * splitk * 8192 * 8 + 256;
   };
   if (g.tiles < n_tiles) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -508,7 +574,7 @@ static bool gran_ws(int splitk, int n_tiles, hipStream_t st, GranArgs* ga) {
   ga->splitk = splitk;
   ga->ticket = (u64*)base;
   ga->ssg = (u64*)(base + tk);
-  ga->gran = (u64*)(base + tk + (size_t)g.tiles * splitk * 128 * 8);
+  ga->gran = (u64*)(base + tk + (size_t)g.tiles * splitk * 256 * 8);
   int* fw = p2p_split_fault_word_ptr(st);
   ga->err = fw ? fw : (int*)(ws + pgemm::g_split_ws.bytes - sizeof(unsigned));
   ga->align = kstep_align();
@@ -518,29 +584,34 @@ static bool gran_ws(int splitk, int n_tiles, hipStream_t st, GranArgs* ga) {
 template <int MT, int EPI, bool NORM, bool SPLIT, bool RES>
 int launch_v(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles, int up_off,
              void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st,
-             const GranArgs& ga) {
-  hipLaunchKernelGGL((wide_gemm_kernel<MT, EPI, NORM, SPLIT, RES>), dim3(n_tiles * ga.splitk),
-                     dim3(NT), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, n_tiles, up_off,
-                     out, ldo, eps, ea, ga);
+             const GranArgs& ga, int nw) {
+  if (nw == 16)
+    hipLaunchKernelGGL((wide_gemm_kernel<MT, EPI, NORM, SPLIT, RES, 16>), dim3(n_tiles * ga.splitk),
+                       dim3(16 * 64), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, n_tiles,
+                       up_off, out, ldo, eps, ea, ga);
+  else
+    hipLaunchKernelGGL((wide_gemm_kernel<MT, EPI, NORM, SPLIT, RES, 8>), dim3(n_tiles * ga.splitk),
+                       dim3(8 * 64), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, n_tiles,
+                       up_off, out, ldo, eps, ea, ga);
   return (int)hipGetLastError();
 }
 
 template <int MT, int EPI, bool NORM>
 int launch_mt(const void* Wt, const void* X, int ldx, int M, int K, int n_tiles, int up_off,
-              void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st, int splitk) {
+              void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st, int splitk, int nw) {
   const int al = splitk > 1 ? kstep_align() : 1;
   const int S = K / 32, slice_ks = ((S / al + splitk - 1) / splitk) * al;  // the longest slice's k-steps
   const bool res = g_res && (slice_ks + KC - 1) / KC <= res_chunks<MT>();
   if (splitk > 1) {
     GranArgs ga{};
     if (!gran_ws(splitk, n_tiles, st, &ga))  // (no workspace growth while a graph is captured)
-      return launch_mt<MT, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, 1);
-    return res ? launch_v<MT, EPI, NORM, true, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, ga)
-               : launch_v<MT, EPI, NORM, true, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, ga);
+      return launch_mt<MT, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, 1, nw);
+    return res ? launch_v<MT, EPI, NORM, true, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, ga, nw)
+               : launch_v<MT, EPI, NORM, true, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, ga, nw);
   }
   GranArgs none{1, nullptr, nullptr, nullptr, nullptr, 1};
-  return res ? launch_v<MT, EPI, NORM, false, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none)
-             : launch_v<MT, EPI, NORM, false, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none);
+  return res ? launch_v<MT, EPI, NORM, false, true>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none, nw)
+             : launch_v<MT, EPI, NORM, false, false>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, none, nw);
 }
 
 // K slices: the grid must stay <= one block per CU (every slice of a tile resident for the
@@ -571,7 +642,7 @@ static int pick_split(int n_tiles, int nc, int req) {
 
 template <int EPI, bool NORM>
 int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, void* out, int ldo,
-           float eps, const EpiArgs& ea, hipStream_t st, int req_split) {
+           float eps, const EpiArgs& ea, hipStream_t st, int req_split, int nw) {
   const int cols = EPI == EPI_SILU ? 64 : 128;  // output columns per tile
   const int n_out = EPI == EPI_SILU ? N / 2 : N;
   if (M <= 0 || M > 64 || K % (32 * KC) || n_out % cols) return (int)hipErrorInvalidValue;
@@ -579,10 +650,10 @@ int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, void* ou
   const int up_off = EPI == EPI_SILU ? N / 32 : 0;
   const int splitk = pick_split(n_tiles, K / (32 * KC), req_split);
   switch ((M + 15) / 16) {
-    case 1: return launch_mt<1, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, splitk);
-    case 2: return launch_mt<2, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, splitk);
-    case 3: return launch_mt<3, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, splitk);
-    case 4: return launch_mt<4, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, splitk);
+    case 1: return launch_mt<1, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, splitk, nw);
+    case 2: return launch_mt<2, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, splitk, nw);
+    case 3: return launch_mt<3, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, splitk, nw);
+    case 4: return launch_mt<4, EPI, NORM>(Wt, X, ldx, M, K, n_tiles, up_off, out, ldo, eps, ea, st, splitk, nw);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -590,33 +661,35 @@ int launch(const void* Wt, const void* X, int ldx, int M, int K, int N, void* ou
 }  // namespace wide
 
 // Called by skinny_dispatch (skinny_gemm.hip) for launch codes with the WIDE bit; ea_p points
-// at the caller's EpiArgs (one identical definition per translation unit).  req_split: K
-// slices (0 = heuristic).  Dense bf16 weights only (no FP8, no grouped MoE mode).
+// at the caller's EpiArgs (one identical definition per translation unit).  code: bits 0..7
+// the K slices (0 = heuristic), bit 8 set = 16 waves per workgroup (two per column group,
+// ops.gemm.WIDE16), else 8.  Dense bf16 weights only (no FP8, no grouped MoE mode).
 extern "C" int p2p_wide_dispatch(const void* Wt, const void* X, int ldx, int M, int K, int N,
                                  int epi, int norm, void* out, int ldo, float eps, const void* ea_p,
-                                 int req_split, hipStream_t st) {
+                                 int code, hipStream_t st) {
   const EpiArgs& ea = *reinterpret_cast<const EpiArgs*>(ea_p);
   if (ea.wscale || ea.moe_cnt) return (int)hipErrorInvalidValue;
   using namespace wide;
+  const int req_split = code & 0xff, nw = (code >> 8) & 1 ? 16 : 8;
   switch (epi) {
     case EPI_STORE:
-      return norm ? launch<EPI_STORE, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split)
-                  : launch<EPI_STORE, false>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split);
+      return norm ? launch<EPI_STORE, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split, nw)
+                  : launch<EPI_STORE, false>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split, nw);
     case EPI_RESID:
       if (norm) return (int)hipErrorInvalidValue;
-      return launch<EPI_RESID, false>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split);
+      return launch<EPI_RESID, false>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split, nw);
     case EPI_SILU:
       if (!norm) return (int)hipErrorInvalidValue;
-      return launch<EPI_SILU, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split);
+      return launch<EPI_SILU, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split, nw);
     case EPI_F32:
-      return norm ? launch<EPI_F32, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split)
-                  : launch<EPI_F32, false>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split);
+      return norm ? launch<EPI_F32, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split, nw)
+                  : launch<EPI_F32, false>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split, nw);
     case EPI_QKV_ROPE:
       if (!norm) return (int)hipErrorInvalidValue;
-      return launch<EPI_QKV_ROPE, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split);
+      return launch<EPI_QKV_ROPE, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split, nw);
     case EPI_ARGMAX:
       if (!norm) return (int)hipErrorInvalidValue;
-      return launch<EPI_ARGMAX, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split);
+      return launch<EPI_ARGMAX, true>(Wt, X, ldx, M, K, N, out, ldo, eps, ea, st, req_split, nw);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -103,7 +103,8 @@ def _configs(K, M=1, tiled=False, midm=False, wide=False):
     if midm and M > 1 and K % 128 == 0:
         out.append(G.MIDM_FLAG)
     if wide and M > 1:
-        out += [G.WIDE_FLAG, G.WIDE_FLAG | (4 << 8), G.WIDE_FLAG | (8 << 8)]
+        for nw in (0, G.WIDE16):
+            out += [G.WIDE_FLAG | nw, G.WIDE_FLAG | nw | (4 << 8), G.WIDE_FLAG | nw | (8 << 8)]
     # NG=2 at M <= 16 (twice the weight bytes in flight per wave) is supported by the kernel
     # but was never faster at the 8B decode shapes (two bench runs, w1-w8): not tuned
     for ng in ((1,) if M <= 16 else (1, 2)):
@@ -125,7 +126,7 @@ def describe(code: int) -> str:
         return "packed+" + describe(code & ~G.AFRAG_FLAG)
     if code & G.WIDE_FLAG:
         sk = (code >> 8) & 0xff
-        return "wide/s%s" % (sk if sk else "auto")
+        return "wide%s/s%s" % ("16" if code & G.WIDE16 else "", sk if sk else "auto")
     ng = (code >> 16) & 0xff
     return "w%d/U%d%s" % (code & 0xff, (code >> 8) & 0xff, "/NG%d" % ng if ng > 1 else "")
 

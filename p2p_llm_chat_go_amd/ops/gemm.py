@@ -165,6 +165,9 @@ MIDM_FLAG = 1 << 25
 # into VGPRs, split-K over workgroups); bits 8..15 = K slices (0 = heuristic); bf16 dense
 # weights, K % 256 == 0, 1 < M <= 64
 WIDE_FLAG = 1 << 26
+# with WIDE_FLAG: 16 waves per workgroup (two per column group, k-steps split by parity),
+# else 8 -- a weight stream needs 16 waves per CU to reach HBM speed (bench/stream_probe.py)
+WIDE16 = 1 << 16
 # launch-code bit: the skinny kernel's X is fragment-major (pack_frag), not row-major
 AFRAG_FLAG = 1 << 27
 # the persistent GEMV (csrc/experimental/persist_gemv.hip, libp2p_experimental.so): one 4-wave workgroup per CU (x the

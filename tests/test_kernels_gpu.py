@@ -152,19 +152,22 @@ def test_midm_gemm_every_epilogue(M, K):
 @pytest.mark.parametrize("K,split", [(1024, 0), (1024, 1), (1536, 4), (2048, 3), (2048, 8),
                                      (5120, 1), (4096, 5), (4096, 16)])
 @pytest.mark.parametrize("res", [True, False])
-def test_wide_gemm_every_epilogue(M, K, split, res):
+@pytest.mark.parametrize("nw", [8, 16])
+def test_wide_gemm_every_epilogue(M, K, split, res, nw):
     """The wide mid-M kernel (launch-code bit ops.gemm.WIDE_FLAG: 8 waves x 16 columns share
     LDS activation chunks, split-K over workgroups meeting through tagged granules) on every
     epilogue vs fp32 references; 1536 / 4 slices gives slices of one and two chunks, 4096 / 16
     sixteen one-chunk slices (two poll batches).  res:
     the slice's activations resident in LDS where they fit (else, and with res off, the
-    ring); 5120 unsplit never fits (20 chunks)."""
+    ring); 5120 unsplit never fits (20 chunks).  nw 16 (ops.gemm.WIDE16): two waves per
+    column group splitting the k-steps by parity, summed through LDS."""
     from p2p_llm_chat_go_amd.ops import _lib
-    from p2p_llm_chat_go_amd.ops.gemm import WIDE_FLAG
+    from p2p_llm_chat_go_amd.ops.gemm import WIDE16, WIDE_FLAG
 
     _lib.lib().p2p_wide_resident(int(res))
     try:
-        _every_epilogue(M, WIDE_FLAG | (split << 8), 2000 + M + K + split, K=K)
+        _every_epilogue(M, WIDE_FLAG | (split << 8) | (WIDE16 if nw == 16 else 0),
+                        2000 + M + K + split, K=K)
     finally:
         _lib.lib().p2p_wide_resident(1)
     assert ops.tiled_split_fault() == 0
@@ -174,8 +177,9 @@ def test_wide_gemm_split_tags_across_launches():
     """Split-K granule tags (wide_gemm.hip GranArgs): back-to-back launches on the same tiles
     with changing slice counts, row counts and epilogues -- every launch must read only its
     own slices' partials (a stale granule of an earlier launch would change the result), so
-    each repeat is bit-identical to the first launch of its configuration."""
-    from p2p_llm_chat_go_amd.ops.gemm import WIDE_FLAG
+    each repeat is bit-identical to the first launch of its configuration.  8- and 16-wave
+    launches (ops.gemm.WIDE16) alternate on the same granule workspaces."""
+    from p2p_llm_chat_go_amd.ops.gemm import WIDE16, WIDE_FLAG
 
     torch.manual_seed(7)
     K, N = 4096, 1024
@@ -186,8 +190,9 @@ def test_wide_gemm_split_tags_across_launches():
         for split in (2, 5, 8, 16, 5):
             for M, x in xs.items():
                 for epi in (ops.EPI_STORE, ops.EPI_F32):
-                    y = ops.skinny_gemm(W, x, epi, norm=True, waves=WIDE_FLAG | (split << 8))
-                    key = (split, M, epi)
+                    nw = WIDE16 if (rep + split + M) % 2 else 0
+                    y = ops.skinny_gemm(W, x, epi, norm=True, waves=WIDE_FLAG | (split << 8) | nw)
+                    key = (split, M, epi, nw)
                     if key in first:
                         assert torch.equal(y, first[key]), (rep, key)
                     else:
@@ -196,8 +201,8 @@ def test_wide_gemm_split_tags_across_launches():
     assert ops.tiled_split_fault() == 0
     # and the configurations agree with each other (same math, different slice sums)
     for M in xs:
-        a = first[(2, M, ops.EPI_F32)].float()
-        b = first[(16, M, ops.EPI_F32)].float()
+        a = [v for k, v in first.items() if k[:3] == (2, M, ops.EPI_F32)][0].float()
+        b = [v for k, v in first.items() if k[:3] == (16, M, ops.EPI_F32)][0].float()
         assert _rel(a, b) < 1e-3
 
 
