@@ -75,8 +75,10 @@ def main():
                 w = wts[it % copies]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
+                # PROBE_NW=16: the 16-wave form (dispatch code bit 8)
+                code = req | (256 if os.environ.get("PROBE_NW", "8") == "16" else 0)
                 err = L.p2p_wide_stamp_dispatch(w.data_ptr(), x.data_ptr(), K, M, K, N, epi, int(norm),
-                                                out.data_ptr(), n_out, 1e-5, ctypes.addressof(ea), req, st)
+                                                out.data_ptr(), n_out, 1e-5, ctypes.addressof(ea), code, st)
                 e1.record()
                 assert err == 0, err
                 torch.cuda.synchronize()
@@ -111,7 +113,8 @@ def main():
                             ph["epi"].append((r[5] - r[4]) * TICK_US)
                     elif r[5]:
                         ph["epi"].append((r[5] - r[2]) * TICK_US)
-            out_row = {"gemm": name, "hot": hot, "M": M, "N": N, "K": K, "req_split": req, "blocks": nb,
+            out_row = {"gemm": name, "hot": hot, "nw": int(os.environ.get("PROBE_NW", "8")), "M": M,
+                       "N": N, "K": K, "req_split": req, "blocks": nb,
                        "splitk": int(rows[0][:, 7].max()) + 1,
                        "event_us_p50": round(q(ev, 0.5), 2)}
             for k, v in ph.items():

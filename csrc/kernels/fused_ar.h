@@ -17,8 +17,8 @@
 //      of the peers (same grid and column mapping on every rank), never a grid barrier;
 //   3. h[m, cols] += sum over ranks in rank order (fp32, one rounding): the unfused
 //      formula, so the two paths are bit-identical on every rank.
-// seq is the group's call index of this block (counters[block] + 1, never 0); block 0
-// keeps the counters of blocks a narrower call does not launch in step, as the one-shot
+// seq is the call index of this column group (counters[group] + 1, never 0); group 0's
+// block keeps the counters of groups a narrower call does not have in step, as the one-shot
 // kernel does.  A granule left from an earlier call carries an older seq, so it is never
 // taken for this call's.  Slot reuse: a rank writes parity p in call k+2 only after its
 // call-(k+1) kernel saw call-(k+1) granules of every peer, which each peer writes only
@@ -44,6 +44,7 @@ struct FusedArArgs {
   unsigned* counters;         // [FAR_MAX_BLOCKS] private per-block call counters
   int* err;                   // set nonzero when a peer never arrived
   long long spin_ticks;       // spin bound (100 MHz wall clock)
+  int groups;                 // column groups of the call (the launch may have fewer blocks)
 };
 
 // Host-side spin bound shared with the one-shot kernels (p2p_car_set_timeout_ms).
@@ -78,7 +79,9 @@ template <int MT>
 __device__ __forceinline__ void epilogue(const float (&v)[MT][4], int M, int g, int lane,
                                          bf16* __restrict__ h, int ldh, const FusedArArgs& fa) {
   const int r = lane & 15, q = lane >> 4;
-  const int blk = blockIdx.x, nblk = gridDim.x;
+  // per column group: the call's group g is finished by exactly one block (the launch may
+  // walk several groups per block: skinny_gemm_kernel, EPI_AR)
+  const int blk = g, nblk = fa.groups;
   const unsigned seq = fa.counters[blk] + 1;
   const int parity = seq & 1;
   const int failed = __hip_atomic_load(fa.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -139,7 +142,7 @@ __device__ __forceinline__ void epilogue(const float (&v)[MT][4], int M, int g, 
     *hp = bf16_bits(a0) | (bf16_bits(a1) << 16);
   }
   if (lane == 0) fa.counters[blk] = seq;
-  if (blk == 0)  // keep the counters of blocks a narrower call does not launch in step
+  if (blk == 0)  // keep the counters of groups a narrower call does not have in step
     for (int j = nblk + lane; j < FAR_MAX_BLOCKS; j += 64) fa.counters[j] = seq;
 }
 

@@ -33,6 +33,9 @@
 //               block's 16 columns, then one 64-bit atomicMax of
 //               (ordered(value) << 32 | ~index) per row and block (ties -> lowest id).
 // Split-K across the waves of a block (WAVES), reduced through LDS.
+#include <map>
+#include <mutex>
+
 #include "skinny_gemm_impl.h"
 #include "midm_gemm.h"
 
@@ -133,6 +136,8 @@ static int skinny_dispatch(const void* Wt, const void* X, int ldx, int M, int K,
   waves &= 0xff;
   if (waves <= 0) waves = pick_waves(groups, K, mt);
   if (epi == EPI_SILU && mt == 4 && waves > 4) waves = 4;
+  if (waves == 16 && (mt != 1 || ea.wscale || ea.moe_cnt || epi == EPI_SILU))
+    waves = 8;  // 16 waves: batch-1 bf16 projections other than SwiGLU
   EpiArgs ea2 = ea;
   ea2.u = u_req;
   ea2.ng = ng_req;
@@ -213,6 +218,33 @@ P2P_API int p2p_skinny_gemm_qkv_rope(const void* Wt, const void* X, int ldx, int
   return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_QKV_ROPE, 1, nullptr, 0, eps, waves, ea, stream);
 }
 
+// Ranks of a TP group resident on this device (1 on a node with a GPU per rank; the group
+// size for virtual ranks): the fused all-reduce launch holds at most 1 / n of the device's
+// block slots (skinny_gemm_impl.h skinny_gemm_kernel, EPI_AR).
+static int g_far_coresident = 1;
+P2P_API void p2p_far_set_coresident(int n) { g_far_coresident = n >= 1 ? n : 1; }
+
+int far_grid(int groups, const void* kernel, int threads) {
+  static std::map<const void*, int> occ;  // blocks per CU of each instantiation (host side)
+  static std::mutex mu;
+  int per_cu;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = occ.find(kernel);
+    if (it == occ.end()) {
+      int b = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, threads, 0) != hipSuccess || b < 1) b = 1;
+      it = occ.emplace(kernel, b).first;
+    }
+    per_cu = it->second;
+  }
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int cap = std::max(1, per_cu * std::max(cus, 1) / g_far_coresident);
+  return std::min(groups, cap);
+}
+
 // TP row-parallel projection with the all-reduce fused into the epilogue (fused_ar.h):
 //   h[m, :N] += sum over the group's ranks of (X @ W^T)[m, :N]   (bf16 partials, rank order)
 // bases: every rank's fused buffer (p2p_far_buffer_bytes(max_bytes), own at [rank]);
@@ -236,6 +268,7 @@ P2P_API int p2p_skinny_gemm_ar(const void* Wt, const void* X, int ldx, int M, in
   ea.far.counters = counters;
   ea.far.err = err;
   ea.far.spin_ticks = p2p_car_spin_ticks();
+  ea.far.groups = N / 16;
   waves &= ~(WIDE_FLAG | MIDM_FLAG | (1 << 24));  // skinny only
   return skinny_dispatch(Wt, X, ldx, M, K, N, EPI_AR, 0, h, ldh, 0.f, waves, ea, stream);
 }

@@ -34,10 +34,12 @@ __device__ __forceinline__ bf16x8 widen(const u32x4& p, int h) {
   return r;
 }
 
-template <int MT, int WAVES, int EPI, bool NORM, int U, bool MOE = false, int NG = 1, bool F8 = false>
-__global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
+// One block's work: column group(s) g0 = bid * NG.  (A function of its own so the EPI_AR
+// launch can walk several column groups per block, skinny_gemm_kernel below.)
+template <int MT, int WAVES, int EPI, bool NORM, int U, bool MOE, int NG, bool F8>
+__device__ __forceinline__ void skinny_body(
     const bf16x8* __restrict__ Wt, const bf16* __restrict__ X, int ldx, int M, int K,
-    int up_group_offset, void* __restrict__ out, int ldo, float eps, EpiArgs ea) {
+    int up_group_offset, void* __restrict__ out, int ldo, float eps, const EpiArgs& ea, int bid) {
   // NG column groups per block share every A (activation) fragment: at MT > 1 the
   // A loads (MT per k-step) and the NORM sum of squares dominate unless reused.
   constexpr int NB = (EPI == EPI_SILU) ? 2 : 1;
@@ -46,7 +48,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   const int S = (K >> 5) / KP;    // super-steps
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int g0 = blockIdx.x * NG;
+  const int g0 = bid * NG;
   const int s0 = (S * w) / WAVES;
   const int s1 = (S * (w + 1)) / WAVES;
   const int r = lane & 15, q = lane >> 4;
@@ -324,6 +326,30 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
   }
 }
 
+// EPI_AR (TP row-parallel + fused all-reduce): every column group's epilogue waits in place
+// for the same column group of every peer rank, so all ranks' blocks of a call must be able
+// to be resident at once.  On its own device a rank's grid always is; ranks sharing a device
+// (virtual-rank tests) are not, and in round 5 a TP=4 engine on one device deadlocked until the
+// spin bound (4 ranks x 256 blocks x 8 waves > the device's 4096 wave slots at 128 VGPRs).  So
+// the launch is capped to the blocks the device holds for its share of co-resident ranks
+// (p2p_far_set_coresident) and each block walks column groups gb, gb + grid, ...: no block
+// ever waits on one that cannot be scheduled.
+template <int MT, int WAVES, int EPI, bool NORM, int U, bool MOE = false, int NG = 1, bool F8 = false>
+__global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
+    const bf16x8* __restrict__ Wt, const bf16* __restrict__ X, int ldx, int M, int K,
+    int up_group_offset, void* __restrict__ out, int ldo, float eps, EpiArgs ea) {
+  if constexpr (EPI == EPI_AR) {
+    for (int gb = blockIdx.x; gb < ea.far.groups; gb += gridDim.x) {
+      skinny_body<MT, WAVES, EPI, NORM, U, MOE, NG, F8>(Wt, X, ldx, M, K, up_group_offset, out,
+                                                        ldo, eps, ea, gb);
+      __syncthreads();  // the split-K reduction buffer is reused by the next group
+    }
+  } else {
+    skinny_body<MT, WAVES, EPI, NORM, U, MOE, NG, F8>(Wt, X, ldx, M, K, up_group_offset, out, ldo,
+                                                      eps, ea, blockIdx.x);
+  }
+}
+
 // k-steps per pipeline batch for MT=1: ONE setting for every instantiation unit (defined in
 // skinny_gemm.hip, set by p2p_skinny_gemm_tune)
 }  // namespace
@@ -334,6 +360,12 @@ template <int MT, int WAVES, int EPI, bool NORM, int U>
 int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
                void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st);
 
+}  // namespace
+// Blocks of the EPI_AR launch: the column groups, capped to what the device holds for its
+// share of the ranks resident on it (skinny_gemm.hip, p2p_far_set_coresident).
+int far_grid(int groups, const void* kernel, int threads);
+namespace {
+
 template <int MT, int WAVES, int EPI, bool NORM>
 int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
               void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
@@ -343,6 +375,7 @@ int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, 
   // FP8 holds KP = 2 A fragments per weight load: the deep batch spills to scratch at
   // 8 waves (<= 128 VGPRs) and at MT = 4, so those take the shallow one.
   if (ea.wscale && (WAVES == 8 || MT == 4)) u = MT == 1 ? 4 : 2;
+  if (WAVES == 16) u = 4;
   if constexpr (MT == 1) {
     if (u == 8)
       return launch_mwu<MT, WAVES, EPI, NORM, 8>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
@@ -357,9 +390,29 @@ int launch_mw(const void* Wt, const void* X, int ldx, int M, int K, int groups, 
 template <int MT, int WAVES, int EPI, bool NORM, int U>
 int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups, int up_off,
                void* out, int ldo, float eps, const EpiArgs& ea, hipStream_t st) {
+  if constexpr (WAVES == 16) {
+    // 16 waves (batch 1, bf16, one column group per block, 4-deep batches: <= 128 VGPRs with
+    // no scratch; not SwiGLU, whose two weight streams per wave spill): a weight stream
+    // reaches HBM speed only with ~16 waves per CU (bench/stream_probe.py,
+    // profiles/r6_stream_probe.md), and the N = 4096 row-parallel projections have just 256
+    // column groups, one per CU
+    if constexpr (MT != 1 || U != 4 || EPI == EPI_SILU) {
+      return (int)hipErrorInvalidValue;
+    } else {
+      if (ea.wscale || ea.moe_cnt) return (int)hipErrorInvalidValue;
+      int grid = groups;
+      if constexpr (EPI == EPI_AR) grid = far_grid(groups, (const void*)skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>, WAVES * 64);
+      hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>), dim3(grid), dim3(WAVES * 64), 0,
+                         st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, up_off, out, ldo, eps, ea);
+      return (int)hipGetLastError();
+    }
+  } else {
   if (ea.wscale) {  // FP8 weights (dense projections, one column group per block)
     if (ea.moe_cnt || (K % 64) != 0) return (int)hipErrorInvalidValue;  // k-step pairs
-    hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, false, 1, true>), dim3(groups),
+    int grid = groups;
+    if constexpr (EPI == EPI_AR)
+      grid = far_grid(groups, (const void*)skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, false, 1, true>, WAVES * 64);
+    hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U, false, 1, true>), dim3(grid),
                        dim3(WAVES * 64), 0, st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K,
                        up_off, out, ldo, eps, ea);
     return (int)hipGetLastError();
@@ -389,9 +442,12 @@ int launch_mwu(const void* Wt, const void* X, int ldx, int M, int K, int groups,
       }
     }
   }
-  hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>), dim3(groups), dim3(WAVES * 64), 0,
+  int grid = groups;
+  if constexpr (EPI == EPI_AR) grid = far_grid(groups, (const void*)skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>, WAVES * 64);
+  hipLaunchKernelGGL((skinny_gemm_kernel<MT, WAVES, EPI, NORM, U>), dim3(grid), dim3(WAVES * 64), 0,
                      st, (const bf16x8*)Wt, (const bf16*)X, ldx, M, K, up_off, out, ldo, eps, ea);
   return (int)hipGetLastError();
+  }  // WAVES != 16
 }
 
 template <int MT, int EPI, bool NORM>
@@ -402,6 +458,10 @@ int launch_m(int waves, const void* Wt, const void* X, int ldx, int M, int K, in
     case 2: return launch_mw<MT, 2, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
     case 4: return launch_mw<MT, 4, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
     case 8: return launch_mw<MT, 8, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+    case 16:
+      if constexpr (MT == 1)
+        return launch_mw<MT, 16, EPI, NORM>(Wt, X, ldx, M, K, groups, up_off, out, ldo, eps, ea, st);
+      break;
   }
   return (int)hipErrorInvalidValue;
 }

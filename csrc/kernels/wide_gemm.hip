@@ -106,8 +106,11 @@ __global__ __launch_bounds__(NW * 64) void wide_gemm_kernel(const bf16x8* __rest
   constexpr int NQ = NW / 4;     // NORM: k-step classes (mod NQ) x 4 m-tiles = NW waves
   constexpr int NQ2 = 2;         // classes left after the pair exchange (NW = 16: 2 + 2 -> 2)
   // pipeline depth: D chunks ahead (RS = D + 1 register sets of KW weight fragments: 128
-  // VGPRs at NW = 8, D = 3; 48 at NW = 16, D = 2), activation ring of D + 2 slots (<= 128 KiB)
-  constexpr int D = NW == 16 ? (MT >= 4 ? 1 : 2) : (MT >= 4 ? 2 : 3);
+  // VGPRs at NW = 8, D = 3; 32 at NW = 16, D = 1), activation ring of D + 2 slots (<= 128 KiB).
+  // NW = 16 keeps ONE chunk (4 KiB per wave, 64 KiB per CU) ahead: the stream probe's best
+  // in-flight depth at 16 waves per CU (deeper queues let every chunk of every CU arrive at
+  // once, late, and the MFMAs start only then: r5 stamps, 6-10 us to the first chunk)
+  constexpr int D = NW == 16 ? 1 : (MT >= 4 ? 2 : 3);
   constexpr int RS = D + 1;
   constexpr int RING = D + 2;
   constexpr int SLOT = MT * KC * 64;  // bf16x8 per ring slot

@@ -112,6 +112,10 @@ def _configs(K, M=1, tiled=False, midm=False, wide=False):
             for w in (1, 2, 4, 8):
                 if (K // 32) // w >= 8 and not (ng > 1 and w == 8):
                     out.append(w | (u << 8) | ((ng if ng > 1 else 0) << 16))
+    if M <= 16 and (K // 32) // 16 >= 8:
+        # 16 waves per block (bf16, not SwiGLU: the kernel falls back to 8 there), 4-deep
+        # batches: the stream probe's 16 waves per CU at the 256-column-group projections
+        out.append(16 | (4 << 8))
     return out
 
 

@@ -85,6 +85,25 @@ def peer_access_failures(group=None, device=None, can_access=None) -> list:
     return [f for fs in every for f in fs]
 
 
+def coresident_ranks(group=None, device=None) -> int:
+    """How many ranks of ``group`` (this one included) run on this rank's device: same host
+    and the same device ordinal or PCI bus id (virtual ranks share one)."""
+    import socket
+
+    world = dist.get_world_size(group)
+    dev = torch.device(device) if device is not None else torch.device(
+        "cuda", torch.cuda.current_device())
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    try:
+        bus = torch.cuda.get_device_properties(idx).pci_bus_id
+    except Exception:  # noqa: BLE001
+        bus = None
+    me = (socket.gethostname(), idx, bus)
+    info = [None] * world
+    dist.all_gather_object(info, me, group=group)
+    return sum(1 for h, i, b in info if h == me[0] and (i == idx or (bus is not None and b == bus)))
+
+
 def describe_failures(fails) -> str:
     return "; ".join("rank %d (device %d) -> rank %d (device %d): %s" % f for f in fails)
 
@@ -124,6 +143,11 @@ class CustomAllReduce:
             self.far_counters = torch.zeros(1024, dtype=torch.int32, device=self.device)
             self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         torch.cuda.synchronize(self.device)
+        # ranks of this group on THIS device (virtual ranks: all of them; a node with one GPU
+        # per rank: 1): the fused all-reduce launch keeps to its share of the device's block
+        # slots, so every rank's grid fits at once (csrc/kernels/skinny_gemm_impl.h EPI_AR)
+        self.coresident = coresident_ranks(self.group, self.device)
+        L.p2p_far_set_coresident(self.coresident)
         dist.barrier(group=self.group)
 
     def _map(self, size):

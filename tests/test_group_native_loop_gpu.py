@@ -36,9 +36,9 @@ def _req(i, sampled=False, n=24):
 def _serve(world, native, reqs):
     env = {"ENGINE_NATIVE_LOOP": "1" if native else "0", "P2P_CAR_TIMEOUT_MS": "30000",
            "P2P_QA_TIMEOUT_MS": "30000",
-           # 8 virtual ranks share one device's wave slots: the unfused all-reduce pair
-           # (tests/test_world8_gpu.py explains the fused epilogue's residency limit there)
-           "P2P_TP_FUSED_AR": "0" if world >= 8 else os.environ.get("P2P_TP_FUSED_AR", "1")}
+           # the fused all-reduce epilogue at every width: its launch keeps to the ranks'
+           # share of the one device (tests/test_world8_gpu.py explains the residency limit)
+           "P2P_TP_FUSED_AR": os.environ.get("P2P_TP_FUSED_AR", "1")}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:

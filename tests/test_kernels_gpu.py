@@ -51,6 +51,15 @@ def test_skinny_gemm_waves_and_f32(waves):
     assert _rel(out.cpu(), ref) < 5e-3
 
 
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("K", [1024, 4096])
+def test_skinny_gemm_16_waves_every_epilogue(M, K):
+    """The 16-wave skinny launch (batch <= 16, 4-deep batches; the SwiGLU epilogue falls back
+    to 8 waves) on every epilogue vs fp32 references (K 1024: two k-steps per wave, the
+    pipeline's tail path only)."""
+    _every_epilogue(M, 16 | (4 << 8), 3000 + M + K, K=K)
+
+
 @pytest.mark.parametrize("M", [1, 7, 40])
 def test_skinny_gemm_resid(M):
     torch.manual_seed(M)

@@ -60,8 +60,10 @@ def _worker(rank, world, port, q, kind, mode, env):
     # 8 processes time-share one device: a rank's kernel can wait on a peer whose queue is
     # not scheduled yet, so the spin bounds (all-reduce, fused qkv+attention hand-off) are
     # generous here (5 s on real GPUs)
+    # (the wide GEMM's K slices also meet inside one launch: capped to one slice, as the
+    # cluster does for virtual ranks, engine/cluster.py)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), P2P_CAR_TIMEOUT_MS="30000",
-                      P2P_QA_TIMEOUT_MS="30000", **env)
+                      P2P_QA_TIMEOUT_MS="30000", P2P_WIDE_SPLIT_CAP="1", **env)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     WORLD = world
     try:
@@ -146,21 +148,19 @@ def _worker(rank, world, port, q, kind, mode, env):
         dist.destroy_process_group()
 
 
-# The unfused all-reduce pair at TP=8 and TP=4.  The fused GEMM's workgroups wait in place
-# for the same workgroup of every peer: on 8 GPUs each device runs only its own grid and
-# in-order dispatch guarantees progress, but virtual ranks on ONE device share its wave slots
-# and LDS, so ranks whose grids are already spinning can keep a late rank's earlier kernels
-# from being scheduled at all (a deadlock until the spin bound).  At 8 ranks that held only
-# when the ranks happened to run in step (round 4: 5 of 5 timeouts on fresh boxes); at 4
-# ranks, with the split-K waves capped and whole-group qkv producers, it held through round
-# 4 and stalled on 5 of 6 runs in round 5 (2-key-wave consumers and unsplit wide GEMMs did
-# not change that), with no kernel of the path changed.  So the fused epilogue is covered
-# bit-exactly by test_fused_ar_gpu.py (world 8, one launch per rank in lockstep) and inside
-# an engine by test_group_native_loop_gpu.py (TP 2 and 4, virtual ranks, replies equal to
-# the Python lockstep loop); here both engine widths run the unfused pair.
+# TP=4 and TP=8 run the fused all-reduce epilogue (ops.skinny_gemm_ar).  Its workgroups wait
+# in place for the same column group of every peer, so every rank's grid must be able to be
+# resident at once: true on a node with a GPU per rank, not for virtual ranks sharing ONE
+# device's wave slots -- round 5's TP=4 case deadlocked there until the spin bound on 5 of 6
+# runs (4 ranks x 256 workgroups x 8 waves > the 4096 wave slots at 128 VGPRs).  Since round 6
+# each rank's fused launch holds at most 1/n of the device's block slots for the n ranks
+# resident on it (CustomAllReduce.coresident -> p2p_far_set_coresident) and walks the column
+# groups in a grid-stride loop, so no workgroup waits on one that cannot be scheduled.  The
+# unfused pair keeps a case of its own.
 @pytest.mark.parametrize("kind,mode,world,env", [
+    ("dense", "tp", 8, {}),
+    ("dense", "tp", 4, {}),
     ("dense", "tp", 8, {"P2P_TP_FUSED_AR": "0"}),
-    ("dense", "tp", 4, {"P2P_TP_FUSED_AR": "0"}),
     ("moe", "allreduce", 8, {}), ("moe", "a2a", 8, {})])
 def test_world8_virtual_ranks_full_width(kind, mode, world, env):
     ctx = mp.get_context("spawn")
