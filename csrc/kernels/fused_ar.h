@@ -122,7 +122,7 @@ __device__ __forceinline__ void epilogue(const float (&v)[MT][4], int M, int g, 
       for (int p = 0; p < FAR_MAX_RANKS; ++p) ok &= (unsigned)(x[p] >> 32) == seq;
       if (ok || failed) break;
       if (wall_clock64() - t0 > fa.spin_ticks) {
-        atomicOr(fa.err, 1);
+        atomicOr(fa.err, 2);  // bit 1: a fused epilogue timed out (one-shot kernels set bit 0)
         break;
       }
       __builtin_amdgcn_s_sleep(1);

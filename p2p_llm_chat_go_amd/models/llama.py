@@ -318,12 +318,17 @@ class LlamaModel:
             # one-shot wait timed out does not leave its peers blocked in this collective
             fault = self.comm.max_int(fault)
         if fault & 4:
-            if local_timeout is not None:
-                raise local_timeout
             from ..parallel.custom_ar import CollectiveTimeout
 
+            # name every wait that timed out in the group: a stuck in-launch hand-off or
+            # split-K slice on one rank starves the others' collectives
+            also = "".join(s for bit, s in ((1, "; an in-launch hand-off also timed out"),
+                                            (2, "; a split-K slice wait also timed out"))
+                           if fault & bit)
+            if local_timeout is not None:
+                raise CollectiveTimeout(str(local_timeout) + also) from local_timeout
             raise CollectiveTimeout("a one-shot collective timed out on a peer rank of the "
-                                    "group (the TP group is broken)")
+                                    "group (the TP group is broken)" + also)
         if fault & 1:
             raise RuntimeError("fused in-launch hand-off (qkv -> attention, attention -> "
                                "o_proj) timed out on a rank of the group (results invalid)")

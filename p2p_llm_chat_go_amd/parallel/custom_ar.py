@@ -230,9 +230,11 @@ class CustomAllReduce:
 
     def check(self):
         """Raise if any call timed out waiting for a peer (numbers would be wrong)."""
-        if int(self.err.item()) != 0:
-            raise CollectiveTimeout("custom all-reduce: a peer never arrived (timeout); "
-                                    "the TP group is broken")
+        e = int(self.err.item())
+        if e != 0:
+            where = {1: "one-shot kernel", 2: "fused GEMM epilogue"}.get(e, "one-shot + fused")
+            raise CollectiveTimeout("custom all-reduce: a peer never arrived (timeout in the %s); "
+                                    "the TP group is broken" % where)
 
     def fused_ok(self, M: int, N: int, ld: int) -> bool:
         """Can ops.skinny_gemm_ar sum an [M, N] partial (row stride ld) through the fused
