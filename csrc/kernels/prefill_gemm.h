@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "gemm_epilogue.h"
+#include "lds_pipe.h"
 
 // The split-K fault word of the current device (tiled_gemm.hip): one int per device,
 // allocated with the first split-K workspace and never moved, so a captured graph, the
@@ -178,16 +179,14 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
     bsrc[i] = Wt + ((size_t)group_of(blk >> 1) * S + (blk & 1)) * 64 + lane;
   }
 
+  // asm DMA + asm LDS reads (lds_pipe.h): with the builtins the compiler put vmcnt(0)
+  // before every stage read, draining the STAGES-deep pipeline at every k-tile
   auto issue = [&](int kt, int st) {
     bf16x8* base = lds + st * STAGE;
 #pragma unroll
-    for (int i = 0; i < AI; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + kt * BK),
-                                       (lds_ptr_t)(base + (w + 8 * i) * 64), 16, 0, 0);
+    for (int i = 0; i < AI; ++i) ldsp::dma_lds<16>(asrc[i] + kt * BK, base + (w + 8 * i) * 64);
 #pragma unroll
-    for (int i = 0; i < BI; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (size_t)kt * 2 * 64),
-                                       (lds_ptr_t)(base + (AB + w + 8 * i) * 64), 16, 0, 0);
+    for (int i = 0; i < BI; ++i) ldsp::dma_lds<16>(bsrc[i] + (size_t)kt * 2 * 64, base + (AB + w + 8 * i) * 64);
   };
 
   int bgi[FN];
@@ -226,9 +225,10 @@ __global__ __launch_bounds__(NT) void prefill_gemm_kernel(const bf16x8* __restri
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = sb[(bgi[j] * 2 + ks) * 64 + lane];
+      for (int j = 0; j < FN; ++j) bfr[j] = ldsp::lds_rd(sb + (bgi[j] * 2 + ks) * 64 + lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = sa[((wm * FM + i) * 2 + ks) * 64 + lane];
+      for (int i = 0; i < FM; ++i) af[i] = ldsp::lds_rd(sa + ((wm * FM + i) * 2 + ks) * 64 + lane);
+      ldsp::lds_wait(af, bfr);
       // keep the MFMA cluster together against the co-resident wave (guide T5)
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll

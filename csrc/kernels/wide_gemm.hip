@@ -80,6 +80,57 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// LDS reads of the k loop as inline asm.  The activations reach LDS by DMA
+// (global_load_lds), and the compiler cannot tell which ring slot a pending DMA writes: it
+// put an s_waitcnt vmcnt(0) before every ds_read of the ring, so each chunk's compute waited
+// for ALL loads in flight (the next D chunks' weights and activations too) and the pipeline
+// drained at every chunk (r6 disassembly; gate_up 16 x 2.8 us per chunk on the ring path).
+// The kernel's own counted vmcnt wait + barrier already makes chunk t's slot complete, so
+// the reads go out as asm (the compiler inserts no wait for them) and lds_wait holds their
+// results until they land.
+__device__ __forceinline__ unsigned lds_off(const void* p) { return (unsigned)(uintptr_t)(lds_ptr_t)p; }
+__device__ __forceinline__ bf16x8 lds_rd(const bf16x8* p) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_off(p)));
+  return v;
+}
+// The LDS DMA itself goes out as asm too: with the builtin's DMA events pending, the
+// compiler's own vmcnt tracking of the weight loads gave up (mixed event kinds on one
+// counter) and put vmcnt(0) before every MFMA of the ring path, draining the pipeline just the
+// same.  M0 = the wave's LDS destination; lane i's BYTES land at M0 + i * BYTES.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+template <int BYTES>
+__device__ __forceinline__ void dma_lds(const void* g, const void* l) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_off(l));
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0)
+                 : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m0)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+// The weight stream as asm as well: the compiler does not count the asm DMAs, so its own
+// waits for the weight registers came out AD x D loads short -- each MFMA waited for part of
+// the NEXT chunk.  With every k-loop load and LDS read in asm, the kernel's counted
+// wait_chunks + barrier + lds_wait are the only waits (an MFMA needs its A fragments from
+// lds_wait, which follows the chunk's wait, so it never runs on a weight still in flight).
+__device__ __forceinline__ bf16x8 gload_nt(const bf16x8* p) {
+  bf16x8 v;
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(bf16x8 (&a)[N]) {
+  static_assert(N >= 1 && N <= 4, "lds_wait: 1-4 fragments");
+  if constexpr (N == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]));
+  if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]));
+  if constexpr (N == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]));
+  if constexpr (N == 4)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
+}
+
 // chunks of a K slice whose activations fit LDS at once (the RES variant): <= 144 KiB
 template <int MT>
 constexpr int res_chunks() { return 18 / MT; }
@@ -154,24 +205,32 @@ __global__ __launch_bounds__(NW * 64) void wide_gemm_kernel(const bf16x8* __rest
     asrc[i] = X + (size_t)row * ldx + 8 * (lane >> 4);
   }
 
-  // chunk c's activations: wave w loads k-step w & 7 of the m-tiles of its parity (NW = 16:
-  // the odd wave of a pair repeats its last m-tile when MT is odd, so every wave issues AD
-  // instructions -- the same bytes to the same LDS place -- and the counted waits hold)
+  // Chunk c's loads.  Past the slice (c >= n: the last D steps) the same instructions go out
+  // on hot addresses -- the slice's last activation chunk into ring slot c % NSLOT, which no
+  // later step reads, and the activations' first fragment row for the weights -- so every
+  // step issues and waits alike.  The addresses are selected, not branched on: a branch
+  // made the compiler merge the in-flight register sets and copy them (a vmcnt(0) before
+  // each copy), which drained the pipeline at every chunk.
+  // Activations: wave w loads k-step w & 7 of the m-tiles of its parity (NW = 16: the odd
+  // wave of a pair repeats its last m-tile when MT is odd, so every wave issues AD
+  // instructions -- the same bytes to the same LDS place -- and the counted waits hold).
   auto issue_a = [&](int c) {
     bf16x8* base = ring + (c % NSLOT) * SLOT;
-    const int kk = ks0 + c * KC + min(wg, kv_of(c) - 1);
+    const int cc = min(c, n - 1);
+    const int kk = ks0 + cc * KC + min(wg, kv_of(cc) - 1);
 #pragma unroll
     for (int a = 0; a < AD; ++a) {
       const int i = min(par + NPAR * a, MT - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (size_t)kk * 32),
-                                       (lds_ptr_t)(base + (i * KC + wg) * 64), 16, 0, 0);
+      dma_lds<16>(asrc[i] + (size_t)kk * 32, base + (i * KC + wg) * 64);
     }
   };
+  const bf16x8* whot = reinterpret_cast<const bf16x8*>(X) + lane;
   auto issue_w = [&](int c, bf16x8(&wr)[KW]) {
     const int kb = ks0 + c * KC, kl = kv_of(c) - 1;
+    const bool real = c < n;
 #pragma unroll
     for (int j = 0; j < KW; ++j)
-      wr[j] = __builtin_nontemporal_load(wsrc + (size_t)(kb + min(par + NPAR * j, kl)) * 64);
+      wr[j] = gload_nt(real ? wsrc + (size_t)(kb + min(par + NPAR * j, kl)) * 64 : whot);
   };
   auto issue = [&](int c, bf16x8(&wr)[KW]) {
     if constexpr (!RES) issue_a(c);
@@ -222,8 +281,8 @@ __global__ __launch_bounds__(NW * 64) void wide_gemm_kernel(const bf16x8* __rest
   if constexpr (EPI == EPI_QKV_ROPE)
     if (w == 0) {
       const int mm = min(lane, M - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(ea.slots + mm), (lds_ptr_t)slot_l, 4, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(ea.pos + mm), (lds_ptr_t)pos_l, 4, 0, 0);
+      dma_lds<4>(ea.slots + mm, slot_l);
+      dma_lds<4>(ea.pos + mm, pos_l);
     }
 
   f32x4 acc[MT];
@@ -238,19 +297,33 @@ __global__ __launch_bounds__(NW * 64) void wide_gemm_kernel(const bf16x8* __rest
     for (int j = 0; j < KW; ++j) {
       const int k = par + NPAR * j;
       if (!FULL && k >= kv) break;
-      bf16x8 a[MT];
+      // A fragments in flight together: every m-tile's (one at a time for MT = 4 at NW = 16)
+      constexpr int AB = (NW == 16 && MT == 4) ? 1 : MT;
 #pragma unroll
-      for (int i = 0; i < MT; ++i) a[i] = base[(i * KC + k) * 64 + lane];
+      for (int i0 = 0; i0 < MT; i0 += AB) {
+        bf16x8 a[AB];
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], wr[j], acc[i], 0, 0, 0);
+        for (int i = 0; i < AB; ++i) a[i] = lds_rd(base + ((i0 + i) * KC + k) * 64 + lane);
+        lds_wait(a);
+#pragma unroll
+        for (int i = 0; i < AB; ++i)
+          acc[i0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], wr[j], acc[i0 + i], 0, 0, 0);
+      }
     }
     if constexpr (NORM) {
       if (sq_mt < MT) {
+        // reads in flight together: all of the chunk's at NW = 8, one at NW = 16 (128 VGPRs)
+        constexpr int NS = KC / NQ, NB = NW == 16 ? 1 : NS;
 #pragma unroll
-        for (int k = 0; k < KC; k += NQ) {
-          if (!FULL && k + sq_q >= kv) break;
-          ss = sumsq8(base[(sq_mt * KC + k + sq_q) * 64 + lane], ss);
+        for (int u0 = 0; u0 < NS; u0 += NB) {
+          bf16x8 x[NB];
+#pragma unroll
+          for (int u = 0; u < NB; ++u)  // a partial chunk reads a stale k-step, not summed
+            x[u] = lds_rd(base + (sq_mt * KC + (u0 + u) * NQ + sq_q) * 64 + lane);
+          lds_wait(x);
+#pragma unroll
+          for (int u = 0; u < NB; ++u)
+            if (FULL || (u0 + u) * NQ + sq_q < kv) ss = sumsq8(x[u], ss);
         }
       }
     }
@@ -271,24 +344,25 @@ __global__ __launch_bounds__(NW * 64) void wide_gemm_kernel(const bf16x8* __rest
   if constexpr (RES)  // the whole slice's activations first (host: n <= res_chunks)
     for (int c = 0; c < n; ++c) issue_a(c);
 #pragma unroll
-  for (int j = 0; j < D; ++j)
-    if (j < n) issue(j, wr[j]);
+  for (int j = 0; j < D; ++j) issue(j, wr[j]);
   for (int tb = 0; tb < n; tb += RS) {
 #pragma unroll
     for (int j = 0; j < RS; ++j) {
       const int t = tb + j;
-      if (t >= n) break;
-      if (t + D < n) issue(t + D, wr[(j + D) % RS]);
-      wait_chunks(min(D, n - 1 - t));
-      if (!RES || t == 0) {  // RES: chunk 0's weights landed => this wave's DMA parts too
-        if (SPLIT && t == 0 && tid == 0) tag_l = (unsigned)(tkt / (u64)splitk) + 1u;  // landed (oldest load)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (t == 0) WSTAMP(1, wall_clock64());
+      issue(t + D, wr[(j + D) % RS]);
+      if (t < n) {
+        wait_chunks(D);  // exactly D chunks went out after chunk t
+        if (!RES || t == 0) {  // RES: chunk 0's weights landed => this wave's DMA parts too
+          if (SPLIT && t == 0 && tid == 0) tag_l = (unsigned)(tkt / (u64)splitk) + 1u;  // landed (oldest load)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          if (t == 0) WSTAMP(1, wall_clock64());
+        }
+        compute(t, wr[j]);
       }
-      compute(t, wr[j]);
     }
   }
+  wait_vmcnt<0>();  // the tail's DMAs land before the ring is reused below
 
   WSTAMP(2, wall_clock64());
   // ---- this wave's row sums of squares: the NQ waves w = sq_mt + 4 x hold m-tile sq_mt ----

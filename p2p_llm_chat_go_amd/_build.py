@@ -92,6 +92,32 @@ def _headers(d):
 EXPERIMENTAL_LIB = os.path.join(LIBDIR, "libp2p_experimental.so")
 
 
+# Kernels whose k loop streams through inline-asm loads (csrc/kernels/wide_gemm.hip): the
+# compiler does not know those registers are still in flight, so a spill of one would read
+# it before it lands.  Their translation units must compile with zero scratch.
+NO_SCRATCH = {"wide_gemm.hip", "tiled_gemm.hip"}
+
+
+def check_no_scratch(src, remarks: str, obj=None):
+    """Raise if any kernel of ``src`` uses scratch (the -Rpass-analysis=kernel-resource-usage
+    remarks of its compile)."""
+    import re
+
+    bad, name = [], None
+    for line in remarks.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+        m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+        if m and int(m.group(1)) > 0:
+            bad.append("%s (%s B/lane)" % (name, m.group(1)))
+    if bad:
+        if obj and os.path.exists(obj):
+            os.remove(obj)
+        raise RuntimeError("%s: kernels with scratch (asm-pipelined loads must not spill): %s"
+                           % (os.path.basename(src), "; ".join(bad)))
+
+
 def build_kernels(force=False, jobs=8, experimental=False):
     """Compile csrc/kernels/*.hip for gfx950 into one shared library (C ABI, ctypes).
 
@@ -114,8 +140,15 @@ def build_kernels(force=False, jobs=8, experimental=False):
         objs.append(o)
         if force or _stale(o, [s] + hdrs):
             todo.append((s, o))
+    def compile_one(s, o):
+        if os.path.basename(s) not in NO_SCRATCH:
+            return _run([HIPCC] + flags + ["-c", s, "-o", o])
+        out = _run([HIPCC] + flags + ["-Rpass-analysis=kernel-resource-usage", "-c", s, "-o", o])
+        check_no_scratch(s, out, o)
+        return out
+
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        futs = [ex.submit(_run, [HIPCC] + flags + ["-c", s, "-o", o]) for s, o in todo]
+        futs = [ex.submit(compile_one, s, o) for s, o in todo]
         for f in futs:
             f.result()
     # a source removed from the directory leaves its object behind: relink from the

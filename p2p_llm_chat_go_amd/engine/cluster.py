@@ -513,6 +513,7 @@ class ClusterServer:
         self.model_name = model_name
         self.max_tokens = max_tokens
         self.tokenizer_path = tokenizer or checkpoint
+        self._front_tok = None
         spec = dict(model=model, tp=tp, ep=ep, max_batch=max_batch, max_tokens=max_tokens,
                     model_name=model_name, weights=weights, tokenizer=tokenizer, sd_seed=sd_seed,
                     kv_pages=kv_pages, warmup=warmup, world=gpus, checkpoint=checkpoint or None,
@@ -687,22 +688,43 @@ class ClusterServer:
             return None
         import json as _json
 
-        from .tokenizer import get_tokenizer
-
-        if self.tokenizer_path and os.path.isdir(self.tokenizer_path) \
-                and os.path.exists(os.path.join(self.tokenizer_path, "config.json")):
-            from ..models.weights import config_from_hf
-
-            cfg = config_from_hf(self.tokenizer_path)
-        else:
-            from ..models.config import get_config
-
-            cfg = get_config(self.model)
-        tok = get_tokenizer(cfg, self.tokenizer_path)
+        tok = self._tokenizer()
         return {"cluster": [r.socket for r in self._replicas], "model": self.model_name,
                 "default_max_tokens": int(self.max_tokens),
                 "timeout_s": float(os.environ.get("ENGINE_TIMEOUT", "60")),
                 "tokenizer": _json.dumps(tok.native_spec())}
+
+    def _tokenizer(self):
+        """The tokenizer a replica leader uses (built once, in this process)."""
+        if self._front_tok is None:
+            from .tokenizer import get_tokenizer
+
+            if self.tokenizer_path and os.path.isdir(self.tokenizer_path) \
+                    and os.path.exists(os.path.join(self.tokenizer_path, "config.json")):
+                from ..models.weights import config_from_hf
+
+                cfg = config_from_hf(self.tokenizer_path)
+            else:
+                from ..models.config import get_config
+
+                cfg = get_config(self.model)
+            self._front_tok = get_tokenizer(cfg, self.tokenizer_path)
+        return self._front_tok
+
+    def encode_request(self, req_text: str) -> list:
+        """Prompt ids of an Ollama request: the C ABI's fallback tokenisation on the
+        native_front path (non-ASCII text with the synthetic tokenizer), the same as a
+        replica leader's (native_loop.NativeLoopServer.encode_request)."""
+        tok = self._tokenizer()
+        req = json.loads(req_text)
+        if req.get("endpoint") == "chat":
+            return tok.chat_messages_ids(req.get("messages") or [])
+        if req.get("raw"):
+            return tok.encode(req.get("prompt", ""), bos=True)
+        return tok.chat_ids(req.get("prompt", ""))
+
+    def decode_ids(self, ids) -> str:
+        return self._tokenizer().decode(list(ids))
 
     def handle_json(self, req_text: str) -> str:
         req = json.loads(req_text)

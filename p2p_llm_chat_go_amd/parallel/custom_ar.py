@@ -233,6 +233,10 @@ class CustomAllReduce:
         e = int(self.err.item())
         if e != 0:
             where = {1: "one-shot kernel", 2: "fused GEMM epilogue"}.get(e, "one-shot + fused")
+            if e & 2:  # each column group's call count: where this rank's sequence stopped
+                c = self.far_counters[:256].cpu()
+                where += " (rank %d, coresident %d: fused call counts over column groups min %d max %d)" % (
+                    self.rank, self.coresident, int(c.min()), int(c.max()))
             raise CollectiveTimeout("custom all-reduce: a peer never arrived (timeout in the %s); "
                                     "the TP group is broken" % where)
 

@@ -50,12 +50,12 @@ class Procs:
     def __init__(self):
         self.procs = []
 
-    def spawn(self, name, env=None, args=None, stdout=None):
+    def spawn(self, name, env=None, args=None, stdout=None, stderr=None):
         e = dict(os.environ)
         e.update(env or {})
         cmd = [os.path.join(BIN, name)] if args is None else args
         p = subprocess.Popen(cmd, env=e, stdout=stdout or subprocess.DEVNULL,
-                             stderr=subprocess.DEVNULL)
+                             stderr=stderr or subprocess.DEVNULL)
         self.procs.append(p)
         return p
 

@@ -498,14 +498,22 @@ def test_node_daemon_hosts_engine_in_process(procs, dev, tokfile, cluster, tmp_p
         env["TOKENIZER_PATH"] = train_bpe_tokenizer(tmp_path, vocab=500)
     if cluster:
         env.update(cluster)
-    procs.spawn("p2p-node", env)
+    err = open(os.path.join(str(tmp_path), "node.err"), "w")
+    procs.spawn("p2p-node", env, stderr=err)
+
+    def log():  # the node's (and its engine's) stderr, for the assertion messages
+        err.flush()
+        with open(err.name, errors="replace") as f:
+            return f.read()[-4000:]
+
     a = "http://127.0.0.1:%d" % port
     wait_http(a + "/me", timeout=600 if cluster else 120)
     st, body, _ = http("POST", a + "/api/generate", {"model": "llama3.1", "prompt": "hello",
                                                       "stream": False,
                                                       "options": {"num_predict": 5}})
+    assert st == 200, (st, body, log())
     out = json.loads(body)
-    assert st == 200 and out["done"] and out["eval_count"] == 5 and out["prompt_eval_count"] > 0
+    assert out["done"] and out["eval_count"] == 5 and out["prompt_eval_count"] > 0
     st, body, _ = http("POST", a + "/api/generate", {"model": "llama3.1", "prompt": "hello",
                                                       "options": {"num_predict": 3}})
     lines = [json.loads(x) for x in body.strip().splitlines()]
@@ -530,7 +538,7 @@ def test_node_daemon_hosts_engine_in_process(procs, dev, tokfile, cluster, tmp_p
         st, body, _ = http("POST", a + "/api/generate", {"model": "llama3.1", "stream": False,
                                                           "prompt": "Grüße — 日本語? 😀",
                                                           "options": {"num_predict": 4}})
-        assert st == 200 and json.loads(body)["eval_count"] == 4
+        assert st == 200 and json.loads(body)["eval_count"] == 4, (st, body, log())
         m2 = {}
         for line in http("GET", a + "/metrics")[1].splitlines():
             k, _, v = line.partition(" ")

@@ -93,6 +93,17 @@ def test_dp_router_spreads_and_streams():
         m = cs.metrics()
         assert m["replicas"] == 2 and m["live_replicas"] == 2
         assert all(r["routed"] > 0 for r in m["per_replica"])
+        # the engine C ABI's fallback tokenisation when it routes a cluster natively
+        # (ClusterServer.native_front): the tokenizer a replica leader uses
+        from p2p_llm_chat_go_amd.engine.tokenizer import get_tokenizer
+        from p2p_llm_chat_go_amd.models.config import get_config
+
+        tok = get_tokenizer(get_config("tiny-llama-gqa"), None)
+        text = "Grüße — 日本語? 😀"
+        assert cs.encode_request(_req({}, prompt=text)) == tok.chat_ids(text)
+        assert cs.encode_request(json.dumps({"prompt": text, "raw": True})) == tok.encode(text, bos=True)
+        ids = tok.encode(text)
+        assert cs.decode_ids(ids) == tok.decode(ids)
     finally:
         cs.close()
 
