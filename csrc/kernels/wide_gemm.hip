@@ -116,10 +116,43 @@ __device__ __forceinline__ void dma_lds(const void* g, const void* l) {
 // the NEXT chunk.  With every k-loop load and LDS read in asm, the kernel's counted
 // wait_chunks + barrier + lds_wait are the only waits (an MFMA needs its A fragments from
 // lds_wait, which follows the chunk's wait, so it never runs on a weight still in flight).
-__device__ __forceinline__ bf16x8 gload_nt(const bf16x8* p) {
-  bf16x8 v;
-  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p));
-  return v;
+// KW loads of one chunk, skipped inside the asm when c >= n (past the slice): the compiler
+// sees every register set written at every step, so it never merges an in-flight set with an
+// older one (a branch around the loads made it copy in-flight registers), and no dummy load
+// ever goes out (the slice's last chunk is the last thing waited for).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+template <int KW>
+__device__ __forceinline__ void gload_chunk(bf16x8 (&w)[KW], const bf16x8* const (&p)[KW], int c, int n) {
+  static_assert(KW == 4 || KW == 8, "gload_chunk: 4 or 8 k-steps per wave");
+  if constexpr (KW == 4)
+    asm volatile(
+        "s_cmp_lt_i32 %8, %9\n\ts_cbranch_scc0 1f\n\t"
+        "global_load_dwordx4 %0, %4, off nt\n\tglobal_load_dwordx4 %1, %5, off nt\n\t"
+        "global_load_dwordx4 %2, %6, off nt\n\tglobal_load_dwordx4 %3, %7, off nt\n1:"
+        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
+        : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "s"(c), "s"(n)
+        : "scc");
+  else
+    asm volatile(
+        "s_cmp_lt_i32 %16, %17\n\ts_cbranch_scc0 1f\n\t"
+        "global_load_dwordx4 %0, %8, off nt\n\tglobal_load_dwordx4 %1, %9, off nt\n\t"
+        "global_load_dwordx4 %2, %10, off nt\n\tglobal_load_dwordx4 %3, %11, off nt\n\t"
+        "global_load_dwordx4 %4, %12, off nt\n\tglobal_load_dwordx4 %5, %13, off nt\n\t"
+        "global_load_dwordx4 %6, %14, off nt\n\tglobal_load_dwordx4 %7, %15, off nt\n1:"
+        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]),
+          "=&v"(w[6]), "=&v"(w[7])
+        : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]),
+          "s"(c), "s"(n)
+        : "scc");
+}
+#pragma clang diagnostic pop
+// after a chunk's counted wait: its registers re-defined, so no use (or copy) of them can be
+// scheduled before the wait
+template <int KW>
+__device__ __forceinline__ void landed(bf16x8 (&w)[KW]) {
+#pragma unroll
+  for (int k = 0; k < KW; ++k) asm volatile("" : "+v"(w[k]));
 }
 template <int N>
 __device__ __forceinline__ void lds_wait(bf16x8 (&a)[N]) {
@@ -205,35 +238,30 @@ __global__ __launch_bounds__(NW * 64) void wide_gemm_kernel(const bf16x8* __rest
     asrc[i] = X + (size_t)row * ldx + 8 * (lane >> 4);
   }
 
-  // Chunk c's loads.  Past the slice (c >= n: the last D steps) the same instructions go out
-  // on hot addresses -- the slice's last activation chunk into ring slot c % NSLOT, which no
-  // later step reads, and the activations' first fragment row for the weights -- so every
-  // step issues and waits alike.  The addresses are selected, not branched on: a branch
-  // made the compiler merge the in-flight register sets and copy them (a vmcnt(0) before
-  // each copy), which drained the pipeline at every chunk.
-  // Activations: wave w loads k-step w & 7 of the m-tiles of its parity (NW = 16: the odd
-  // wave of a pair repeats its last m-tile when MT is odd, so every wave issues AD
-  // instructions -- the same bytes to the same LDS place -- and the counted waits hold).
+  // Chunk c's loads (nothing past the slice, c >= n).  Activations: wave w loads k-step
+  // w & 7 of the m-tiles of its parity (NW = 16: the odd wave of a pair repeats its last
+  // m-tile when MT is odd, so every wave issues AD instructions -- the same bytes to the same
+  // LDS place -- and the counted waits hold).  The weights go out through gload_chunk.
   auto issue_a = [&](int c) {
     bf16x8* base = ring + (c % NSLOT) * SLOT;
-    const int cc = min(c, n - 1);
-    const int kk = ks0 + cc * KC + min(wg, kv_of(cc) - 1);
+    const int kk = ks0 + c * KC + min(wg, kv_of(c) - 1);
 #pragma unroll
     for (int a = 0; a < AD; ++a) {
       const int i = min(par + NPAR * a, MT - 1);
       dma_lds<16>(asrc[i] + (size_t)kk * 32, base + (i * KC + wg) * 64);
     }
   };
-  const bf16x8* whot = reinterpret_cast<const bf16x8*>(X) + lane;
   auto issue_w = [&](int c, bf16x8(&wr)[KW]) {
-    const int kb = ks0 + c * KC, kl = kv_of(c) - 1;
-    const bool real = c < n;
+    const int cc = min(c, n - 1);  // (addresses only; no load goes out for c >= n)
+    const int kb = ks0 + cc * KC, kl = kv_of(cc) - 1;
+    const bf16x8* p[KW];
 #pragma unroll
-    for (int j = 0; j < KW; ++j)
-      wr[j] = gload_nt(real ? wsrc + (size_t)(kb + min(par + NPAR * j, kl)) * 64 : whot);
+    for (int j = 0; j < KW; ++j) p[j] = wsrc + (size_t)(kb + min(par + NPAR * j, kl)) * 64;
+    gload_chunk<KW>(wr, p, c, n);
   };
   auto issue = [&](int c, bf16x8(&wr)[KW]) {
-    if constexpr (!RES) issue_a(c);
+    if constexpr (!RES)
+      if (c < n) issue_a(c);
     issue_w(c, wr);
   };
 
@@ -343,26 +371,27 @@ __global__ __launch_bounds__(NW * 64) void wide_gemm_kernel(const bf16x8* __rest
   bf16x8 wr[RS][KW];
   if constexpr (RES)  // the whole slice's activations first (host: n <= res_chunks)
     for (int c = 0; c < n; ++c) issue_a(c);
+  // Every real chunk's registers are read after its wait (landed + compute), so none is
+  // dead while its load is in flight; past the slice no load goes out at all.
 #pragma unroll
   for (int j = 0; j < D; ++j) issue(j, wr[j]);
   for (int tb = 0; tb < n; tb += RS) {
 #pragma unroll
     for (int j = 0; j < RS; ++j) {
       const int t = tb + j;
+      if (t >= n) break;
       issue(t + D, wr[(j + D) % RS]);
-      if (t < n) {
-        wait_chunks(D);  // exactly D chunks went out after chunk t
-        if (!RES || t == 0) {  // RES: chunk 0's weights landed => this wave's DMA parts too
-          if (SPLIT && t == 0 && tid == 0) tag_l = (unsigned)(tkt / (u64)splitk) + 1u;  // landed (oldest load)
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          if (t == 0) WSTAMP(1, wall_clock64());
-        }
-        compute(t, wr[j]);
+      wait_chunks(min(D, n - 1 - t));  // the chunks that went out after chunk t
+      landed(wr[j]);
+      if (!RES || t == 0) {  // RES: chunk 0's weights landed => this wave's DMA parts too
+        if (SPLIT && t == 0 && tid == 0) tag_l = (unsigned)(tkt / (u64)splitk) + 1u;  // landed (oldest load)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (t == 0) WSTAMP(1, wall_clock64());
       }
+      compute(t, wr[j]);
     }
   }
-  wait_vmcnt<0>();  // the tail's DMAs land before the ring is reused below
 
   WSTAMP(2, wall_clock64());
   // ---- this wave's row sums of squares: the NQ waves w = sq_mt + 4 x hold m-tile sq_mt ----
