@@ -42,7 +42,7 @@ struct FusedArArgs {
   int rank, world;
   size_t max_bytes;           // data bytes per (parity, src) slot
   unsigned* counters;         // [FAR_MAX_BLOCKS] private per-block call counters
-  int* err;                   // set nonzero when a peer never arrived
+  int* err;                   // [4]: nonzero when a peer never arrived (+ where, see below)
   long long spin_ticks;       // spin bound (100 MHz wall clock)
   int groups;                 // column groups of the call (the launch may have fewer blocks)
 };
@@ -123,6 +123,16 @@ __device__ __forceinline__ void epilogue(const float (&v)[MT][4], int M, int g, 
       if (ok || failed) break;
       if (wall_clock64() - t0 > fa.spin_ticks) {
         atomicOr(fa.err, 2);  // bit 1: a fused epilogue timed out (one-shot kernels set bit 0)
+        // the first timeout of this rank records where it waited: err[1] = column group + 1,
+        // err[2] = the call's seq, err[3] = the sources whose granule never carried it
+        unsigned miss = 0;
+#pragma unroll
+        for (int p = 0; p < FAR_MAX_RANKS; ++p)
+          if (p < fa.world && (unsigned)(x[p] >> 32) != seq) miss |= 1u << p;
+        if (atomicCAS(fa.err + 1, 0, blk + 1) == 0) {
+          __hip_atomic_store(fa.err + 2, (int)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(fa.err + 3, (int)miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(1);

@@ -141,7 +141,9 @@ class CustomAllReduce:
             self._far_bases = self._map(L.p2p_far_buffer_bytes(self.far_max_bytes))
             self.counters = torch.zeros(64, dtype=torch.int32, device=self.device)
             self.far_counters = torch.zeros(1024, dtype=torch.int32, device=self.device)
-            self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+            # [0]: timeout bits (1 one-shot, 2 fused); [1..3]: the fused epilogue's first
+            # timeout (column group + 1, call seq, mask of the sources that never arrived)
+            self.err = torch.zeros(4, dtype=torch.int32, device=self.device)
         torch.cuda.synchronize(self.device)
         # ranks of this group on THIS device (virtual ranks: all of them; a node with one GPU
         # per rank: 1): the fused all-reduce launch keeps to its share of the device's block
@@ -230,13 +232,17 @@ class CustomAllReduce:
 
     def check(self):
         """Raise if any call timed out waiting for a peer (numbers would be wrong)."""
-        e = int(self.err.item())
+        ev = self.err.cpu().tolist()
+        e = ev[0]
         if e != 0:
             where = {1: "one-shot kernel", 2: "fused GEMM epilogue"}.get(e, "one-shot + fused")
-            if e & 2:  # each column group's call count: where this rank's sequence stopped
+            if e & 2:  # where the first fused wait gave up, and each group's call count
                 c = self.far_counters[:256].cpu()
-                where += " (rank %d, coresident %d: fused call counts over column groups min %d max %d)" % (
-                    self.rank, self.coresident, int(c.min()), int(c.max()))
+                miss = [p for p in range(self.world) if ev[3] >> p & 1]
+                where += (" (rank %d, coresident %d: first timeout at column group %d of call %d, "
+                          "no granule from ranks %s; call counts over column groups min %d max %d)"
+                          % (self.rank, self.coresident, ev[1] - 1, ev[2], miss, int(c.min()),
+                             int(c.max())))
             raise CollectiveTimeout("custom all-reduce: a peer never arrived (timeout in the %s); "
                                     "the TP group is broken" % where)
 

@@ -63,7 +63,7 @@ def _worker(rank, world, port, q):
                 car.allreduce_add_(h1, part, two_shot=False)
                 ops.skinny_gemm_ar(wt, xb, h2, car, waves=code)
                 torch.cuda.synchronize()
-                if first_fault is None and int(car.err.item()):
+                if first_fault is None and int(car.err[0].item()):
                     first_fault = (rep, M, N, K, code)
                 same = same and torch.equal(h1, h2)
                 # fp32 reference: sum over ranks of their bf16 partials
