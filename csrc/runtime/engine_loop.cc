@@ -62,6 +62,9 @@ void EngineLoop::shutdown() {
   for (void* e : events_)
     if (e) h.eventDestroy(e);
   events_.clear();
+  for (void* e : staged_ev_)
+    if (e) h.eventDestroy(e);
+  staged_ev_.clear();
   if (stream_) h.streamDestroy(stream_);
   stream_ = nullptr;
 }
@@ -78,16 +81,33 @@ int EngineLoop::bucket(int x, const std::vector<int>& b) {
   return -1;
 }
 
+// A staging slot is rewritten by the host for the next chunk while earlier work may still
+// be queued on the stream ahead of the copy that reads it (a pipelined decode chunk, a
+// prefill chunk behind a running decode): the leader would then run a chunk on the NEXT
+// chunk's metadata or sampling parameters while its followers -- whose frames carry their
+// own copy of the bytes -- run the right ones, and the group's ranks drift apart (a sampled
+// reply of a TP=8 group differed from the Python loop's on some runs).  So a slot whose copies
+// have not run yet is waited for before it is handed out again.
 void* EngineLoop::pinned(int slot, size_t bytes) {
   auto& p = pinned_[slot];
+  const HipApi& h = hip_api();
+  if ((int)staged_ev_.size() > slot && staged_ev_[slot])
+    hip_check(h.eventSynchronize(staged_ev_[slot]), "staging slot reuse");
   if (p.second < bytes) {
-    const HipApi& h = hip_api();
     if (p.first) h.hostFree(p.first);
     size_t n = std::max(bytes, (size_t)4096);
     hip_check(h.hostMalloc(&p.first, n, 0), "hipHostMalloc");
     p.second = n;
   }
   return p.first;
+}
+
+void EngineLoop::staged(int slot) {
+  const HipApi& h = hip_api();
+  if ((int)staged_ev_.size() < kSlots) staged_ev_.resize(kSlots, nullptr);
+  if (!staged_ev_[slot])
+    hip_check(h.eventCreateWithFlags(&staged_ev_[slot], 2 /* hipEventDisableTiming */), "hipEventCreate");
+  hip_check(h.eventRecord(staged_ev_[slot], stream_), "hipEventRecord");
 }
 
 // ------------------------------------------------------------------ registration
@@ -607,6 +627,7 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
       i = e;
     }
     hip_check(h.memcpyAsync(g->meta, m, g->meta_len * 4, kH2D, stream_), "prefill meta H2D");
+    staged(kPrefillMeta);
     if (!g->greedy) {
       float* tf = (float*)pinned(kSampF, S * 4);
       int32_t* tk = (int32_t*)pinned(kSampI, S * 4);
@@ -623,6 +644,7 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
       hip_check(h.memcpyAsync(g->topk, tk, S * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->topp, tp, S * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->seeds, sd, S * 8, kH2D, stream_), "samp H2D");
+      for (int sl : {(int)kSampF, (int)kSampI, (int)kSampP, (int)kSampS}) staged(sl);
     }
     uint32_t pf_seq = 0;
     if (mirror_) {
@@ -701,6 +723,7 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
       slots[b] = bt[b * P + pos[b] / 64] * 64 + pos[b] % 64;
     }
     hip_check(h.memcpyAsync(g->meta, m, n * 4, kH2D, stream_), "decode meta H2D");
+    staged(kDecodeMeta);
     hip_check(h.memsetAsync(g->step, 0, 4, stream_), "step reset");
     if (g->keys && g->keys_bytes)
       hip_check(h.memsetAsync(g->keys, 0, g->keys_bytes, stream_), "keys reset");
@@ -726,6 +749,7 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
       hip_check(h.memcpyAsync(g->topk, tk, B * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->topp, tp, B * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->seeds, sd, B * 8, kH2D, stream_), "samp H2D");
+      for (int sl : {(int)kSampF, (int)kSampI, (int)kSampP, (int)kSampS}) staged(sl);
     }
     if (mirror_) {
       const char K = 'D';

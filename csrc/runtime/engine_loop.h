@@ -193,6 +193,9 @@ class EngineLoop {
   const PrefillGraphDesc* prefill_graph(int rows, int nseq, bool greedy);
   static int bucket(int x, const std::vector<int>& b);
   void* pinned(int slot, size_t bytes);
+  // after the H2D copies from a staging slot are enqueued: the slot is not rewritten (or
+  // freed) until they have run -- see pinned()
+  void staged(int slot);
   int64_t now_ns() const;
 
   LoopConfig cfg_;
@@ -222,6 +225,7 @@ class EngineLoop {
   // device-side state of the loop thread
   void* stream_ = nullptr;
   std::vector<std::pair<void*, size_t>> pinned_;  // host staging buffers by slot
+  std::vector<void*> staged_ev_;                   // per slot: recorded after its last H2D
   std::vector<void*> events_;                     // one per hist buffer
   std::deque<Chunk> flight_;                      // decode chunks enqueued, not yet read (<= 2)
   const DecodeGraphDesc* loaded_ = nullptr;       // graph whose state holds loaded_ids_
