@@ -30,9 +30,10 @@
 // checked) before its MFMAs.  Tags: launch epoch (epoch[0], read by every workgroup at
 // start; the last workgroup to finish advances it) x layers + layer + 1, per buffer, so a
 // granule of an earlier layer or launch never matches.  Buffer reuse across layers is safe
-// because every workgroup takes part in Q, O and D (NB <= qkv groups, NB <= H / 16): no
+// because every workgroup takes part in O, U and D (NB <= H / 16, NB <= gate/up halves): no
 // workgroup can publish layer l + 1's copy of a buffer before every workgroup has swept
-// layer l's.  All spins are bounded (5 s) and give up together once the fault word is set,
+// layer l's.  (Workgroups past the qkv half groups skip Q: round 6, for the 70B TP=8 rank
+// shard, whose 160 qkv halves would otherwise have capped the grid at 160 of 256 CUs.)  All spins are bounded (5 s) and give up together once the fault word is set,
 // so a broken launch drains; the whole grid must be resident (p2p_decode_engine_ok).
 #include "common.h"
 
@@ -252,12 +253,14 @@ __device__ __forceinline__ bf16x8 wload(const Stream& st, int s) {
   return st.on ? __builtin_nontemporal_load(st.wp + (size_t)s * 64) : zero_bf16x8();
 }
 
-// Issue the loads of the stream's first PFK k-steps (the prefetch credit).  Every wave's
-// k-range is a multiple of U and at least PFK steps (p2p_decode_engine_ok), so no load or
-// MFMA below needs a bounds guard.
+// Issue the loads of the stream's first PFK k-steps (the prefetch credit).  A wave's k-range
+// may be shorter than the credit (the 70B TP=8 shard's o_proj: K = 1024, 8 k-steps per wave)
+// or not a multiple of U (its down: K = 3584, 28): the steps past the range load nothing
+// and are not computed (wave-uniform guards).
 __device__ __forceinline__ void prefetch(const Stream& st, bf16x8 (&pf)[PFK]) {
+  const int n = st.s1 - st.s0;
 #pragma unroll
-  for (int i = 0; i < PFK; ++i) pf[i] = wload(st, st.s0 + i);
+  for (int i = 0; i < PFK; ++i) pf[i] = i < n ? wload(st, st.s0 + i) : zero_bf16x8();
 }
 
 // acc = this wave's partial 16 x 16 tile (rows = batch rows from xs).  U k-steps per
@@ -283,16 +286,18 @@ __device__ __forceinline__ void gemv(const Stream& st, const Stream& next, bool 
   bf16x8 bA[U], bB[U];
   auto load = [&](bf16x8(&bw)[U], int at) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) bw[u] = wload(st, at + u);
+    for (int u = 0; u < U; ++u) bw[u] = at + u < s1 ? wload(st, at + u) : zero_bf16x8();
   };
   auto compute = [&](const bf16x8(&bw)[U], int at) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) step(bw[u], at + u);
+    for (int u = 0; u < U; ++u)
+      if (at + u < s1) step(bw[u], at + u);
   };
   int s = st.s0 + PFK;
   if (s < s1) load(bA, s);
 #pragma unroll
-  for (int i = 0; i < PFK; ++i) step(pf[i], st.s0 + i);
+  for (int i = 0; i < PFK; ++i)
+    if (st.s0 + i < s1) step(pf[i], st.s0 + i);
   bool pend = has_next;
   if (s >= s1 && pend) {  // the whole range was the credit
     prefetch(next, pf);
@@ -551,8 +556,17 @@ void decode_engine_kernel(DEArgs a) {
       hres[u][j] = (w == 0 && u < no && m < M) ? (float)a.h[(size_t)m * a.ldh + g * 16 + r] : 0.f;
     }
 
+  // workgroups past the qkv units (NB > NQ2: the 70B TP=8 shard has 160 qkv half groups
+  // for 256 CUs) start on their o_proj group; the attention workgroup's credit is issued
+  // after its attention (registers)
+  const bool has_q = b < NQ2;
   bf16x8 pf[PFK];
-  prefetch(stream_qkv_half(a.w[0], b, H), pf);  // behind the embedding rows
+#pragma unroll
+  for (int i = 0; i < PFK; ++i) pf[i] = zero_bf16x8();
+  if (has_q)
+    prefetch(stream_qkv_half(a.w[0], b, H), pf);  // behind the embedding rows
+  else if (!att)
+    prefetch(stream_group(a.w[1], b, Hq * HD), pf);
   load_rows(a.h, a.ldh, M, H, xs, xstride);
   const int H2 = H / 2, I2 = I / 2;
 
@@ -701,8 +715,10 @@ void decode_engine_kernel(DEArgs a) {
       const Stream st = stream_group(Wd, g, I);
       const bool more = u + 1 < no;
       f32x4 acc;
-      gemv(st, more ? stream_group(Wd, g + NB, I) : stream_qkv_half(a.w[4 * (l + 1) % (4 * a.L)], b, H),
-           more || !last, pf, xs, xstride, M, acc);
+      const bf16x8* const* wn = a.w + 4 * (l + 1) % (4 * a.L);  // the next layer's weights
+      gemv(st, more ? stream_group(Wd, g + NB, I)
+                    : (has_q ? stream_qkv_half(wn[0], b, H) : stream_group(wn[1], b, Hq * HD)),
+           more || (!last && (has_q || !att)), pf, xs, xstride, M, acc);
       if (!reduce(acc, red())) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -770,11 +786,16 @@ int n_cus() {
   return c;
 }
 
+// One workgroup per CU, at most one per o_proj / down column group.  More workgroups than
+// qkv half groups is fine (r6: the 70B TP=8 shard, 160 halves): those skip Q, and every
+// workgroup still takes part in O, U and D, which is what keeps the buffer reuse safe (a
+// workgroup publishes layer l+1's copy of a buffer only after every workgroup's U output of
+// layer l+1, i.e. after each has swept layer l's).
 int grid_for(int H, int Hq, int Hkv) {
-  const int NQ = (Hq + 2 * Hkv) * (HD / 16) * 2;  // qkv half groups
+  (void)Hq;
+  (void)Hkv;
   int nb = n_cus();
   if (H / 16 < nb) nb = H / 16;
-  if (NQ < nb) nb = NQ;
   return nb;
 }
 
@@ -797,10 +818,11 @@ P2P_API int p2p_decode_engine_grid(int H, int Hq, int Hkv) { return grid_for(H, 
 P2P_API int p2p_decode_engine_ok(int M, int H, int I, int Hq, int Hkv, int max_ctx) {
   if (M < 1 || M > MAXM || Hkv <= 0 || Hq % Hkv || max_ctx > KW * MKPW || H % 16 || I % 16)
     return 0;
-  // every wave's k-range (K / 32 / W steps) a multiple of U holding the prefetch credit
+  // every wave a whole number of k-steps (ranges shorter than the prefetch credit or not a
+  // multiple of U are guarded in gemv)
   for (int K : {H, I, Hq * HD})
-    if (K % (32 * W * U) || K / 32 / W < PFK) return 0;
-  if ((H / 2) % (32 * W * U) || H / 2 / 32 / W < PFK) return 0;  // qkv k-halves
+    if (K % (32 * W)) return 0;
+  if ((H / 2) % (32 * W)) return 0;  // qkv k-halves
   const int G = Hq / Hkv;
   const void* k = kernel_for(G);
   if (!k) return 0;

@@ -15,12 +15,25 @@ from p2p_llm_chat_go_amd.models.weights import EngineWeights
 pytestmark = pytest.mark.gpu
 
 
-def _setup(ctxs, layers=3, seed=5):
-    cfg = LLAMA31_8B.replace(n_layers=layers)
+def _shard_cfg(layers):
+    """llama3.1-70B's per-rank shapes at TP=8 as a TP=1 model (bench/decode_engine_bench.py
+    --tp8-shard): 8 q heads + 1 kv head, 3584 ffn columns (28 k-steps per wave in down, not
+    a multiple of the 8-step batch), o_proj K = 1024 (8 k-steps per wave, under the
+    16-fragment prefetch credit), 160 qkv half groups for 256 workgroups."""
+    from p2p_llm_chat_go_amd.models.config import get_config
+
+    c = get_config("llama3.1-70b")
+    return c.replace(name="llama3.1-70b-tp8-shard", n_heads=c.n_heads // 8, n_kv_heads=1,
+                     ffn=c.ffn // 8, vocab=c.vocab // 8, n_layers=layers)
+
+
+def _setup(ctxs, layers=3, seed=5, shard=False):
+    cfg = _shard_cfg(layers) if shard else LLAMA31_8B.replace(n_layers=layers)
     w = EngineWeights.random(cfg, "cuda", seed=seed)
     eng = Engine(cfg, weights=w, device="cuda", kv_pages=64, max_batch=8)
     pages = [eng.kv.allocator.alloc(4) for _ in ctxs]
-    prompts = [[(31 * b + 7 * i) % 30000 + 100 for i in range(c)] for b, c in enumerate(ctxs)]
+    V = min(30000, cfg.vocab - 200)
+    prompts = [[(31 * b + 7 * i) % V + 100 for i in range(c)] for b, c in enumerate(ctxs)]
     pre = [(p[:-1], pg) for p, pg in zip(prompts, pages) if len(p) > 1]
     if pre:
         eng.prefill([x[0] for x in pre], [x[1] for x in pre])
@@ -31,11 +44,14 @@ def _rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-6))
 
 
-@pytest.mark.parametrize("ctxs", [[1], [108], [64, 200], [5, 65, 128, 256], [256, 1, 77]])
-def test_decode_engine_matches_layer_launches(ctxs):
+@pytest.mark.parametrize("ctxs,shard", [([1], False), ([108], False), ([64, 200], False),
+                                        ([5, 65, 128, 256], False), ([256, 1, 77], False),
+                                        ([108], True), ([5, 200], True)])
+def test_decode_engine_matches_layer_launches(ctxs, shard):
+    """shard: the 70B TP=8 rank shapes (the engine had refused them)."""
     from p2p_llm_chat_go_amd.ops.decode_engine import decode_engine_ok
 
-    eng, cfg, pages, prompts = _setup(ctxs)
+    eng, cfg, pages, prompts = _setup(ctxs, shard=shard)
     m = eng.model
     R = len(ctxs)
     assert decode_engine_ok(m, R, 256)
