@@ -1,6 +1,6 @@
 """Persistent decode engine vs the per-layer launches: one decode step of llama3.1-8B (all
 32 layers, random-init bf16, context 108) captured in a hipGraph each way and replayed;
---trace adds the engine's per-phase wall-clock stamps (csrc/kernels/decode_engine.hip TR):
+--trace adds the engine's per-phase wall-clock stamps (csrc/experimental/decode_engine.hip TR):
 per layer, the median / max over workgroups of each phase's duration.
 
   python bench/decode_engine_bench.py [--rows 1] [--ctx 108] [--iters 200] [--trace]
@@ -79,7 +79,7 @@ def main():
         out["engine_us" if mode else "layers_us"] = round(us, 1)
     out["engine_ran"] = m._de is not None
     if a.trace and m._de is not None:
-        L = _lib.lib()
+        L = _lib.experimental()  # the engine lives in the experimental library
         nb = L.p2p_decode_engine_grid(cfg.hidden, m.nq, m.nkv)
         tr = torch.zeros(nb * cfg.n_layers * 10, dtype=torch.int64, device=dev)
         L.p2p_decode_engine_trace(tr.data_ptr())
