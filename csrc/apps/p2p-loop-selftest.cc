@@ -207,7 +207,7 @@ int run(bool pipeline, bool riders_all) {
   });
   loop.set_eager_prefill([](const std::vector<std::vector<int>>& prompts,
                             const std::vector<std::vector<int>>&, const std::vector<int>&,
-                            const std::vector<LoopSampling>&) {
+                            const std::vector<LoopSampling>&, int) {
     std::vector<int> f;
     for (const auto& p : prompts) f.push_back(nxt(p.back(), (int)p.size() - 1));
     return f;
@@ -321,15 +321,15 @@ int run_group() {
     }
   });
   auto eager = [](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>&,
-                  const std::vector<int>&, const std::vector<LoopSampling>&) {
+                  const std::vector<int>&, const std::vector<LoopSampling>&, int) {
     std::vector<int> f;
     for (const auto& p : prompts) f.push_back(nxt(p.back(), (int)p.size() - 1));
     return f;
   };
   loop.set_eager_prefill([&](const std::vector<std::vector<int>>& p, const std::vector<std::vector<int>>& pg,
-                             const std::vector<int>& st, const std::vector<LoopSampling>& sm) {
+                             const std::vector<int>& st, const std::vector<LoopSampling>& sm, int) {
     leader_eager++;
-    return eager(p, pg, st, sm);
+    return eager(p, pg, st, sm, 0);
   });
   struct Follower {
     std::unique_ptr<EngineMirror> m;
@@ -355,9 +355,9 @@ int run_group() {
     });
     F.m->set_eager_prefill([&F, eager](const std::vector<std::vector<int>>& p,
                                        const std::vector<std::vector<int>>& pg,
-                                       const std::vector<int>& st, const std::vector<LoopSampling>& sm) {
+                                       const std::vector<int>& st, const std::vector<LoopSampling>& sm, int) {
       F.eager++;
-      return eager(p, pg, st, sm);
+      return eager(p, pg, st, sm, 0);
     });
     F.th = std::thread([&F] { F.result = F.m->run(); });
   }
@@ -426,6 +426,138 @@ int run_group() {
              : 1;
 }
 
+// An EP all-to-all group (LoopConfig::dp_world = 3: leader + 2 followers, DP attention): each
+// sequence lives on one rank, every rank runs its own share through the same shapes (its own
+// metadata in its own frame), the followers send their tokens back with their frames' status,
+// and every reply must be exactly right -- which it is only if every share's tokens reached
+// the leader's scheduler in the right rows.  The eager prefill of every rank gets the same
+// padded row count, the largest share's.
+int run_group_dp() {
+  constexpr int NF = 2;
+  LoopConfig c;
+  c.num_pages = 512;
+  c.max_batch = 8;
+  c.max_prefill_tokens = 256;
+  c.max_ctx = 2048;
+  c.eos = {EOS};
+  c.decode_chunk = 8;
+  c.admit_wait_us = 200.0;
+  c.mixed = false;
+  c.dp_world = NF + 1;
+  c.row_buckets = {16, 32, 48, 64, 96, 128, 192, 256};
+  c.prefill_max_pages = PREFILL_PAGES;
+  EngineLoop loop(c);
+  int sv[NF][2];
+  std::vector<int> fds;
+  for (int f = 0; f < NF; ++f) {
+    if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv[f]) != 0) return 1;
+    fds.push_back(sv[f][0]);
+  }
+  loop.set_mirror(fds);
+  using DMap = std::map<std::tuple<int, int>, std::unique_ptr<DecodeGraph>>;
+  DMap ld;
+  std::atomic<int> leader_eager{0}, bad_pad{0};
+  loop.set_provider([&](const std::string& kind, int a, int b, bool greedy) {
+    loop.mirror_provide(kind, a, b, greedy);
+    if (kind == "decode") {
+      ld[{a, b}].reset(new DecodeGraph(a, b));
+      loop.add_decode_graph(ld[{a, b}]->d);
+    } else {
+      bad_pad++;  // dp groups prefill eagerly: no prefill graph may be asked for
+    }
+  });
+  auto eager = [&bad_pad](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>&,
+                          const std::vector<int>&, const std::vector<LoopSampling>&, int pad) {
+    std::vector<int> f;
+    int rows = 0;
+    for (const auto& p : prompts) {
+      f.push_back(nxt(p.back(), (int)p.size() - 1));
+      rows += (int)p.size();
+    }
+    if (pad < rows || pad < 1) bad_pad++;
+    return f;
+  };
+  loop.set_eager_prefill([&](const std::vector<std::vector<int>>& p, const std::vector<std::vector<int>>& pg,
+                             const std::vector<int>& st, const std::vector<LoopSampling>& sm, int pad) {
+    leader_eager++;
+    return eager(p, pg, st, sm, pad);
+  });
+  struct Follower {
+    std::unique_ptr<EngineMirror> m;
+    DMap d;
+    std::atomic<int> eager{0};
+    std::string result = "?";
+    std::thread th;
+  };
+  Follower fol[NF];
+  for (int f = 0; f < NF; ++f) {
+    Follower& F = fol[f];
+    F.m.reset(new EngineMirror(sv[f][1], 0));
+    EngineMirror* M = F.m.get();
+    F.m->set_provider([&F, M](const std::string& kind, int a, int b, bool) {
+      if (kind == "decode") {
+        F.d[{a, b}].reset(new DecodeGraph(a, b));
+        M->add_decode_graph(F.d[{a, b}]->d);
+      }
+    });
+    F.m->set_eager_prefill([&F, eager](const std::vector<std::vector<int>>& p,
+                                       const std::vector<std::vector<int>>& pg,
+                                       const std::vector<int>& st, const std::vector<LoopSampling>& sm, int pad) {
+      F.eager++;
+      return eager(p, pg, st, sm, pad);
+    });
+    F.th = std::thread([&F] { F.result = F.m->run(); });
+  }
+  loop.start();
+  std::atomic<int> failures{0}, checked{0};
+  auto peer = [&](int k) {
+    std::mt19937 rng(301 + k);
+    for (int n = 0; n < 8; ++n) {
+      const int L = std::vector<int>{3, 17, 44, 64, 120, 200}[rng() % 6];
+      std::vector<int> prompt(L);
+      for (int& t : prompt) t = (int)(rng() % (V - 1));
+      const int max_new = 1 + (int)(rng() % 40);
+      const int64_t id = loop.submit(prompt, max_new, false, LoopSampling());
+      LoopResult r;
+      if (!loop.wait(id, 30.0, &r) || !r.error.empty()) {
+        std::fprintf(stderr, "selftest dp: request failed: %s\n", r.error.c_str());
+        failures++;
+      }
+      loop.release(id);
+      if (r.tokens != expected(prompt, max_new, false)) {
+        std::fprintf(stderr, "selftest dp: reply mismatch (L=%d n=%d)\n", L, max_new);
+        failures++;
+      }
+      checked++;
+    }
+  };
+  std::vector<std::thread> ths;
+  for (int k = 0; k < 8; ++k) ths.emplace_back(peer, k);
+  for (auto& t : ths) t.join();
+  auto lm = loop.metrics();
+  loop.shutdown();
+  long fol_launches = 0;
+  for (int f = 0; f < NF; ++f) {
+    fol[f].th.join();
+    fol[f].m->shutdown();
+    close(sv[f][0]);
+    close(sv[f][1]);
+    if (!fol[f].result.empty()) {
+      std::fprintf(stderr, "selftest dp: follower %d ended with '%s'\n", f, fol[f].result.c_str());
+      failures++;
+    }
+    if (fol[f].eager.load() != leader_eager.load()) failures++;
+    for (auto& kv : fol[f].d) fol_launches += kv.second->launches;
+  }
+  std::printf("group dp: checked=%d failures=%d eager=%d follower_launches=%ld bad=%d frames=%ld\n",
+              checked.load(), failures.load(), leader_eager.load(), fol_launches, bad_pad.load(),
+              (long)lm["mirror_frames"]);
+  return failures.load() == 0 && bad_pad.load() == 0 && g_bad.load() == 0 && checked.load() == 64 &&
+                 fol_launches > 0
+             ? 0
+             : 1;
+}
+
 // Faults on a follower rank: a follower whose graph fault word is set, or whose
 // eager-prefill callback raises, answers that frame with its status bits; the leader must
 // fail exactly that step (the request gets the reason), clear every rank's words, and go
@@ -458,7 +590,7 @@ int run_group_faults() {
     }
   });
   auto eager = [](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>&,
-                  const std::vector<int>&, const std::vector<LoopSampling>&) {
+                  const std::vector<int>&, const std::vector<LoopSampling>&, int) {
     std::vector<int> f;
     for (const auto& p : prompts) f.push_back(nxt(p.back(), (int)p.size() - 1));
     return f;
@@ -475,9 +607,9 @@ int run_group_faults() {
     }
   });
   m.set_eager_prefill([&](const std::vector<std::vector<int>>& p, const std::vector<std::vector<int>>& pg,
-                          const std::vector<int>& st, const std::vector<LoopSampling>& sm) {
+                          const std::vector<int>& st, const std::vector<LoopSampling>& sm, int) {
     if (g_follower_eager_fail.exchange(0)) throw std::runtime_error("injected eager failure");
-    return eager(p, pg, st, sm);
+    return eager(p, pg, st, sm, 0);
   });
   std::string fres = "?";
   std::thread fth([&] { fres = m.run(); });
@@ -553,7 +685,7 @@ int run_remote() {
       }
     });
     L->set_eager_prefill([](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>&,
-                            const std::vector<int>&, const std::vector<LoopSampling>&) {
+                            const std::vector<int>&, const std::vector<LoopSampling>&, int) {
       std::vector<int> f;
       for (const auto& p : prompts) f.push_back(nxt(p.back(), (int)p.size() - 1));
       return f;
@@ -640,6 +772,7 @@ int main() {
   rc |= run(true, true);
   rc |= run_group();
   rc |= run_group_faults();
+  rc |= run_group_dp();
   rc |= run_remote();
   if (rc == 0) std::printf("LOOP_SELFTEST_OK\n");
   return rc;

@@ -89,6 +89,7 @@ LoopConfig loop_cfg(const py::dict& d) {
   c.prefill_max_pages = val_of<int>(d, "prefill_max_pages", 64);
   c.prefill_graph_after = val_of<int>(d, "prefill_graph_after", 2);
   c.pipeline_free_slots = val_of<bool>(d, "pipeline_free_slots", false);
+  c.dp_world = val_of<int>(d, "dp_world", 1);
   return c;
 }
 
@@ -165,11 +166,13 @@ EngineLoop::GraphProvider py_provider(py::function f) {
 EngineLoop::EagerPrefill py_eager(py::function f) {
   auto fn = std::make_shared<py::function>(std::move(f));
   return [fn](const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>& pages,
-              const std::vector<int>& starts, const std::vector<LoopSampling>& samp) {
+              const std::vector<int>& starts, const std::vector<LoopSampling>& samp, int pad_rows) {
     py::gil_scoped_acquire gil;
     try {
       py::list sp;
       for (auto& s : samp) sp.append(py::make_tuple(s.temperature, s.top_k, s.top_p, s.seed));
+      if (pad_rows > 0)  // EP a2a groups (LoopConfig::dp_world): exactly this many rows
+        return py::cast<std::vector<int>>((*fn)(prompts, pages, starts, sp, pad_rows));
       return py::cast<std::vector<int>>((*fn)(prompts, pages, starts, sp));
     } catch (py::error_already_set& e) {
       throw std::runtime_error(std::string("eager prefill raised: ") + e.what());

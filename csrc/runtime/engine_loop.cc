@@ -110,6 +110,71 @@ void EngineLoop::staged(int slot) {
   hip_check(h.eventRecord(staged_ev_[slot], stream_), "hipEventRecord");
 }
 
+std::vector<std::vector<int64_t>> EngineLoop::split_by_home(const std::vector<int64_t>& ids,
+                                                             bool assign) {
+  const int W = std::max(1, cfg_.dp_world);
+  std::vector<std::vector<int64_t>> parts(W);
+  std::lock_guard<std::mutex> lk(mu_);
+  if (assign) {
+    // a new sequence goes to the rank holding the fewest live ones (ties rotate), as
+    // engine/cluster.py LockstepEngine._parts does for the Python loop
+    std::vector<int> live(W, 0);
+    for (int64_t id : sched_.running()) {
+      if (std::find(ids.begin(), ids.end(), id) != ids.end()) continue;
+      auto it = reqs_.find(id);
+      if (it != reqs_.end()) live[it->second.home]++;
+    }
+    for (int64_t id : ids) {
+      int h = 0;
+      for (int r = 1; r < W; ++r) {
+        const int a = (r - home_rr_ + W) % W, b = (h - home_rr_ + W) % W;
+        if (live[r] < live[h] || (live[r] == live[h] && a < b)) h = r;
+      }
+      home_rr_ = (h + 1) % W;
+      live[h]++;
+      reqs_[id].home = h;
+    }
+  }
+  for (int64_t id : ids) {
+    auto it = reqs_.find(id);
+    parts[it != reqs_.end() ? it->second.home : 0].push_back(id);
+  }
+  return parts;
+}
+
+// A decode graph's batch state for rows `ids` (DecodeState layout: ids | pos | ctx | slots |
+// block tables; rows past them are dummies on the null page at position 0) and, for sampled
+// graphs, its sampler slots.  Caller holds no lock.
+void EngineLoop::decode_meta(const DecodeGraphDesc* g, const std::vector<int64_t>& ids, int32_t* m,
+                             float* tf, int32_t* tk, float* tp, int64_t* sd) {
+  const int B = g->B, P = g->max_pages;
+  std::memset(m, 0, (size_t)B * (4 + P) * 4);
+  int32_t *idv = m, *pos = m + B, *ctx = m + 2 * B, *slots = m + 3 * B, *bt = m + 4 * B;
+  std::vector<LoopSampling> samp;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (size_t b = 0; b < ids.size(); ++b) {
+      const SchedRequest& r = sched_.get(ids[b]);
+      for (size_t i = 0; i < r.pages.size() && (int)i < P; ++i) bt[b * P + i] = r.pages[i];
+      idv[b] = r.tokens.empty() ? 0 : r.tokens.back();
+      pos[b] = r.pos;
+      samp.push_back(reqs_[ids[b]].samp);
+    }
+  }
+  for (int b = 0; b < B; ++b) {
+    ctx[b] = pos[b] + 1;
+    slots[b] = bt[b * P + pos[b] / 64] * 64 + pos[b] % 64;
+  }
+  if (!tf) return;
+  for (int b = 0; b < B; ++b) {
+    const LoopSampling d = b < (int)samp.size() ? samp[b] : LoopSampling();
+    tf[b] = b < (int)samp.size() ? d.temperature : 0.f;
+    tk[b] = d.top_k;
+    tp[b] = d.top_p;
+    sd[b] = b < (int)samp.size() ? d.seed : 0;
+  }
+}
+
 // ------------------------------------------------------------------ registration
 void EngineLoop::add_decode_graph(const DecodeGraphDesc& d) {
   std::lock_guard<std::mutex> lk(gmu_);
@@ -330,6 +395,7 @@ std::map<std::string, double> EngineLoop::metrics() {
   m["waiting"] = sched_.n_waiting();
   m["free_kv_pages"] = sched_.free_pages();
   m["native_loop"] = 1;
+  m["dp_world"] = cfg_.dp_world;
   if (mirror_) {
     m["mirror_frames"] = mirror_->frames();
     m["mirror_bytes"] = mirror_->bytes();
@@ -507,7 +573,7 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
       max_pages_needed = std::max(max_pages_needed, (int)((s.prompt->size() + 63) / 64));
       seqs.push_back(std::move(s));
     }
-    if (cfg_.mixed) {
+    if (cfg_.mixed && cfg_.dp_world <= 1) {
       // running sequences fill the chunk's last 64-row tile, never start another one
       // riders_all: every running sequence rides (bounded by the chunk budget) -- under high
       // concurrency a prompt admitted alone would otherwise stall the sequences that do not
@@ -543,10 +609,75 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
   const int rb = bucket(n_rows, cfg_.row_buckets);
   const int sb = std::min(bucket(nseq, cfg_.batch_buckets), cfg_.max_batch);
   const PrefillGraphDesc* g = nullptr;
-  if (rb > 0 && sb >= nseq && max_pages_needed <= cfg_.prefill_max_pages)
+  const bool dp = cfg_.dp_world > 1;
+  if (!dp && rb > 0 && sb >= nseq && max_pages_needed <= cfg_.prefill_max_pages)
     g = prefill_graph(rb, sb, greedy);
   std::vector<int> first(nseq, 0);
-  if (!g) {
+  if (dp) {
+    // EP a2a group: every rank prefills its own share of the new sequences, padded to the
+    // largest share's rows (the exchange needs equal row counts), through the eager path;
+    // the followers' first tokens come back with their frame's status
+    riders.clear();
+    std::vector<int64_t> ids;
+    for (auto& s : seqs)
+      if (s.prompt) ids.push_back(s.id);
+    const std::vector<std::vector<int64_t>> parts = split_by_home(ids, true);
+    std::map<int64_t, const Seq*> by_id;
+    for (auto& s : seqs) by_id[s.id] = &s;
+    int pad = 1;
+    for (auto& part : parts) {
+      int rows = 0;
+      for (int64_t id : part) rows += (int)by_id[id]->prompt->size();
+      pad = std::max(pad, rows);
+    }
+    auto share = [&](const std::vector<int64_t>& part, std::vector<std::vector<int>>* prompts,
+                     std::vector<std::vector<int>>* pages, std::vector<int>* starts,
+                     std::vector<LoopSampling>* samp) {
+      for (int64_t id : part) {
+        const Seq* q = by_id[id];
+        prompts->push_back(*q->prompt);
+        pages->push_back(q->pages);
+        starts->push_back(0);
+        samp->push_back(q->samp);
+      }
+    };
+    const int64_t te = now_ns();
+    uint32_t mseq = 0;
+    if (mirror_) {
+      for (size_t f = 1; f < parts.size(); ++f) {
+        std::vector<std::vector<int>> pr, pg;
+        std::vector<int> st;
+        std::vector<LoopSampling> sp;
+        share(parts[f], &pr, &pg, &st, &sp);
+        mirror_->set_target((int)f - 1);
+        mirror_->eager(pr, pg, st, sp, pad, true);
+      }
+      mseq = mirror_->flush();
+    }
+    std::vector<std::vector<int>> pr, pg;
+    std::vector<int> st;
+    std::vector<LoopSampling> sp;
+    share(parts[0], &pr, &pg, &st, &sp);
+    const std::vector<int> mine = eager_(pr, pg, st, sp, pad);
+    eager_ns_ += now_ns() - te;
+    n_eager_prefill_++;
+    follower_check(mseq, "eager prefill");
+    std::map<int64_t, int> tok;
+    for (size_t i = 0; i < parts[0].size() && i < mine.size(); ++i) tok[parts[0][i]] = mine[i];
+    for (size_t f = 1; f < parts.size(); ++f) {
+      const std::vector<int> t = mirror_ ? mirror_->take_tokens((int)f - 1, mseq) : std::vector<int>();
+      if (t.size() < parts[f].size())
+        throw std::runtime_error("group follower " + std::to_string(f) + " sent " +
+                                 std::to_string(t.size()) + " first tokens for " +
+                                 std::to_string(parts[f].size()) + " sequences");
+      for (size_t i = 0; i < parts[f].size(); ++i) tok[parts[f][i]] = t[i];
+    }
+    int b = 0;
+    for (auto& s : seqs) {
+      if (!s.prompt) break;
+      first[b++] = tok[s.id];
+    }
+  } else if (!g) {
     // beyond every captured shape (a long prompt): Python's chunked eager prefill, without
     // riders (they decode in the next step instead)
     if (!eager_) throw std::runtime_error("prompt exceeds the captured prefill shapes");
@@ -567,7 +698,7 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
       mirror_->eager(prompts, pages, starts, samp);
       mseq = mirror_->flush();
     }
-    first = eager_(prompts, pages, starts, samp);
+    first = eager_(prompts, pages, starts, samp, 0);
     eager_ns_ += now_ns() - te;
     n_eager_prefill_++;
     follower_check(mseq, "eager prefill");
@@ -700,51 +831,31 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
 void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_t>& ids,
                               bool load, int k) {
   const HipApi& h = hip_api();
+  const bool dp = cfg_.dp_world > 1;
+  std::vector<std::vector<int64_t>> parts;
+  if (dp) parts = split_by_home(ids, false);
+  const std::vector<int64_t>& mine = dp ? parts[0] : ids;
   if (load) {
     const int B = g->B, P = g->max_pages;
     const size_t n = (size_t)B * (4 + P);
     int32_t* m = (int32_t*)pinned(kDecodeMeta, n * 4);
-    std::memset(m, 0, n * 4);
-    int32_t *idv = m, *pos = m + B, *ctx = m + 2 * B, *slots = m + 3 * B, *bt = m + 4 * B;
-    std::vector<std::tuple<float, int, float, int64_t>> samp;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      for (size_t b = 0; b < ids.size(); ++b) {
-        const SchedRequest& r = sched_.get(ids[b]);
-        for (size_t i = 0; i < r.pages.size() && (int)i < P; ++i) bt[b * P + i] = r.pages[i];
-        idv[b] = r.tokens.empty() ? 0 : r.tokens.back();
-        pos[b] = r.pos;
-        const LoopSampling& s = reqs_[ids[b]].samp;
-        samp.emplace_back(s.temperature, s.top_k, s.top_p, s.seed);
-      }
+    float* tf = nullptr;
+    int32_t* tk = nullptr;
+    float* tp = nullptr;
+    int64_t* sd = nullptr;
+    if (!g->greedy) {
+      tf = (float*)pinned(kSampF, B * 4);
+      tk = (int32_t*)pinned(kSampI, B * 4);
+      tp = (float*)pinned(kSampP, B * 4);
+      sd = (int64_t*)pinned(kSampS, B * 8);
     }
-    for (int b = 0; b < B; ++b) {  // rows >= n: dummies on the null page at position 0
-      ctx[b] = pos[b] + 1;
-      slots[b] = bt[b * P + pos[b] / 64] * 64 + pos[b] % 64;
-    }
+    decode_meta(g, mine, m, tf, tk, tp, sd);
     hip_check(h.memcpyAsync(g->meta, m, n * 4, kH2D, stream_), "decode meta H2D");
     staged(kDecodeMeta);
     hip_check(h.memsetAsync(g->step, 0, 4, stream_), "step reset");
     if (g->keys && g->keys_bytes)
       hip_check(h.memsetAsync(g->keys, 0, g->keys_bytes, stream_), "keys reset");
     if (!g->greedy) {
-      float* tf = (float*)pinned(kSampF, B * 4);
-      int32_t* tk = (int32_t*)pinned(kSampI, B * 4);
-      float* tp = (float*)pinned(kSampP, B * 4);
-      int64_t* sd = (int64_t*)pinned(kSampS, B * 8);
-      for (int b = 0; b < B; ++b) {
-        if (b < (int)samp.size()) {
-          tf[b] = std::get<0>(samp[b]);
-          tk[b] = std::get<1>(samp[b]);
-          tp[b] = std::get<2>(samp[b]);
-          sd[b] = std::get<3>(samp[b]);
-        } else {
-          tf[b] = 0.f;
-          tk[b] = 40;
-          tp[b] = 0.9f;
-          sd[b] = 0;
-        }
-      }
       hip_check(h.memcpyAsync(g->temp, tf, B * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->topk, tk, B * 4, kH2D, stream_), "samp H2D");
       hip_check(h.memcpyAsync(g->topp, tp, B * 4, kH2D, stream_), "samp H2D");
@@ -753,15 +864,35 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
     }
     if (mirror_) {
       const char K = 'D';
-      mirror_->h2d(K, g->B, g->ctx, g->greedy, kFMeta, m, n * 4);
+      if (!dp) {
+        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFMeta, m, n * 4);
+        if (!g->greedy) {
+          mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTemp, tf, B * 4);
+          mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTopk, tk, B * 4);
+          mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTopp, tp, B * 4);
+          mirror_->h2d(K, g->B, g->ctx, g->greedy, kFSeeds, sd, B * 8);
+        }
+      } else {  // every follower its own share's state (EP a2a: different sequences per rank)
+        std::vector<int32_t> fm(n);
+        std::vector<float> ftf(B), ftp(B);
+        std::vector<int32_t> ftk(B);
+        std::vector<int64_t> fsd(B);
+        for (size_t f = 1; f < parts.size(); ++f) {
+          decode_meta(g, parts[f], fm.data(), g->greedy ? nullptr : ftf.data(), ftk.data(),
+                      ftp.data(), fsd.data());
+          mirror_->set_target((int)f - 1);
+          mirror_->h2d(K, g->B, g->ctx, g->greedy, kFMeta, fm.data(), n * 4);
+          if (!g->greedy) {
+            mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTemp, ftf.data(), B * 4);
+            mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTopk, ftk.data(), B * 4);
+            mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTopp, ftp.data(), B * 4);
+            mirror_->h2d(K, g->B, g->ctx, g->greedy, kFSeeds, fsd.data(), B * 8);
+          }
+        }
+        mirror_->set_target(-1);
+      }
       mirror_->memset0(K, g->B, g->ctx, g->greedy, kFStep, 4);
       if (g->keys && g->keys_bytes) mirror_->memset0(K, g->B, g->ctx, g->greedy, kFKeys, g->keys_bytes);
-      if (!g->greedy) {
-        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTemp, pinned_[kSampF].first, B * 4);
-        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTopk, pinned_[kSampI].first, B * 4);
-        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFTopp, pinned_[kSampP].first, B * 4);
-        mirror_->h2d(K, g->B, g->ctx, g->greedy, kFSeeds, pinned_[kSampS].first, B * 8);
-      }
     }
     loaded_ = g;
     loaded_ids_ = ids;
@@ -776,6 +907,12 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
   if (mirror_) {  // the followers replay the same graphs (their collectives pair with ours)
     if (nk) mirror_->launch('D', g->B, g->ctx, g->greedy, 1, (uint32_t)nk);
     if (n1) mirror_->launch('D', g->B, g->ctx, g->greedy, 0, (uint32_t)n1);
+    if (dp)  // each follower sends its share's k new tokens back with this frame's status
+      for (size_t f = 1; f < parts.size(); ++f) {
+        mirror_->set_target((int)f - 1);
+        mirror_->tokens('D', g->B, g->ctx, g->greedy, 0, (uint32_t)loaded_steps_, (uint32_t)k,
+                        (uint32_t)parts[f].size());
+      }
     mseq = mirror_->flush();
   }
   for (int i = 0; i < nk; ++i) {
@@ -785,7 +922,8 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
   for (int i = 0; i < n1; ++i) hip_check(h.graphLaunch(g->exec, stream_), "decode graph launch");
   Chunk c;
   c.g = g;
-  c.ids = ids;
+  c.ids = mine;
+  if (dp) c.parts.assign(parts.begin() + 1, parts.end());
   c.s0 = loaded_steps_;
   c.k = k;
   c.buf = hist_buf_;
@@ -832,9 +970,23 @@ void EngineLoop::collect() {
     const int32_t* row = hist + (size_t)b * c.k;
     toks[b].assign(row, row + c.k);
   }
+  std::vector<int64_t> ids = c.ids;
+  for (size_t f = 0; f < c.parts.size(); ++f) {  // dp groups: the followers' shares
+    const std::vector<int> t = mirror_->take_tokens((int)f, c.mseq);
+    if (t.size() < c.parts[f].size() * (size_t)c.k) {
+      flight_.clear();
+      throw std::runtime_error("group follower " + std::to_string(f + 1) + " sent " +
+                               std::to_string(t.size()) + " tokens for " +
+                               std::to_string(c.parts[f].size()) + " x " + std::to_string(c.k));
+    }
+    for (size_t b = 0; b < c.parts[f].size(); ++b) {
+      ids.push_back(c.parts[f][b]);
+      toks.emplace_back(t.begin() + b * c.k, t.begin() + (b + 1) * c.k);
+    }
+  }
   {
     std::lock_guard<std::mutex> lk(mu_);
-    sched_.on_decode_tokens(c.ids, toks);
+    sched_.on_decode_tokens(ids, toks);
     n_decode_steps_ += c.k;
     if (flight_.empty()) sched_.flush_deferred();  // nothing in flight can touch them now
   }
@@ -914,7 +1066,13 @@ void EngineLoop::decode(const std::vector<int64_t>& running_in, bool waiting) {
       need = std::max(need, r.prompt_len + r.max_new + 2 * cfg_.decode_chunk + 2);
       greedy &= reqs_[id].samp.greedy();
     }
-    const int B = bucket((int)ids.size(), cfg_.batch_buckets);
+    int rows = (int)ids.size();
+    if (cfg_.dp_world > 1) {  // every rank runs the largest share's batch bucket
+      std::vector<int> per(cfg_.dp_world, 0);
+      rows = 0;
+      for (int64_t id : ids) rows = std::max(rows, ++per[reqs_[id].home]);
+    }
+    const int B = bucket(rows, cfg_.batch_buckets);
     const int C = bucket(need, cfg_.ctx_buckets);
     if (B < 0 || C < 0) throw std::runtime_error("decode batch / context exceeds the buckets");
     return std::make_tuple(B, C, greedy);

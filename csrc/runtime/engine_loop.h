@@ -103,6 +103,13 @@ struct LoopConfig {
   int prefill_max_pages = 64;  // block-table width of the prefill graphs (their context bucket / 64)
   bool pipeline_free_slots = false;  // speculate decode chunks even while a batch slot is free
   int prefill_graph_after = 2;  // a chunk shape is captured on its n-th use (eager before)
+  // EP all-to-all groups (DP attention): the group's dp_world ranks hold DIFFERENT sequences.
+  // Each sequence gets a home rank at admission (fewest live sequences); every prefill / decode
+  // call runs each rank's share through the same shapes (prefill padded to the largest share,
+  // decode at the largest share's batch bucket), followers' frames carry their own metadata,
+  // and their tokens come back on the status channel (runtime/mirror.h 'T', 'E').  Prefill is
+  // the eager callback (the a2a prefill's exact-count exchange is not a graph).  1 = off.
+  int dp_world = 1;
 };
 
 struct LoopResult {
@@ -118,9 +125,11 @@ class EngineLoop {
  public:
   // kind "decode": (B bucket, ctx bucket, -); "prefill": (row bucket, seq bucket, -)
   using GraphProvider = std::function<void(const std::string& kind, int a, int b, bool greedy)>;
+  // pad_rows > 0 (dp_world > 1): run exactly that many rows (the rest dummies), as every rank
+  // of an EP a2a group must
   using EagerPrefill = std::function<std::vector<int>(
       const std::vector<std::vector<int>>& prompts, const std::vector<std::vector<int>>& pages,
-      const std::vector<int>& starts, const std::vector<LoopSampling>& sampling)>;
+      const std::vector<int>& starts, const std::vector<LoopSampling>& sampling, int pad_rows)>;
 
   explicit EngineLoop(const LoopConfig& cfg);
   ~EngineLoop();
@@ -168,6 +177,7 @@ class EngineLoop {
     bool done = false;
     bool released = false;  // the caller gave up on it: drop it when it finishes
     std::string error;
+    int home = 0;           // dp_world > 1: the rank that holds this sequence
   };
   struct Chunk {  // a decode chunk in flight
     const DecodeGraphDesc* g = nullptr;
@@ -176,6 +186,7 @@ class EngineLoop {
     int buf = 0;        // pinned hist buffer index
     void* ev = nullptr;
     uint32_t mseq = 0;  // the group frame that launched it (follower status, mirror.h)
+    std::vector<std::vector<int64_t>> parts;  // dp_world > 1: follower f + 1's rows (ids)
   };
 
   void run();
@@ -186,6 +197,11 @@ class EngineLoop {
   void collect();  // read the oldest chunk in flight
   void drain();    // read every chunk in flight
   void fail_all(const std::string& why);
+  // dp_world > 1: the ids by home rank (index = rank), homes given to ids that have none
+  std::vector<std::vector<int64_t>> split_by_home(const std::vector<int64_t>& ids, bool assign);
+  // one rank's decode metadata (DecodeState layout) and sampler slots for `ids`
+  void decode_meta(const DecodeGraphDesc* g, const std::vector<int64_t>& ids, int32_t* m,
+                   float* tf, int32_t* tk, float* tp, int64_t* sd);
   [[noreturn]] void on_fault(int32_t* err, const char* where);
   void follower_check(uint32_t seq, const char* where);
   const DecodeGraphDesc* decode_graph(int B, int ctx, bool greedy);
@@ -232,6 +248,7 @@ class EngineLoop {
   std::vector<int64_t> loaded_ids_;
   int loaded_steps_ = 0;                          // replays since the last load
   int hist_buf_ = 0;
+  int home_rr_ = 0;  // dp_world > 1: rotating tie-break of home assignment
   static constexpr int kMaxFaultsInRow = 3;
   int faults_in_row_ = 0;  // consecutive steps that ended with a kernel fault word set
   int32_t* aux_err_ = nullptr;  // set_aux_fault

@@ -92,7 +92,17 @@ void MirrorSender::h2d(char kind, int a, int b, bool greedy, uint8_t field, cons
   head('H', kind, a, b, greedy);
   put<uint8_t>(field);
   put<uint32_t>((uint32_t)n);
-  buf_.append((const char*)src, n);
+  append((const char*)src, n);
+}
+
+void MirrorSender::tokens(char kind, int a, int b, bool greedy, uint8_t src, uint32_t s0,
+                          uint32_t k, uint32_t rows) {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  head('T', kind, a, b, greedy);
+  put<uint8_t>(src);
+  put<uint32_t>(s0);
+  put<uint32_t>(k);
+  put<uint32_t>(rows);
 }
 
 void MirrorSender::memset0(char kind, int a, int b, bool greedy, uint8_t field, size_t n) {
@@ -121,16 +131,18 @@ void MirrorSender::provide(char kind, int a, int b, bool greedy) {
 
 void MirrorSender::eager(const std::vector<std::vector<int>>& prompts,
                          const std::vector<std::vector<int>>& pages, const std::vector<int>& starts,
-                         const std::vector<LoopSampling>& samp) {
+                         const std::vector<LoopSampling>& samp, int pad_rows, bool want) {
   std::lock_guard<std::recursive_mutex> lk(mu_);
   put<char>('E');
   put<uint32_t>((uint32_t)prompts.size());
+  put<int32_t>(pad_rows);
+  put<uint8_t>(want ? 1 : 0);
   for (size_t i = 0; i < prompts.size(); ++i) {
     put<uint32_t>((uint32_t)prompts[i].size());
-    buf_.append((const char*)prompts[i].data(), prompts[i].size() * 4);
+    append((const char*)prompts[i].data(), prompts[i].size() * 4);
     const std::vector<int>& pg = i < pages.size() ? pages[i] : std::vector<int>();
     put<uint32_t>((uint32_t)pg.size());
-    buf_.append((const char*)pg.data(), pg.size() * 4);
+    append((const char*)pg.data(), pg.size() * 4);
     put<int32_t>(i < starts.size() ? starts[i] : 0);
     const LoopSampling s = i < samp.size() ? samp[i] : LoopSampling();
     put<float>(s.temperature);
@@ -142,26 +154,46 @@ void MirrorSender::eager(const std::vector<std::vector<int>>& prompts,
 
 void MirrorSender::stop() {
   std::lock_guard<std::recursive_mutex> lk(mu_);
+  target_ = -1;
   put<char>('S');
   flush();
 }
 
+// Every follower gets a frame whenever any has records (possibly empty), so frame numbers
+// stay the same on every follower.
 uint32_t MirrorSender::flush() {
   std::lock_guard<std::recursive_mutex> lk(mu_);
-  if (buf_.empty()) return 0;
-  const uint32_t n = (uint32_t)buf_.size();
-  std::string frame(reinterpret_cast<const char*>(&n), 4);
-  frame += buf_;
-  buf_.clear();
-  for (int fd : fds_) write_all(fd, frame.data(), frame.size());
+  target_ = -1;
+  bool any = false;
+  for (auto& b : bufs_) any |= !b.empty();
+  if (!any) return 0;
+  for (size_t f = 0; f < fds_.size(); ++f) {
+    const uint32_t n = (uint32_t)bufs_[f].size();
+    std::string frame(reinterpret_cast<const char*>(&n), 4);
+    frame += bufs_[f];
+    bufs_[f].clear();
+    write_all(fds_[f], frame.data(), frame.size());
+    bytes_ += (long)frame.size();
+  }
   frames_++;
-  bytes_ += (long)frame.size();
   return (uint32_t)frames_.load();
+}
+
+std::vector<int> MirrorSender::take_tokens(int f, uint32_t seq) {
+  std::lock_guard<std::recursive_mutex> lk(mu_);
+  std::vector<int> out;
+  if (f < 0 || (size_t)f >= toks_.size()) return out;
+  auto it = toks_[f].find(seq);
+  if (it == toks_[f].end()) return out;
+  out = std::move(it->second);
+  toks_[f].erase(it);
+  return out;
 }
 
 uint32_t MirrorSender::await(uint32_t seq, double timeout_s) {
   std::lock_guard<std::recursive_mutex> lk(mu_);
   if (acked_.size() != fds_.size()) acked_.assign(fds_.size(), 0);
+  if (toks_.size() != fds_.size()) toks_.resize(fds_.size());
   uint32_t bits = 0;
   const auto t0 = std::chrono::steady_clock::now();
   for (size_t f = 0; f < fds_.size(); ++f) {
@@ -174,9 +206,15 @@ uint32_t MirrorSender::await(uint32_t seq, double timeout_s) {
       if (r <= 0)
         throw std::runtime_error("group follower " + std::to_string(f + 1) +
                                  " did not report frame " + std::to_string(seq));
-      uint32_t rep[2];
+      uint32_t rep[3];
       if (!read_exact(fds_[f], (char*)rep, sizeof rep))
         throw std::runtime_error("group follower " + std::to_string(f + 1) + " is gone");
+      if (rep[2]) {  // the frame's tokens (dp groups)
+        std::vector<int> t(rep[2]);
+        if (!read_exact(fds_[f], (char*)t.data(), (size_t)rep[2] * 4))
+          throw std::runtime_error("group follower " + std::to_string(f + 1) + " is gone");
+        toks_[f][rep[0]] = std::move(t);
+      }
       acked_[f] = rep[0];
       bits |= rep[1];
     }
@@ -215,6 +253,8 @@ void EngineMirror::shutdown() {
   }
   if (rep_words_) h.hostFree(rep_words_);
   rep_words_ = nullptr;
+  if (rep_toks_) h.hostFree(rep_toks_);
+  rep_toks_ = nullptr;
   for (int i = 0; i < 2; ++i) {
     if (stage_[i]) h.hostFree(stage_[i]);
     if (stage_ev_[i]) h.eventDestroy(stage_ev_[i]);
@@ -241,6 +281,8 @@ void EngineMirror::add_decode_graph(const DecodeGraphDesc& d) {
   g.fields[kFTopp] = d.topp;
   g.fields[kFSeeds] = d.seeds;
   g.err = d.err;
+  g.hist = d.hist;
+  g.max_steps = d.max_steps;
   std::lock_guard<std::mutex> lk(gmu_);
   graphs_[std::make_tuple('D', g.a, g.b, g.greedy)] = g;
 }
@@ -258,6 +300,7 @@ void EngineMirror::add_prefill_graph(const PrefillGraphDesc& d) {
   g.fields[kFTopp] = d.topp;
   g.fields[kFSeeds] = d.seeds;
   g.err = d.err;
+  g.first = d.first;
   std::lock_guard<std::mutex> lk(gmu_);
   graphs_[std::make_tuple('P', g.a, g.b, g.greedy)] = g;
 }
@@ -299,7 +342,8 @@ std::map<std::string, double> EngineMirror::metrics() {
   return m;
 }
 
-uint32_t EngineMirror::apply(const std::string& frame, std::vector<int32_t*>* launched) {
+uint32_t EngineMirror::apply(const std::string& frame, std::vector<int32_t*>* launched,
+                             FrameOut* out) {
   const HipApi& h = hip_api();
   // h2d payloads of this frame go through one pinned staging buffer (copied up front)
   char* st = (char*)staging(frame.size());
@@ -322,6 +366,8 @@ uint32_t EngineMirror::apply(const std::string& frame, std::vector<int32_t*>* la
       }
       if (op == 'E') {
         const uint32_t n = r.get<uint32_t>();
+        const int32_t pad = r.get<int32_t>();
+        const bool want = r.get<uint8_t>() != 0;
         std::vector<std::vector<int>> prompts, pages;
         std::vector<int> starts;
         std::vector<LoopSampling> samp;
@@ -338,7 +384,8 @@ uint32_t EngineMirror::apply(const std::string& frame, std::vector<int32_t*>* la
         }
         if (!eager_) throw std::runtime_error("mirror: no eager prefill callback");
         hip_check(h.streamSynchronize(stream_), "mirror sync");  // the model code runs on its stream
-        eager_(prompts, pages, starts, samp);
+        std::vector<int> first = eager_(prompts, pages, starts, samp, pad);
+        if (want) out->host.insert(out->host.end(), first.begin(), first.end());
         n_eager_++;
         continue;
       }
@@ -354,6 +401,19 @@ uint32_t EngineMirror::apply(const std::string& frame, std::vector<int32_t*>* la
         continue;
       }
       Graph* g = find(kind, a, b, greedy);
+      if (op == 'T') {  // this rank's tokens go back with the frame's status (dp groups)
+        const uint8_t src = r.get<uint8_t>();
+        const uint32_t s0 = r.get<uint32_t>(), k = r.get<uint32_t>(), rows = r.get<uint32_t>();
+        if (src == 0) {
+          if (!g->hist || (int)(s0 + k) > g->max_steps || (int)rows > g->a)
+            throw std::runtime_error("mirror: bad decode token record");
+          out->copies.push_back(TokCopy{g->hist + s0, (size_t)g->max_steps, rows, k});
+        } else {
+          if (!g->first || (int)rows > g->b) throw std::runtime_error("mirror: bad prefill token record");
+          out->copies.push_back(TokCopy{g->first, 1, rows, 1});
+        }
+        continue;
+      }
       if (op == 'H') {
         const uint8_t f = r.get<uint8_t>();
         const uint32_t n = r.get<uint32_t>();
@@ -398,7 +458,8 @@ uint32_t EngineMirror::apply(const std::string& frame, std::vector<int32_t*>* la
 
 // Queue the frame's status: its launched graphs' fault words and the split-K word are
 // copied to a pinned slot behind the frame's work; reporter() answers once that landed.
-void EngineMirror::report(uint32_t seq, const std::vector<int32_t*>& launched, uint32_t host_bits) {
+void EngineMirror::report(uint32_t seq, const std::vector<int32_t*>& launched, uint32_t host_bits,
+                          const FrameOut& out) {
   const HipApi& h = hip_api();
   std::unique_lock<std::mutex> lk(rmu_);
   const int slot = rep_next_;
@@ -419,9 +480,28 @@ void EngineMirror::report(uint32_t seq, const std::vector<int32_t*>& launched, u
     hip_check(h.memcpyAsync(w + nw++, e, 4, kD2H, stream_), "mirror status D2H");
   }
   if (aux_err_) hip_check(h.memcpyAsync(w + nw++, aux_err_, 4, kD2H, stream_), "mirror status D2H");
+  // the frame's tokens: host ones first (eager prefill), then the device rows, packed
+  int nt = 0;
+  if (!out.host.empty() || !out.copies.empty()) {
+    if (!rep_toks_) hip_check(h.hostMalloc((void**)&rep_toks_, (size_t)kRep * kRepToks * 4, 0), "mirror tokens");
+    int32_t* t = rep_toks_ + (size_t)slot * kRepToks;
+    for (int v : out.host) {
+      if (nt >= kRepToks) throw std::runtime_error("mirror: frame tokens exceed the report slot");
+      t[nt++] = v;
+    }
+    for (const TokCopy& c : out.copies) {
+      if (nt + (size_t)c.rows * c.k > (size_t)kRepToks)
+        throw std::runtime_error("mirror: frame tokens exceed the report slot");
+      if (c.rows)
+        hip_check(h.memcpy2DAsync(t + nt, (size_t)c.k * 4, c.src, c.pitch * 4, (size_t)c.k * 4, c.rows,
+                                  kD2H, stream_),
+                  "mirror tokens D2H");
+      nt += (int)(c.rows * c.k);
+    }
+  }
   hip_check(h.eventRecord(rep_ev_[slot], stream_), "mirror status event");
   lk.lock();
-  rq_.push_back(Report{seq, host_bits, slot, nw});
+  rq_.push_back(Report{seq, host_bits, slot, nw, nt});
   lk.unlock();
   rcv_.notify_all();
 }
@@ -443,14 +523,17 @@ void EngineMirror::reporter() {
     for (int i = 0; i < rp.nwords; ++i)
       if (rep_words_[(size_t)rp.slot * kRepWords + i] != 0) bits |= 1;
     if (bits & 1) n_faults_++;
+    std::string msg(12 + (size_t)rp.ntok * 4, '\0');
+    const uint32_t head[3] = {rp.seq, bits, (uint32_t)rp.ntok};
+    memcpy(&msg[0], head, 12);
+    if (rp.ntok) memcpy(&msg[12], rep_toks_ + (size_t)rp.slot * kRepToks, (size_t)rp.ntok * 4);
     {
-      std::lock_guard<std::mutex> lk(rmu_);
+      std::lock_guard<std::mutex> lk(rmu_);  // the slot (and its tokens) is free after the copy
       rep_busy_[rp.slot] = false;
     }
     rcv_.notify_all();
-    const uint32_t msg[2] = {rp.seq, bits};
     try {
-      write_all(fd_, (const char*)msg, sizeof msg);
+      write_all(fd_, msg.data(), msg.size());
     } catch (const std::exception&) {  // the leader is gone: nothing to tell
     }
   }
@@ -478,16 +561,17 @@ std::string EngineMirror::run() {
       n_frames_++;
       ++seq;
       launched.clear();
+      FrameOut fout;
       uint32_t host_bits;
       try {
-        host_bits = apply(frame, &launched);
+        host_bits = apply(frame, &launched, &fout);
       } catch (const std::string&) {  // stop
         hip_check(h.streamSynchronize(stream_), "mirror drain");
         return "";
       }
       if (!launched.empty() && ++launch_frames_ == inject_at_ && aux_err_)
         hip_check(h.memsetAsync(aux_err_, 1, 4, stream_), "mirror fault injection");
-      report(seq, launched, host_bits);
+      report(seq, launched, host_bits, fout);
     }
   } catch (const std::exception& e) {
     return e.what();

@@ -25,9 +25,18 @@
 //   'L' launch   kind a b greedy which count        (which 0: one-step exec, 1: exec_k)
 //   'F' faults                                      (zero every graph's fault word)
 //   'V' provide  kind a b greedy                    (capture + register this shape)
-//   'E' eager    n_seq {prompt, pages, start, sampling} x n_seq
+//   'E' eager    n_seq pad_rows want {prompt, pages, start, sampling} x n_seq
+//   'T' tokens   kind a b greedy src s0 k rows    (dp groups: send back hist[rows][s0 .. s0+k)
+//                                                  of a decode graph, src 0, or the first
+//                                                  tokens of a prefill graph, src 1)
 //   'S' stop
 // kind: 'D' decode graph (B, ctx bucket), 'P' prefill graph (rows, seq bucket).
+//
+// EP all-to-all groups (DP attention, LoopConfig::dp_world): the ranks hold different
+// sequences, so a frame is per follower -- the shared records (launches, counter resets,
+// captures) go to every follower, the metadata / sampling / eager-prefill records of a
+// follower's own share only to it (MirrorSender::set_target) -- and the status answer of a
+// frame carries that follower's tokens ('T' records, an 'E' record with want = 1).
 //
 // Status back channel (a kernel fault is local to the rank that saw it): for
 // every frame a follower answers on the same socket, once the device work the frame
@@ -38,6 +47,7 @@
 // reads the answers of every frame up to a step's before it hands that step's tokens out
 // (MirrorSender::await), so a fault on any rank fails the step on the leader too; its
 // fault record ('F') clears every graph word and the split-K word on the followers.
+// Answer: {u32 seq, u32 bits, u32 ntok, i32 tok[ntok]} (ntok = 0 unless the frame asked).
 #pragma once
 #include <stdint.h>
 
@@ -68,7 +78,11 @@ enum MirrorField : uint8_t {
 
 class MirrorSender {
  public:
-  explicit MirrorSender(std::vector<int> fds) : fds_(std::move(fds)) {}
+  explicit MirrorSender(std::vector<int> fds) : fds_(std::move(fds)), bufs_(fds_.size()) {}
+  // records from here on go to follower f only (0-based; -1: every follower, the default)
+  void set_target(int f) { target_ = f; }
+  void tokens(char kind, int a, int b, bool greedy, uint8_t src, uint32_t s0, uint32_t k,
+              uint32_t rows);
   void h2d(char kind, int a, int b, bool greedy, uint8_t field, const void* src, size_t n);
   void memset0(char kind, int a, int b, bool greedy, uint8_t field, size_t n);
   void launch(char kind, int a, int b, bool greedy, uint8_t which, uint32_t count);
@@ -76,7 +90,7 @@ class MirrorSender {
   void provide(char kind, int a, int b, bool greedy);
   void eager(const std::vector<std::vector<int>>& prompts,
              const std::vector<std::vector<int>>& pages, const std::vector<int>& starts,
-             const std::vector<LoopSampling>& samp);
+             const std::vector<LoopSampling>& samp, int pad_rows = 0, bool want = false);
   void stop();
   // one frame to every follower; returns its sequence number (1, 2, ...; 0 if nothing was
   // pending); throws if a channel is broken
@@ -84,6 +98,8 @@ class MirrorSender {
   // the OR of every follower's status bits over the frames up to `seq` (blocks until each
   // follower answered them; throws if a follower is gone or silent past timeout_s)
   uint32_t await(uint32_t seq, double timeout_s = 120.0);
+  // the tokens follower f sent back with frame seq (after await(seq); empty if none)
+  std::vector<int> take_tokens(int f, uint32_t seq);
   long frames() const { return frames_; }
   long bytes() const { return bytes_; }
   long follower_faults() const { return follower_faults_; }
@@ -92,11 +108,20 @@ class MirrorSender {
   void head(char op, char kind, int a, int b, bool greedy);
   template <class T>
   void put(T v) {
-    buf_.append(reinterpret_cast<const char*>(&v), sizeof(T));
+    append(reinterpret_cast<const char*>(&v), sizeof(T));
+  }
+  void append(const char* p, size_t n) {
+    if (target_ >= 0) {
+      bufs_[target_].append(p, n);
+    } else {
+      for (auto& b : bufs_) b.append(p, n);
+    }
   }
   std::vector<int> fds_;
   std::vector<uint32_t> acked_;  // per follower: the last frame it answered
-  std::string buf_;
+  std::vector<std::string> bufs_;  // per follower: its pending frame
+  int target_ = -1;
+  std::vector<std::map<uint32_t, std::vector<int>>> toks_;  // per follower: frame -> tokens
   std::recursive_mutex mu_;
   std::atomic<long> frames_{0}, bytes_{0}, follower_faults_{0};
 };
@@ -132,12 +157,27 @@ class EngineMirror {
     void* exec_k = nullptr;
     void* fields[7] = {};
     int32_t* err = nullptr;
+    int32_t* hist = nullptr;   // decode: [B][max_steps] tokens by step
+    int max_steps = 0;
+    int32_t* first = nullptr;  // prefill: [n_seq] first tokens
+  };
+  // what a frame sends back besides its status bits: device token rows to copy (after the
+  // frame's work) and tokens the host already has (an eager prefill's first tokens)
+  struct TokCopy {
+    const int32_t* src;
+    size_t pitch;  // int32 elements between rows
+    uint32_t rows, k;
+  };
+  struct FrameOut {
+    std::vector<TokCopy> copies;
+    std::vector<int> host;
   };
   Graph* find(char kind, int a, int b, bool greedy);
   // applies one frame; returns the host failure bit (the frame's remaining records skipped)
-  uint32_t apply(const std::string& frame, std::vector<int32_t*>* launched);
+  uint32_t apply(const std::string& frame, std::vector<int32_t*>* launched, FrameOut* out);
   void* staging(size_t n);
-  void report(uint32_t seq, const std::vector<int32_t*>& launched, uint32_t host_bits);
+  void report(uint32_t seq, const std::vector<int32_t*>& launched, uint32_t host_bits,
+              const FrameOut& out);
   void reporter();
 
   int fd_, device_;
@@ -155,12 +195,13 @@ class EngineMirror {
   int32_t* aux_err_ = nullptr;
   long inject_at_ = 0, launch_frames_ = 0;
   // status reports: a ring of pinned word slots + events, drained in order by reporter()
-  static constexpr int kRep = 32, kRepWords = 16;
+  static constexpr int kRep = 32, kRepWords = 16, kRepToks = 8192;
   struct Report {
     uint32_t seq, host_bits;
-    int slot, nwords;
+    int slot, nwords, ntok;
   };
   int32_t* rep_words_ = nullptr;  // [kRep][kRepWords] pinned
+  int32_t* rep_toks_ = nullptr;   // [kRep][kRepToks] pinned: the frame's tokens
   void* rep_ev_[kRep] = {};
   bool rep_busy_[kRep] = {};
   int rep_next_ = 0;

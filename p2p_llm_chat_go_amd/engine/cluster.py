@@ -411,9 +411,10 @@ def _leader_main(spec, replica, eng, parent_conn, follower_conns):
         # channels carry the leader loop's frames from now on, runtime/mirror.h)
         for c in follower_conns:
             c.send(("mirror", PREFILL_CTX))
+        # (EP a2a: every rank serves its own sequences, dp_world = the group)
         server = NativeEngineServer(eng, tok, mirror_fds=[c.fileno() for c in follower_conns],
-                                    **kw)
-    else:  # EP a2a (DP attention): the Python loop, whose calls the leader broadcasts
+                                    dp_world=group if split else 1, **kw)
+    else:  # the Python loop (ENGINE_NATIVE_LOOP=0, CPU engines): the leader broadcasts its calls
         server = EngineServer(front, tok, **kw)
     send_lock = threading.Lock()
     cancelled = set()

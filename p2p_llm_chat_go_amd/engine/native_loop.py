@@ -16,8 +16,9 @@ Prompts longer than the largest prefill bucket fall back to Python's chunked pre
 (``eager``).  Used for single-GPU replicas (TP = EP = 1) when the engine runs its graphs
 on a GPU (``ENGINE_NATIVE_LOOP``, default on), and for TP / EP groups: the leader's loop
 records its device operations and the followers' ``EngineMirror`` threads replay them
-(``run_follower_mirror``, ``csrc/runtime/mirror.h``); only the EP a2a mode (DP attention,
-per-rank sequences) keeps the Python loop and its pickled broadcast.
+(``run_follower_mirror``, ``csrc/runtime/mirror.h``) -- the EP a2a mode (DP attention,
+per-rank sequences) included: each rank's share travels in its own frame
+(``LoopConfig::dp_world``).
 """
 from __future__ import annotations
 
@@ -48,7 +49,7 @@ class NativeEngineServer(EngineServer):
                  max_batch: int | None = None, decode_chunk: int = 8,
                  default_max_tokens: int = 128, max_ctx: int | None = None,
                  prewarm: bool = True, prefill_ctx: int | None = None,
-                 mirror_fds: list | None = None):
+                 mirror_fds: list | None = None, dp_world: int = 1):
         # no Python engine thread: the EngineServer state this class uses is set here
         self.engine = engine
         self.tok = tokenizer or get_tokenizer(engine.cfg)
@@ -69,7 +70,10 @@ class NativeEngineServer(EngineServer):
             "eos": [int(e) for e in engine.cfg.eos_ids], "decode_chunk": decode_chunk,
             "admit_wait_us": float(os.environ.get("ENGINE_ADMIT_WAIT_US", "500")),
             "prefill_first": os.environ.get("ENGINE_PREFILL_FIRST", "1") != "0",
-            "mixed": True, "pipeline": os.environ.get("ENGINE_PIPELINE", "1") != "0",
+            # EP a2a groups (dp_world > 1: DP attention, per-rank sequences) prefill each
+            # rank's share eagerly, padded to the largest share; no riders
+            "mixed": dp_world <= 1, "dp_world": int(dp_world),
+            "pipeline": os.environ.get("ENGINE_PIPELINE", "1") != "0",
             # every running sequence rides in a prompt chunk (ENGINE_RIDERS=tile: only the
             # last 64-row tile's free rows): +4 % at 32 peers, +16 % at 64, same at 8
             # (profiles/r4_serve_native_vs_python.jsonl)
@@ -91,6 +95,7 @@ class NativeEngineServer(EngineServer):
 
             self.loop.set_aux_fault(split_fault_word(dev))
         self.group = 1 + len(mirror_fds or ())
+        self.dp_world = int(dp_world)
         self.loop.set_provider(self._provide)
         self.loop.set_eager_prefill(self._eager_prefill)
         self._registered = set()
@@ -128,6 +133,8 @@ class NativeEngineServer(EngineServer):
         for B in batches or [b for b in BATCH_BUCKETS if b <= self.max_batch]:
             self._provide("decode", B, 256, True)
         eng = self.engine
+        if self.dp_world > 1:
+            return  # prompt chunks run eagerly in EP a2a groups (no prefill graphs)
         if mode == "basic":
             seqs, rows = [1], rows or (16, 32, 48, 64, 96, 128)
         else:
@@ -139,10 +146,11 @@ class NativeEngineServer(EngineServer):
                 if sb <= r <= min(eng.max_prefill_tokens, eng.prefill_graph_max_rows):
                     self._provide("prefill", r, sb, True)
 
-    def _eager_prefill(self, prompts, pages, starts, samp):
+    def _eager_prefill(self, prompts, pages, starts, samp, pad_rows=0):
         params = [SamplingParams(temperature=t, top_k=k, top_p=p, seed=s) for t, k, p, s in samp]
-        first = self.engine.prefill(prompts, pages, sampling=params,
-                                    starts=starts if any(starts) else None, graph=False)
+        first = self.engine.prefill(prompts, pages, sampling=params or None,
+                                    starts=starts if any(starts) else None, graph=False,
+                                    pad_rows=pad_rows or None)
         return [int(x) for x in first.cpu().tolist()]
 
     # --------------------------------------------------------------- API
@@ -296,10 +304,12 @@ def capture_for_loop(eng: Engine, kind: str, a: int, b: int, greedy: bool, prefi
 
 def group_native_ok(engine: Engine, dp_split: bool) -> bool:
     """A TP / EP group serves on the native loop (leader) + mirrors (followers) when its
-    engines run graphs on GPUs and every rank serves the same sequences (not the EP a2a
-    mode's DP attention, whose ranks hold different sequences)."""
-    return (not dp_split and engine.device.type == "cuda" and engine.use_graph
-            and engine.prefill_graphs_enabled
+    engines run graphs on GPUs.  The EP a2a mode (DP attention, dp_split: the ranks hold
+    different sequences) runs there too since round 6 -- each rank's share in its own frame,
+    the followers' tokens back on the status channel (LoopConfig::dp_world); its prompt
+    chunks prefill eagerly, so it does not need prefill graphs."""
+    return (engine.device.type == "cuda" and engine.use_graph
+            and (dp_split or engine.prefill_graphs_enabled)
             and os.environ.get("ENGINE_NATIVE_LOOP", "1") != "0")
 
 
@@ -315,10 +325,11 @@ def run_follower_mirror(engine: Engine, fd: int, prefill_ctx: int) -> None:
         desc = capture_for_loop(engine, kind, a, b, greedy, prefill_ctx)
         (m.add_decode_graph if kind == "decode" else m.add_prefill_graph)(desc)
 
-    def eager(prompts, pages, starts, samp):
+    def eager(prompts, pages, starts, samp, pad_rows=0):
         params = [SamplingParams(temperature=t, top_k=k, top_p=p, seed=s) for t, k, p, s in samp]
-        first = engine.prefill(prompts, pages, sampling=params,
-                               starts=starts if any(starts) else None, graph=False)
+        first = engine.prefill(prompts, pages, sampling=params or None,
+                               starts=starts if any(starts) else None, graph=False,
+                               pad_rows=pad_rows or None)
         return [int(x) for x in first.cpu().tolist()]
 
     m.set_provider(provide)
