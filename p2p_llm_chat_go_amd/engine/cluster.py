@@ -171,14 +171,17 @@ class LockstepEngine:
     def _decode_split(self, last_ids, pos, block_tables, ctx, k, params):
         parts = self._parts(block_tables, decode=True)
         bmax = max(1, max(len(p) for p in parts))
+        # one graph kind for the whole group (every rank replays the same graph)
+        greedy = params is None or all(p.greedy for p in params)
         for r, c in enumerate(self._conns, start=1):
             idx = parts[r]
             c.send(("decode_part", self._sub(last_ids, idx), self._sub(pos, idx),
-                    self._sub(block_tables, idx), ctx, k, self._sub(params, idx), bmax))
+                    self._sub(block_tables, idx), ctx, k, self._sub(params, idx), bmax,
+                    greedy))
         idx = parts[0]
         mine = self._eng.decode_steps(self._sub(last_ids, idx), self._sub(pos, idx),
                                       self._sub(block_tables, idx), ctx, k,
-                                      self._sub(params, idx), batch_bucket=bmax)
+                                      self._sub(params, idx), batch_bucket=bmax, greedy=greedy)
         results = [mine] + [self._recv(c) for c in self._conns]
         hist = [None] * len(last_ids)
         for part, res in zip(parts, results):
@@ -298,9 +301,9 @@ def _follower_loop(eng, conn):
             res = (res[0].cpu(), res[1].cpu()) if ret else res.cpu()
             conn.send(("part", res))
         elif op == "decode_part":
-            _, ids, pos, bts, ctx, k, params, bmax = msg
+            _, ids, pos, bts, ctx, k, params, bmax, greedy = msg
             conn.send(("part", eng.decode_steps(ids, pos, bts, ctx, k, params,
-                                                batch_bucket=bmax)))
+                                                batch_bucket=bmax, greedy=greedy)))
         if eng.device.type == "cuda":
             import torch
 

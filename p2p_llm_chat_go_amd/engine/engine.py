@@ -347,15 +347,23 @@ class Engine:
 
     # --------------------------------------------------------------- decode
     def decode_steps(self, last_ids: list, pos: list, block_tables: list, ctx: int, k: int,
-                     params: list | None = None, batch_bucket: int | None = None) -> list:
+                     params: list | None = None, batch_bucket: int | None = None,
+                     greedy: bool | None = None) -> list:
         """k decode steps for running sequences (continuous batching): row b continues
         from token ``last_ids[b]`` at position ``pos[b]`` in its pages; ``params`` =
         per-row SamplingParams (None / all greedy: the fused-argmax graph).  Returns the
         k new tokens of every row (host lists).  Every TP/EP rank makes the same call
         (engine.cluster broadcasts it), so the graphs' collectives line up.
         batch_bucket: run the graph of this many rows (>= len(last_ids); DP-attention EP
-        ranks with different batches must replay the same bucket)."""
-        greedy = params is None or all(p.greedy for p in params)
+        ranks with different batches must replay the same bucket).
+        greedy: the graph kind when the caller decides it for the whole group (DP-attention
+        shares: one rank's all-greedy share still replays the sampled graph when another
+        rank's share samples -- a graph kind captured on one rank only would run its capture
+        warmup's collectives alone)."""
+        if greedy is None:
+            greedy = params is None or all(p.greedy for p in params)
+        elif not greedy and params is None:
+            params = []
         g = self.decode_graph(max(len(last_ids), batch_bucket or 1), ctx, greedy=greedy)
         st = g.state
         st.load(last_ids, pos, block_tables)
