@@ -58,6 +58,9 @@ std::atomic<int> g_bad{0};
 // fault injection on a follower rank (run_group_faults): the next follower decode replay
 // sets its graph's fault word; the next follower eager prefill raises
 std::atomic<int> g_follower_fault{0}, g_follower_eager_fail{0};
+// a collective timeout (run_coll_fault): the next decode replay sets the collective word
+std::atomic<int> g_coll_trigger{0};
+int32_t g_coll_word = 0;
 
 template <int I>
 int tramp() { return g_slot[I](); }
@@ -102,6 +105,7 @@ struct DecodeGraph {
       const int B = d.B, S = d.max_steps, s = step[0];
       launches++;
       if (follower && g_follower_fault.exchange(0)) errw[0] = 1;
+      if (g_coll_trigger.exchange(0)) g_coll_word = 1;
       trace = mix(trace, (uint64_t)s);
       for (int32_t v : meta) trace = mix(trace, (uint64_t)(uint32_t)v);
       if (s >= S) {
@@ -764,6 +768,57 @@ int run_remote() {
 
 }  // namespace
 
+// A collective timeout (the IPC kernels' error word, EngineLoop::set_coll_fault) is not a
+// transient fault: the request in flight fails with the reason and the replica is dead.
+int run_coll_fault() {
+  LoopConfig c;
+  c.num_pages = 256;
+  c.max_batch = 4;
+  c.max_prefill_tokens = 256;
+  c.max_ctx = 2048;
+  c.eos = {EOS};
+  c.decode_chunk = 4;
+  c.row_buckets = {16, 32, 48, 64, 96, 128, 192, 256};
+  c.prefill_max_pages = PREFILL_PAGES;
+  c.prefill_graph_after = 1;
+  EngineLoop loop(c);
+  std::vector<std::unique_ptr<DecodeGraph>> dg;
+  std::vector<std::unique_ptr<PrefillGraph>> pg;
+  loop.set_provider([&](const std::string& kind, int a, int b, bool) {
+    if (kind == "decode") {
+      dg.emplace_back(new DecodeGraph(a, b));
+      loop.add_decode_graph(dg.back()->d);
+    } else {
+      pg.emplace_back(new PrefillGraph(a, b));
+      loop.add_prefill_graph(pg.back()->d);
+    }
+  });
+  loop.set_coll_fault(reinterpret_cast<uintptr_t>(&g_coll_word));
+  loop.start();
+  int failures = 0;
+  LoopResult r;
+  int64_t id = loop.submit({1, 2, 3, 4, 5}, 12, false, LoopSampling());
+  if (!loop.wait(id, 30.0, &r) || !r.error.empty()) failures++;  // clean
+  loop.release(id);
+  g_coll_trigger = 1;
+  id = loop.submit({6, 7, 8}, 12, false, LoopSampling());
+  loop.wait(id, 30.0, &r);
+  loop.release(id);
+  if (r.error.find("collective timeout") == std::string::npos) {
+    failures++;
+    std::fprintf(stderr, "coll fault: request error '%s'\n", r.error.c_str());
+  }
+  const std::string dead = loop.dead();
+  if (dead.find("collective timeout") == std::string::npos) {
+    failures++;
+    std::fprintf(stderr, "coll fault: replica not dead ('%s')\n", dead.c_str());
+  }
+  loop.shutdown();
+  g_coll_word = 0;
+  std::printf("coll fault: failures=%d dead='%s'\n", failures, dead.c_str());
+  return failures == 0 ? 0 : 1;
+}
+
 int main() {
   hip_api_use_host_fake();
   int rc = 0;
@@ -773,6 +828,7 @@ int main() {
   rc |= run_group();
   rc |= run_group_faults();
   rc |= run_group_dp();
+  rc |= run_coll_fault();
   rc |= run_remote();
   if (rc == 0) std::printf("LOOP_SELFTEST_OK\n");
   return rc;

@@ -195,6 +195,7 @@ void bind_engine_loop(py::module_& m) {
       // TP / EP group leader: record every device operation for the followers (mirror.h)
       .def("set_mirror", &EngineLoop::set_mirror)
       .def("set_aux_fault", &EngineLoop::set_aux_fault, py::arg("word"))
+      .def("set_coll_fault", &EngineLoop::set_coll_fault, py::arg("word"))
       .def("serve", &EngineLoop::serve, py::arg("name"))
       .def("mirror_provide", &EngineLoop::mirror_provide, py::call_guard<py::gil_scoped_release>())
       .def("start", &EngineLoop::start, py::call_guard<py::gil_scoped_release>())
@@ -261,6 +262,7 @@ void bind_engine_loop(py::module_& m) {
       .def("set_provider", [](EngineMirror& M, py::function f) { M.set_provider(py_provider(f)); })
       .def("set_eager_prefill", [](EngineMirror& M, py::function f) { M.set_eager_prefill(py_eager(f)); })
       .def("set_aux_fault", &EngineMirror::set_aux_fault, py::arg("word"))
+      .def("set_coll_fault", &EngineMirror::set_coll_fault, py::arg("word"))
       .def("run", &EngineMirror::run, py::call_guard<py::gil_scoped_release>())
       .def("metrics", &EngineMirror::metrics)
       .def("shutdown", &EngineMirror::shutdown, py::call_guard<py::gil_scoped_release>());

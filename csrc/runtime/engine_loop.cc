@@ -26,7 +26,8 @@ enum Slot : int {
   kSampP = 10,
   kSampS = 11,
   kAux0 = 12,  // kAux0, kAux0 + 1: split-K fault word per decode buffer; kAux0 + 2 prefill
-  kSlots = 15,
+  kColl0 = 15,  // the same three for the IPC collectives' timeout word (set_coll_fault)
+  kSlots = 18,
 };
 
 }  // namespace
@@ -797,7 +798,10 @@ void EngineLoop::run_prefill(const std::vector<int64_t>& admitted) {
     if (g->err) hip_check(h.memcpyAsync(ew, g->err, 4, kD2H, stream_), "fault word D2H");
     int32_t* ea = (int32_t*)pinned(kAux0 + 2, 4);
     if (aux_err_) hip_check(h.memcpyAsync(ea, aux_err_, 4, kD2H, stream_), "split fault D2H");
+    int32_t* ec = (int32_t*)pinned(kColl0 + 2, 4);
+    if (coll_err_) hip_check(h.memcpyAsync(ec, coll_err_, 4, kD2H, stream_), "collective fault D2H");
     hip_check(h.streamSynchronize(stream_), "prefill sync");
+    if (coll_err_ && *ec != 0) on_coll_fault("prefill");
     if (g->err && *ew != 0) on_fault(g->err, "prefill");
     if (aux_err_ && *ea != 0) on_fault(aux_err_, "prefill (split-K)");
     follower_check(pf_seq, "prefill");
@@ -939,6 +943,8 @@ void EngineLoop::launch_chunk(const DecodeGraphDesc* g, const std::vector<int64_
     hip_check(h.memcpyAsync(pinned(kErr0 + c.buf, 4), g->err, 4, kD2H, stream_), "fault D2H");
   if (aux_err_)
     hip_check(h.memcpyAsync(pinned(kAux0 + c.buf, 4), aux_err_, 4, kD2H, stream_), "split fault D2H");
+  if (coll_err_)
+    hip_check(h.memcpyAsync(pinned(kColl0 + c.buf, 4), coll_err_, 4, kD2H, stream_), "collective fault D2H");
   c.ev = events_[c.buf];
   hip_check(h.eventRecord(c.ev, stream_), "hipEventRecord");
   loaded_steps_ += k;
@@ -951,6 +957,10 @@ void EngineLoop::collect() {
   Chunk c = std::move(flight_.front());
   flight_.pop_front();
   hip_check(h.eventSynchronize(c.ev), "decode chunk sync");
+  if (coll_err_ && *(int32_t*)pinned_[kColl0 + c.buf].first != 0) {
+    flight_.clear();
+    on_coll_fault("decode");
+  }
   if (c.g->err && *(int32_t*)pinned_[kErr0 + c.buf].first != 0) {
     flight_.clear();  // chunks behind a faulted one ran on its invalid state
     on_fault(c.g->err, "decode");
@@ -1030,6 +1040,23 @@ void EngineLoop::on_fault(int32_t* err, const char* where) {
   if (++faults_in_row_ >= kMaxFaultsInRow) {
     std::lock_guard<std::mutex> lk(mu_);
     dead_ = why + ", " + std::to_string(faults_in_row_) + " steps in a row";
+  }
+  throw std::runtime_error(why);
+}
+
+// An IPC collective gave up waiting for a peer (parallel/custom_ar.py CollectiveTimeout):
+// the group's epochs are out of step and later calls skip their waits, so every number from
+// here on is wrong.  Unlike a split-K fault this is not transient: the replica is dead (the
+// Python loop raises the same from LlamaModel.check_faults).
+void EngineLoop::on_coll_fault(const char* where) {
+  const HipApi& h = hip_api();
+  (void)h.streamSynchronize(stream_);
+  loaded_ = nullptr;
+  const std::string why = std::string("collective timeout during ") + where +
+                          ": a peer rank never arrived (the TP / EP group is broken)";
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    dead_ = why;
   }
   throw std::runtime_error(why);
 }

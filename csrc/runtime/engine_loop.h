@@ -147,6 +147,8 @@ class EngineLoop {
   // A second device fault word checked with every graph's own: the kernels' split-K word
   // (p2p_split_fault_word_ptr), which the graphs' split-K GEMMs set when a slice gives up.
   void set_aux_fault(uintptr_t word) { aux_err_ = reinterpret_cast<int32_t*>(word); }
+  // the IPC collectives' timeout word (CustomAllReduce.err[0]): nonzero = the group is broken
+  void set_coll_fault(uintptr_t word) { coll_err_ = reinterpret_cast<int32_t*>(word); }
   // a graph provider about to capture (kind, a, b, greedy): the followers capture it too
   void mirror_provide(const std::string& kind, int a, int b, bool greedy);
   // serve requests from other processes on the abstract unix socket @name (the node of a
@@ -203,6 +205,7 @@ class EngineLoop {
   void decode_meta(const DecodeGraphDesc* g, const std::vector<int64_t>& ids, int32_t* m,
                    float* tf, int32_t* tk, float* tp, int64_t* sd);
   [[noreturn]] void on_fault(int32_t* err, const char* where);
+  [[noreturn]] void on_coll_fault(const char* where);
   void follower_check(uint32_t seq, const char* where);
   const DecodeGraphDesc* decode_graph(int B, int ctx, bool greedy);
   const PrefillGraphDesc* find_prefill_graph(int rows, int nseq, bool greedy);
@@ -252,6 +255,7 @@ class EngineLoop {
   static constexpr int kMaxFaultsInRow = 3;
   int faults_in_row_ = 0;  // consecutive steps that ended with a kernel fault word set
   int32_t* aux_err_ = nullptr;  // set_aux_fault
+  int32_t* coll_err_ = nullptr;  // set_coll_fault
 
   // metrics
   std::atomic<long> n_requests_{0}, n_tokens_{0}, n_prefill_calls_{0}, n_decode_calls_{0},

@@ -476,10 +476,11 @@ void EngineMirror::report(uint32_t seq, const std::vector<int32_t*>& launched, u
   int32_t* w = rep_words_ + (size_t)slot * kRepWords;
   int nw = 0;
   for (int32_t* e : launched) {
-    if (nw >= kRepWords - 1) break;
+    if (nw >= kRepWords - 2) break;
     hip_check(h.memcpyAsync(w + nw++, e, 4, kD2H, stream_), "mirror status D2H");
   }
   if (aux_err_) hip_check(h.memcpyAsync(w + nw++, aux_err_, 4, kD2H, stream_), "mirror status D2H");
+  if (coll_err_) hip_check(h.memcpyAsync(w + nw++, coll_err_, 4, kD2H, stream_), "mirror status D2H");
   // the frame's tokens: host ones first (eager prefill), then the device rows, packed
   int nt = 0;
   if (!out.host.empty() || !out.copies.empty()) {

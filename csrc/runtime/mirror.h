@@ -142,6 +142,9 @@ class EngineMirror {
   // this device's split-K fault word (p2p_split_fault_word_ptr): reported and cleared like
   // the graphs' own words
   void set_aux_fault(uintptr_t word) { aux_err_ = reinterpret_cast<int32_t*>(word); }
+  // the IPC collectives' timeout word: reported with every frame, never reset by 'F' (a
+  // collective timeout breaks the group; the leader fails steps until the replica is dead)
+  void set_coll_fault(uintptr_t word) { coll_err_ = reinterpret_cast<int32_t*>(word); }
   // Applies frames until the leader's stop ("" returned) or a failure (its description:
   // a closed channel, an unknown graph, a HIP error).  Blocking; call without the GIL.
   std::string run();
@@ -193,6 +196,7 @@ class EngineMirror {
   void* stage_ev_[2] = {nullptr, nullptr};
   int cur_ = 0;
   int32_t* aux_err_ = nullptr;
+  int32_t* coll_err_ = nullptr;
   long inject_at_ = 0, launch_frames_ = 0;
   // status reports: a ring of pinned word slots + events, drained in order by reporter()
   static constexpr int kRep = 32, kRepWords = 16, kRepToks = 8192;

@@ -94,6 +94,9 @@ class NativeEngineServer(EngineServer):
             from ..ops.gemm import split_fault_word
 
             self.loop.set_aux_fault(split_fault_word(dev))
+            cw = coll_fault_word(engine)
+            if cw:  # an IPC collective that timed out breaks the group: the replica dies
+                self.loop.set_coll_fault(cw)
         self.group = 1 + len(mirror_fds or ())
         self.dp_world = int(dp_world)
         self.loop.set_provider(self._provide)
@@ -313,6 +316,14 @@ def group_native_ok(engine: Engine, dp_split: bool) -> bool:
             and os.environ.get("ENGINE_NATIVE_LOOP", "1") != "0")
 
 
+def coll_fault_word(engine: Engine) -> int:
+    """Device address of the IPC collectives' timeout word (parallel/custom_ar.py
+    CustomAllReduce.err[0]; 0 without IPC collectives).  The Python loop raises on it in
+    LlamaModel.check_faults; the native loop reads it behind every step."""
+    car = getattr(getattr(engine.model, "comm", None), "car", None)
+    return int(car.err.data_ptr()) if car is not None else 0
+
+
 def run_follower_mirror(engine: Engine, fd: int, prefill_ctx: int) -> None:
     """A follower rank's side of the native group loop: apply the leader's frames from the
     channel ``fd`` until its stop.  Graph captures and eager prefills the leader mirrors
@@ -338,6 +349,9 @@ def run_follower_mirror(engine: Engine, fd: int, prefill_ctx: int) -> None:
         from ..ops.gemm import split_fault_word
 
         m.set_aux_fault(split_fault_word(dev))
+        cw = coll_fault_word(engine)
+        if cw:
+            m.set_coll_fault(cw)
     err = m.run()
     import torch
 
