@@ -75,9 +75,12 @@ __device__ __forceinline__ float bits_bf16(unsigned u) {
 // Epilogue of ONE wave (the block's wave 0, after the split-K reduction).  v[mt][j] is the
 // fp32 value of row m = 16 mt + 4 (lane >> 4) + j, column 16 g + (lane & 15) -- the MFMA
 // 16x16 accumulator layout.  h: the residual [M, ldh] bf16, updated in place.
+// h_pre: the lane's first residual pair (i = lane), when the caller loaded it before its
+// weight stream (nullptr: read here).
 template <int MT>
 __device__ __forceinline__ void epilogue(const float (&v)[MT][4], int M, int g, int lane,
-                                         bf16* __restrict__ h, int ldh, const FusedArArgs& fa) {
+                                         bf16* __restrict__ h, int ldh, const FusedArArgs& fa,
+                                         const unsigned* h_pre = nullptr) {
   const int r = lane & 15, q = lane >> 4;
   // per column group: the call's group g is finished by exactly one block (the launch may
   // walk several groups per block: skinny_gemm_kernel, EPI_AR)
@@ -108,7 +111,7 @@ __device__ __forceinline__ void epilogue(const float (&v)[MT][4], int M, int g, 
     const int m = i >> 3, c = i & 7;
     const size_t off = (size_t)m * row_g + c0 + c;
     unsigned* hp = reinterpret_cast<unsigned*>(h + (size_t)m * ldh + 2 * (c0 + c));
-    const unsigned hv = *hp;
+    const unsigned hv = (h_pre && i == lane) ? *h_pre : *hp;
     float a0 = bits_bf16(hv & 0xffff), a1 = bits_bf16(hv >> 16);
     u64 x[FAR_MAX_RANKS];
 #pragma unroll

@@ -109,6 +109,41 @@ __device__ __forceinline__ void skinny_body(
       }
   }
 
+  // EPI_RESID at batch 1: the residual values are loaded BEFORE the weight stream (one
+  // 2-byte load per lane of wave 0, in flight under the whole stream), so the epilogue never
+  // waits a memory round trip after the split-K reduction.  (Only this block ever writes
+  // these columns, at its very end, so the early read sees the pre-call residual.)
+  constexpr bool kEarlyResid = EPI == EPI_RESID && !MOE && MT == 1;
+  float resv[NG][MT][4];
+  float2 csv[NG][MT][4];
+  auto load_epi_operands = [&]() {
+#pragma unroll
+    for (int c = 0; c < NG; ++c)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = mt * 16 + q * 4 + j;
+          const bool ok = w == 0 && m < M;
+          resv[c][mt][j] = 0.f;
+          csv[c][mt][j] = float2{1.f, 0.f};
+          if constexpr (EPI == EPI_RESID && !MOE)
+            if (ok) resv[c][mt][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + (g0 + c) * 16 + r];
+          if constexpr (EPI == EPI_QKV_ROPE && NG > 1) {
+            const int kk = (g0 + c) & 7;
+            const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
+            if (ok) csv[c][mt][j] = ea.cs[(size_t)rpos[mt][j] * 64 + dd];
+          }
+        }
+  };
+  if constexpr (kEarlyResid) load_epi_operands();
+  // EPI_AR (fused all-reduce epilogue) at batch 1: the same for the residual pair each lane
+  // of wave 0 sums into (fused_ar.h epilogue, its first granule i = lane)
+  unsigned h_pre = 0;
+  if constexpr (EPI == EPI_AR && MT == 1)
+    if (w == 0 && lane < 8 * M)
+      h_pre = reinterpret_cast<const unsigned*>(out)[((size_t)(lane >> 3) * ldo) / 2 + (size_t)g0 * 8 + (lane & 7)];
+
   f32x4 acc[NW][MT];
   float ss[MT];
 #pragma unroll
@@ -186,31 +221,13 @@ __device__ __forceinline__ void skinny_body(
     compute1(b1, a1);
   }
 
-  // ---- epilogue operands, issued by the finishing wave (0) right after its main loop as
-  // one batch, so they land during the split-K reduction: the residual values (EPI_RESID)
-  // and, at NG > 1, the rows' (cos, sin) (EPI_QKV_ROPE).  Loaded element by element inside
-  // the store loop they were a chain of NG x MT x 4 dependent round trips (each store may
-  // alias the next load): +7 us on the 44-row qkv, +1 us per row-quad on the residual GEMMs.
-  float resv[NG][MT][4];
-  float2 csv[NG][MT][4];
-#pragma unroll
-  for (int c = 0; c < NG; ++c)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = mt * 16 + q * 4 + j;
-        const bool ok = w == 0 && m < M;
-        resv[c][mt][j] = 0.f;
-        csv[c][mt][j] = float2{1.f, 0.f};
-        if constexpr (EPI == EPI_RESID && !MOE)
-          if (ok) resv[c][mt][j] = (float)reinterpret_cast<const bf16*>(out)[(size_t)m * ldo + (g0 + c) * 16 + r];
-        if constexpr (EPI == EPI_QKV_ROPE && NG > 1) {
-          const int kk = (g0 + c) & 7;
-          const int dd = ((r < 8) ? 8 * kk + r : 64 + 8 * kk + (r - 8)) & 63;
-          if (ok) csv[c][mt][j] = ea.cs[(size_t)rpos[mt][j] * 64 + dd];
-        }
-      }
+  // ---- epilogue operands (when not loaded before the stream), issued by the finishing wave
+  // (0) right after its main loop as one batch, so they land during the split-K reduction:
+  // the residual values (EPI_RESID at MT > 1) and, at NG > 1, the rows' (cos, sin)
+  // (EPI_QKV_ROPE).  Loaded element by element inside the store loop they were a chain of
+  // NG x MT x 4 dependent round trips (each store may alias the next load): +7 us on the
+  // 44-row qkv, +1 us per row-quad on the residual GEMMs.
+  if constexpr (!kEarlyResid) load_epi_operands();
 
   // ---- split-K reduction across the block's waves ----
   if constexpr (NORM) {
@@ -286,7 +303,8 @@ __device__ __forceinline__ void skinny_body(
         if constexpr (F8) s *= ea.wscale[(size_t)g0 * 16 + r];
         v[mt][j] = acc[0][mt][j] * s;
       }
-    far::epilogue<MT>(v, M, g0, lane, reinterpret_cast<bf16*>(out), ldo, ea.far);
+    far::epilogue<MT>(v, M, g0, lane, reinterpret_cast<bf16*>(out), ldo, ea.far,
+                      MT == 1 ? &h_pre : nullptr);
     return;
   }
 #pragma unroll
