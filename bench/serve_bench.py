@@ -49,6 +49,9 @@ def main():
                          "serving loops, not multi-GPU speed)")
     ap.add_argument("--kv-pages", type=int, default=0, help="KV pages per rank (0: from free memory)")
     ap.add_argument("--ep", type=int, default=1)
+    ap.add_argument("--ep-mode", choices=("allreduce", "a2a"), default="allreduce",
+                    help="EP groups: replicated attention + all-reduce, or DP attention + "
+                         "expert all-to-all")
     ap.add_argument("--warm-rounds", type=int, default=1,
                     help="untimed rounds of the timed pattern first (every peer's requests in "
                          "sequence): graphs for the shapes the mix hits -- a prompt-chunk shape "
@@ -141,10 +144,13 @@ def cluster_main(a):
     process)."""
     from p2p_llm_chat_go_amd.engine.cluster import ClusterServer
 
+    # the replica leaders' loop (read by engine.cluster when the rank processes start)
+    os.environ["ENGINE_NATIVE_LOOP"] = "1" if a.loop == "native" else "0"
     cs = ClusterServer(a.model, gpus=a.gpus, tp=a.tp, ep=a.ep,
                        device="cpu" if a.device == "cpu" else "cuda",
                        max_batch=max(8, a.peers), max_tokens=a.new_tokens,
-                       virtual_ranks=bool(a.virtual), kv_pages=a.kv_pages or None)
+                       virtual_ranks=bool(a.virtual), kv_pages=a.kv_pages or None,
+                       ep_mode=a.ep_mode)
 
     def req(p, r):
         n = a.new_tokens - ((p * 31 + r) * 7919) % (a.jitter + 1)
@@ -179,7 +185,8 @@ def cluster_main(a):
     print(json.dumps({
         "metric": "suggest-reply tokens/sec (continuous batching, multi-GPU node)",
         "value": round(toks / el, 2), "unit": "tokens/s", "model": a.model, "gpus": a.gpus,
-        "tp": a.tp, "ep": a.ep, "replicas": m.get("replicas"), "peers": a.peers,
+        "tp": a.tp, "ep": a.ep, "ep_mode": a.ep_mode, "replicas": m.get("replicas"),
+        "peers": a.peers,
         "requests": len(results), "new_tokens": a.new_tokens, "elapsed_s": round(el, 3),
         "ttft_p50_ms": round(statistics.median(ttft), 3),
         "ttft_p99_ms": round(ttft[min(len(ttft) - 1, int(0.99 * len(ttft)))], 3),
