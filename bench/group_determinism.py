@@ -21,9 +21,14 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--fused", default="1")
     ap.add_argument("--n", type=int, default=24)
+    ap.add_argument("--repeat", type=int, default=0,
+                    help="instead: ONE group per loop, the sampled request sent this many times "
+                         "in a row (run-to-run determinism inside one serving process)")
     a = ap.parse_args()
     os.environ["P2P_TP_FUSED_AR"] = a.fused
     from test_group_native_loop_gpu import _req, _serve
+    if a.repeat:
+        return repeat_main(a)
 
     reqs = [_req(0), _req(1), _req(2, sampled=True, n=a.n), _req(3, n=40)]
     runs = {}
@@ -38,6 +43,32 @@ def main():
         for n in names:
             groups.setdefault(runs[n][i], []).append(n)
         print(json.dumps({"request": i, "distinct_replies": len(groups),
+                          "groups": list(groups.values())}), flush=True)
+
+
+def repeat_main(a):
+    from p2p_llm_chat_go_amd.engine.cluster import ClusterServer
+    from test_group_native_loop_gpu import _req
+
+    for native in (True, False):
+        os.environ.update({"ENGINE_NATIVE_LOOP": "1" if native else "0",
+                           "P2P_CAR_TIMEOUT_MS": "30000", "P2P_QA_TIMEOUT_MS": "30000"})
+        cs = ClusterServer("tiny-llama-gqa", gpus=a.world, tp=a.world, device="cuda", sd_seed=3,
+                           max_batch=2, warmup=False, virtual_ranks=True, start_timeout=600,
+                           kv_pages=256)
+        try:
+            replies = []
+            for i in range(a.repeat):
+                # a greedy request between the sampled ones, as in the test's sequence
+                json.loads(cs.handle_json(_req(1)))
+                replies.append(json.loads(cs.handle_json(_req(2, sampled=True, n=a.n)))["response"])
+        finally:
+            cs.close()
+        groups = {}
+        for i, r in enumerate(replies):
+            groups.setdefault(r, []).append(i)
+        print(json.dumps({"loop": "native" if native else "python", "world": a.world,
+                          "repeats": a.repeat, "distinct_replies": len(groups),
                           "groups": list(groups.values())}), flush=True)
 
 

@@ -93,8 +93,10 @@ def test_group_native_loop_matches_python_lockstep(world):
     # (bit-identical at 2 / 4 / 8 ranks).  Open (round 6): at 8 virtual ranks the NATIVE
     # loop's sampled reply left the Python loop's on 2 of 4 runs, at a different token each
     # time (the Python loop's reply was the same on every run; bench/group_determinism.py
-    # runs each loop twice), while every greedy reply matched.  Until that is found, a world-8
-    # sampled mismatch is reported as an expected failure, not hidden behind a shorter check.
+    # runs each loop twice), while every greedy reply matched; inside ONE group the reply is
+    # stable (12 repeats, both loops: `group_determinism.py --repeat 12`, gpurun_out/r6y_rep8.log),
+    # and the round-6 final GPU tier run matched.  Until the cause is found, a world-8 sampled
+    # mismatch is reported as an expected failure, not hidden behind a shorter check.
     open_issue = None
     for i, (a, b) in enumerate(zip(seq_n, seq_p)):
         assert a["eval_count"] == b["eval_count"]
