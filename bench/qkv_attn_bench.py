@@ -88,9 +88,12 @@ def run(name, Hq, Hkv, K, M, ctx_len, L=32, hidden=None):
                     lambda i: fused(i, wv | (ks << 8) | (2 << 16)), n_inner=L)
     res["two_kernels"] = graph_time(two, n_inner=L)
     res["qkv_only"] = graph_time(qkv_only, n_inner=L)
-    for mode, label in ((0, "fused"), (1, "fused_producers_only"), (2, "fused_handoff_only")):
+    for mode, label in ((0, "fused"), (1, "fused_producers_only"), (2, "fused_handoff_only"),
+                        (6, "fused_kv_wait_handoff_only")):
         Lb.p2p_qkv_attn_probe(mode)
         res[label] = graph_time(fused, n_inner=L)
+        if ctx_len <= 128:  # the engine's launch for <= 128 keys: 2 key waves (w4, whole groups)
+            res[label + "_kw2"] = graph_time(lambda i: fused(i, 4 | (2 << 16)), n_inner=L)
     Lb.p2p_qkv_attn_probe(0)
     torch.cuda.synchronize()
     assert int(err.item()) == 0

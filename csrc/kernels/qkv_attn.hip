@@ -64,7 +64,8 @@ struct QAArgs {
   unsigned* counters; // [M][Hkv]
   int* err;
   int n_cons;         // consumer blocks = M * Hkv
-  int probe;          // bench probe: 2 = consumers stop after the granule sweep
+  int probe;          // bench probe: 2 = consumers stop after the granule sweep, 4 = they
+                      // wait for their K / V page loads before it
   long long spin_ticks;  // hand-off spin bound (P2P_QA_TIMEOUT_MS; 5 s default)
   // o_proj role (p2p_qkv_attn_oproj; null Wo = the attention output goes to `out`)
   const bf16x8* Wo;   // o_proj weight, fragment-major [No / 16][Ko / 32][64][8]
@@ -370,6 +371,7 @@ __device__ __forceinline__ void consumer(const QAArgs& a, int b, char* smem) {
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) kr[bb][s2] = zero_bf16x8();
   }
+  if (a.probe & 4) __builtin_amdgcn_s_waitcnt(0);  // probe: this wave's pages landed first
   // 2. the current token's q (G heads), k and v from the producers' granules
   const unsigned tag = a.counters[r * Hkv + h] + 1;
   const unsigned o_epoch =
@@ -792,7 +794,8 @@ int launch_qa(const QAArgs& a, int G, int groups, hipStream_t stream) {
 static int g_qa_probe = 0;
 
 // Bench probes (bench/qkv_attn_bench.py): 1 = producers only, 2 = hand-off without the
-// attention math; 0 = the real kernel.
+// attention math, 4 (with 2) = the consumers wait for their K / V pages before the hand-off;
+// 0 = the real kernel.
 P2P_API void p2p_qkv_attn_probe(int mode) { g_qa_probe = mode; }
 
 // Fused decode qkv + RoPE + KV write + attention (see the file header).  Wt: the qkv
