@@ -59,8 +59,8 @@ std::atomic<int> g_bad{0};
 // sets its graph's fault word; the next follower eager prefill raises
 std::atomic<int> g_follower_fault{0}, g_follower_eager_fail{0};
 // a collective timeout (run_coll_fault): the next decode replay sets the collective word
-std::atomic<int> g_coll_trigger{0};
-int32_t g_coll_word = 0;
+std::atomic<int> g_coll_trigger{0}, g_fcoll_trigger{0};
+int32_t g_coll_word = 0, g_fcoll_word = 0;  // the leader's / a follower's collective word
 
 template <int I>
 int tramp() { return g_slot[I](); }
@@ -105,7 +105,8 @@ struct DecodeGraph {
       const int B = d.B, S = d.max_steps, s = step[0];
       launches++;
       if (follower && g_follower_fault.exchange(0)) errw[0] = 1;
-      if (g_coll_trigger.exchange(0)) g_coll_word = 1;
+      if (!follower && g_coll_trigger.exchange(0)) g_coll_word = 1;
+      if (follower && g_fcoll_trigger.exchange(0)) g_fcoll_word = 1;
       trace = mix(trace, (uint64_t)s);
       for (int32_t v : meta) trace = mix(trace, (uint64_t)(uint32_t)v);
       if (s >= S) {
@@ -615,6 +616,7 @@ int run_group_faults() {
     if (g_follower_eager_fail.exchange(0)) throw std::runtime_error("injected eager failure");
     return eager(p, pg, st, sm, 0);
   });
+  m.set_coll_fault(reinterpret_cast<uintptr_t>(&g_fcoll_word));
   std::string fres = "?";
   std::thread fth([&] { fres = m.run(); });
   loop.start();
@@ -641,6 +643,13 @@ int run_group_faults() {
   if (!ask(300, &e)) failures++, std::fprintf(stderr, "faults: eager request after the failure failed: %s\n", e.c_str());
   for (auto& kv : fd_)
     if (kv.second->errw[0] != 0) failures++, std::fprintf(stderr, "faults: follower word not cleared\n");
+  // last: a collective timeout on the follower (status bit 4) fails the step and kills the replica
+  g_fcoll_trigger = 1;
+  if (ask(20, &e) || e.find("collective timeout") == std::string::npos)
+    failures++, std::fprintf(stderr, "faults: follower collective timeout not reported (err '%s')\n", e.c_str());
+  if (loop.dead().find("collective timeout") == std::string::npos)
+    failures++, std::fprintf(stderr, "faults: replica not dead after a follower collective timeout\n");
+  g_fcoll_word = 0;
   auto lm = loop.metrics();
   auto mm = m.metrics();
   loop.shutdown();

@@ -969,9 +969,13 @@ void EngineLoop::collect() {
     flight_.clear();
     on_fault(aux_err_, "decode (split-K)");
   }
-  if (mirror_ && c.mseq && mirror_->await(c.mseq)) {
-    flight_.clear();
-    on_fault(nullptr, "decode (on a follower rank)");
+  if (mirror_ && c.mseq) {
+    const uint32_t bits = mirror_->await(c.mseq);
+    if (bits) {
+      flight_.clear();
+      if (bits & 4) on_coll_fault("decode (on a follower rank)");
+      on_fault(nullptr, "decode (on a follower rank)");
+    }
   }
   faults_in_row_ = 0;  // a clean decode chunk: whatever faulted before was transient
   const int32_t* hist = (const int32_t*)pinned_[kHist0 + c.buf].first;
@@ -1013,6 +1017,7 @@ void EngineLoop::collect() {
 void EngineLoop::follower_check(uint32_t seq, const char* where) {
   if (!mirror_ || !seq) return;
   const uint32_t bits = mirror_->await(seq);
+  if (bits & 4) on_coll_fault((std::string(where) + " (on a follower rank)").c_str());
   if (bits) on_fault(nullptr, (std::string(where) + (bits & 2 ? " (failed on a follower rank)"
                                                                : " (on a follower rank)")).c_str());
 }

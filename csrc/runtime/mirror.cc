@@ -227,6 +227,8 @@ uint32_t MirrorSender::await(uint32_t seq, double timeout_s) {
 EngineMirror::EngineMirror(int fd, int device) : fd_(fd), device_(device) {
   const char* e = std::getenv("P2P_MIRROR_INJECT_FAULT");
   inject_at_ = e ? std::atol(e) : 0;
+  const char* ec = std::getenv("P2P_MIRROR_INJECT_COLL");
+  inject_coll_at_ = ec ? std::atol(ec) : 0;
 }
 
 EngineMirror::~EngineMirror() {
@@ -480,7 +482,11 @@ void EngineMirror::report(uint32_t seq, const std::vector<int32_t*>& launched, u
     hip_check(h.memcpyAsync(w + nw++, e, 4, kD2H, stream_), "mirror status D2H");
   }
   if (aux_err_) hip_check(h.memcpyAsync(w + nw++, aux_err_, 4, kD2H, stream_), "mirror status D2H");
-  if (coll_err_) hip_check(h.memcpyAsync(w + nw++, coll_err_, 4, kD2H, stream_), "mirror status D2H");
+  int coll = -1;
+  if (coll_err_) {
+    coll = nw;
+    hip_check(h.memcpyAsync(w + nw++, coll_err_, 4, kD2H, stream_), "mirror status D2H");
+  }
   // the frame's tokens: host ones first (eager prefill), then the device rows, packed
   int nt = 0;
   if (!out.host.empty() || !out.copies.empty()) {
@@ -502,7 +508,7 @@ void EngineMirror::report(uint32_t seq, const std::vector<int32_t*>& launched, u
   }
   hip_check(h.eventRecord(rep_ev_[slot], stream_), "mirror status event");
   lk.lock();
-  rq_.push_back(Report{seq, host_bits, slot, nw, nt});
+  rq_.push_back(Report{seq, host_bits, slot, nw, nt, coll});
   lk.unlock();
   rcv_.notify_all();
 }
@@ -522,7 +528,7 @@ void EngineMirror::reporter() {
     uint32_t bits = rp.host_bits;
     if (h.eventSynchronize(rep_ev_[rp.slot]) != 0) bits |= 2;
     for (int i = 0; i < rp.nwords; ++i)
-      if (rep_words_[(size_t)rp.slot * kRepWords + i] != 0) bits |= 1;
+      if (rep_words_[(size_t)rp.slot * kRepWords + i] != 0) bits |= i == rp.coll ? 4 : 1;
     if (bits & 1) n_faults_++;
     std::string msg(12 + (size_t)rp.ntok * 4, '\0');
     const uint32_t head[3] = {rp.seq, bits, (uint32_t)rp.ntok};
@@ -570,8 +576,13 @@ std::string EngineMirror::run() {
         hip_check(h.streamSynchronize(stream_), "mirror drain");
         return "";
       }
-      if (!launched.empty() && ++launch_frames_ == inject_at_ && aux_err_)
-        hip_check(h.memsetAsync(aux_err_, 1, 4, stream_), "mirror fault injection");
+      if (!launched.empty()) {
+        ++launch_frames_;
+        if (launch_frames_ == inject_at_ && aux_err_)
+          hip_check(h.memsetAsync(aux_err_, 1, 4, stream_), "mirror fault injection");
+        if (launch_frames_ == inject_coll_at_ && coll_err_)
+          hip_check(h.memsetAsync(coll_err_, 1, 4, stream_), "mirror collective fault injection");
+      }
       report(seq, launched, host_bits, fout);
     }
   } catch (const std::exception& e) {

@@ -129,7 +129,8 @@ class MirrorSender {
 class EngineMirror {
  public:
   // P2P_MIRROR_INJECT_FAULT=N (tests): after the N-th frame that launches graphs, this rank
-  // sets its split-K fault word, as a slice that gave up on this rank only would
+  // sets its split-K fault word, as a slice that gave up on this rank only would;
+  // P2P_MIRROR_INJECT_COLL=N: the same for its IPC collectives' timeout word
   EngineMirror(int fd, int device);
   ~EngineMirror();
   EngineMirror(const EngineMirror&) = delete;
@@ -142,8 +143,8 @@ class EngineMirror {
   // this device's split-K fault word (p2p_split_fault_word_ptr): reported and cleared like
   // the graphs' own words
   void set_aux_fault(uintptr_t word) { aux_err_ = reinterpret_cast<int32_t*>(word); }
-  // the IPC collectives' timeout word: reported with every frame, never reset by 'F' (a
-  // collective timeout breaks the group; the leader fails steps until the replica is dead)
+  // the IPC collectives' timeout word: reported with every frame as status bit 4 and never
+  // reset by 'F' (a collective timeout breaks the group: the leader marks the replica dead)
   void set_coll_fault(uintptr_t word) { coll_err_ = reinterpret_cast<int32_t*>(word); }
   // Applies frames until the leader's stop ("" returned) or a failure (its description:
   // a closed channel, an unknown graph, a HIP error).  Blocking; call without the GIL.
@@ -197,12 +198,13 @@ class EngineMirror {
   int cur_ = 0;
   int32_t* aux_err_ = nullptr;
   int32_t* coll_err_ = nullptr;
-  long inject_at_ = 0, launch_frames_ = 0;
+  long inject_at_ = 0, inject_coll_at_ = 0, launch_frames_ = 0;
   // status reports: a ring of pinned word slots + events, drained in order by reporter()
   static constexpr int kRep = 32, kRepWords = 16, kRepToks = 8192;
   struct Report {
     uint32_t seq, host_bits;
     int slot, nwords, ntok;
+    int coll = -1;  // index of the collectives' timeout word among the words (-1: none)
   };
   int32_t* rep_words_ = nullptr;  // [kRep][kRepWords] pinned
   int32_t* rep_toks_ = nullptr;   // [kRep][kRepToks] pinned: the frame's tokens

@@ -138,6 +138,30 @@ def test_group_follower_fault_fails_the_step():
     assert after["response"] == clean[0]["response"] and after["eval_count"] == 24
 
 
+def test_group_follower_collective_timeout_kills_the_replica():
+    """A collective timeout is not transient: the rank's later IPC calls skip their waits, so
+    every sum after it is wrong.  A follower whose collectives' timeout word is set
+    (P2P_MIRROR_INJECT_COLL: after its 3rd launching frame) reports it as its own status bit;
+    the leader fails the request with the reason and marks the replica dead, and the router
+    refuses the next request instead of serving it from a broken group."""
+    import time
+
+    os.environ["P2P_MIRROR_INJECT_COLL"] = "3"
+    try:
+        cs = ClusterServer("tiny-llama-gqa", gpus=2, tp=2, device="cuda", sd_seed=3, max_batch=2,
+                           warmup=False, virtual_ranks=True, start_timeout=600, kv_pages=256)
+    finally:
+        os.environ.pop("P2P_MIRROR_INJECT_COLL", None)
+    try:
+        with pytest.raises(RuntimeError, match="collective timeout"):
+            cs.handle_json(_req(0))
+        time.sleep(2.0)  # the replica's watchdog reports the dead loop
+        with pytest.raises(RuntimeError):
+            cs.handle_json(_req(1))
+    finally:
+        cs.close()
+
+
 def _port():
     import socket
 
