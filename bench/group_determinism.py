@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--fused", default="1")
     ap.add_argument("--n", type=int, default=24)
+    ap.add_argument("--sequence", type=int, default=0,
+                    help="as the GPU test file runs it: worlds 2 and 4 (both loops) first, then "
+                         "world 8 through the native loop this many times and the Python loop once")
     ap.add_argument("--repeat", type=int, default=0,
                     help="instead: ONE group per loop, the sampled request sent this many times "
                          "in a row (run-to-run determinism inside one serving process)")
@@ -29,6 +32,8 @@ def main():
     from test_group_native_loop_gpu import _req, _serve
     if a.repeat:
         return repeat_main(a)
+    if a.sequence:
+        return sequence_main(a)
 
     reqs = [_req(0), _req(1), _req(2, sampled=True, n=a.n), _req(3, n=40)]
     runs = {}
@@ -44,6 +49,29 @@ def main():
             groups.setdefault(runs[n][i], []).append(n)
         print(json.dumps({"request": i, "distinct_replies": len(groups),
                           "groups": list(groups.values())}), flush=True)
+
+
+def sequence_main(a):
+    from test_group_native_loop_gpu import _req, _serve
+
+    reqs = [_req(0), _req(1), _req(2, sampled=True), _req(3, n=40)]
+    for w in (2, 4):
+        for native in (True, False):
+            _serve(w, native, reqs)
+        print("done world", w, flush=True)
+    replies = {}
+    for i in range(a.sequence):
+        seq, _c, _m = _serve(8, True, reqs)
+        replies["native%d" % i] = seq[2]["response"]
+        print("native", i, repr(seq[2]["response"][:60]), flush=True)
+    seq, _c, _m = _serve(8, False, reqs)
+    replies["python"] = seq[2]["response"]
+    print("python", repr(seq[2]["response"][:60]), flush=True)
+    groups = {}
+    for k, r in replies.items():
+        groups.setdefault(r, []).append(k)
+    print(json.dumps({"sequence": a.sequence, "graph_steps": os.environ.get("P2P_GROUP_GRAPH_STEPS"),
+                      "distinct_replies": len(groups), "groups": list(groups.values())}), flush=True)
 
 
 def repeat_main(a):
