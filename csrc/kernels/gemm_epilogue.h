@@ -87,10 +87,19 @@ __device__ __forceinline__ void epi_store(int m, bool valid, int g, int r, float
       key = ok > key ? ok : key;
     }
     // sharded by block id: one 64-bit atomic per (row, shard) keeps contention at
-    // ~groups/KEY_SHARDS arrivals per word instead of all groups on one word.
-    if (valid && r == 0)
-      atomicMax(reinterpret_cast<unsigned long long*>(out) + (size_t)m * KEY_SHARDS + (g % KEY_SHARDS),
-                key);
+    // ~groups/KEY_SHARDS arrivals per word instead of all groups on one word.  The 32 words
+    // of a row share two cache lines, so the atomics of a launch still serialise at one
+    // memory-side channel (8016 of them at the 8B LM head: +25 us over the fp32-logits
+    // epilogue, bench/lmhead_probe.py).  A word only grows within a launch and is reset
+    // between launches (argmax_finalize / advance, a kernel boundary apart), so any value
+    // read back is a lower bound of the word: a key not above it can never win and its
+    // atomic is skipped -- exact, and most groups after the first few skip.
+    if (valid && r == 0) {
+      unsigned long long* kp =
+          reinterpret_cast<unsigned long long*>(out) + (size_t)m * KEY_SHARDS + (g % KEY_SHARDS);
+      if (key > __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(kp, key);
+    }
   } else {
     if (!valid) return;
     const size_t o = (size_t)m * ldo + g * 16 + r;

@@ -632,6 +632,38 @@ def test_lm_head_argmax(M, offset):
     assert ic.long().tolist() == ref.tolist()
 
 
+@pytest.mark.parametrize("code", [1 | (4 << 8), 4 | (8 << 8), 8 | (4 << 8)])
+def test_lm_head_argmax_skip_is_exact(code):
+    """The argmax epilogue skips a group's atomic when the key word already holds a larger
+    key (gemm_epilogue.h): exact ties must still go to the lowest column, and a launch after
+    argmax_finalize's reset must not be filtered by the previous launch's (larger) keys."""
+    torch.manual_seed(3)
+    V, K, M = 32768, 2048, 2
+    W = (torch.randn(V, K) * 0.05).to(torch.bfloat16)
+    best = [9000, 20011]
+    W[best[0]] = W[best[0]] * 4  # a clear winner for x, copied to higher columns (exact ties)
+    for c in (best[0] + 16 * 33, 31000, 32767):
+        W[c] = W[best[0]]
+    Wt = ops.tile_weight(W).to(DEV)
+    x = torch.zeros(M, K)
+    x[0] = W[best[0]].float()
+    x[1] = W[best[1]].float() * 0.01  # second row: small logits, a different winner
+    x = x.to(torch.bfloat16)
+    keys = ops.new_argmax_keys(M, DEV)
+    ids = torch.zeros(M, dtype=torch.int32, device=DEV)
+    for _ in range(2):  # the second launch starts from the finalize's reset
+        ops.lm_head_argmax(Wt, x.to(DEV), keys, waves=code)
+        ops.argmax_finalize(keys, ids)
+        ref = (x.float() @ W.float().t()).argmax(-1)  # first index of the max (torch)
+        assert ids.cpu().long().tolist() == ref.tolist()
+        assert ids.cpu().tolist()[0] == best[0]
+    # a launch whose logits are all far below the previous launch's
+    xs = (x.float() * 1e-3).to(torch.bfloat16)
+    ops.lm_head_argmax(Wt, xs.to(DEV), keys, waves=code)
+    ops.argmax_finalize(keys, ids)
+    assert ids.cpu().long().tolist() == (xs.float() @ W.float().t()).argmax(-1).tolist()
+
+
 # ------------------------------------------------------------ MoE
 @pytest.mark.parametrize("R,E,K,e_lo,e_local", [(1, 8, 2, 0, 8), (37, 8, 2, 4, 4), (64, 4, 2, 0, 4),
                                                  (5, 16, 4, 8, 8)])
