@@ -983,6 +983,12 @@ static int pick_tile(int M, int N) {
   // profiles/r5_prefill_gemm_cold_vs_hipblaslt.jsonl)
   if (N % 128 == 0 && ((M > 128 && M <= 192) || (M > 256 && M <= 320 && N >= 16384)))
     return M <= 192 ? 7 : 6;
+  // qkv-width projections (4096 < N <= 8192) in the 384-row bucket (8 peers x ~44-token
+  // prompts): 192 x 128 tiles, split-K 2 by launch()'s rule -- llama3.1-8B qkv+RoPE 49.2 vs
+  // 57.0 us with 128 x 128 (144 tiles on 256 CUs, unsplit), cold weights
+  // (profiles/r6_prefill_gemm_384_cold.jsonl); o_proj / down (N = 4096) and gate_up measured
+  // best on their picks below
+  if (N % 128 == 0 && M > 320 && M <= 384 && N > 4096 && N <= 8192) return 7;
   const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};
   int best = 0;
   for (auto& c : cand) {

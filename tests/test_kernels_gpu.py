@@ -921,6 +921,33 @@ def test_tiled_qkv_rope_and_argmax(M, tiled_cfg):
     assert (ids.cpu().long() == ref).float().mean() > 0.98  # bf16 near-ties may differ
 
 
+def test_tiled_qkv_rope_384_rows_heuristic():
+    """The 384-row bucket at qkv width (32 + 2 x 8 heads: N = 6144) takes 192 x 128 tiles with
+    split-K 2 by the heuristic (prefill_gemm.h pick_tile): q, K and V against the fp32 path."""
+    from p2p_llm_chat_go_amd.models.config import LLAMA31_8B, rope_table
+    from p2p_llm_chat_go_amd.ops.gemm import tiled_config
+
+    tiled_config(2, 0, 0)
+    torch.manual_seed(1)
+    M, Hq, Hkv, K = 384, 32, 8, 1024
+    W = (torch.randn((Hq + 2 * Hkv) * 128, K) * 0.05).to(torch.bfloat16)
+    Wt = ops.tile_weight(W[ops.rope_row_perm(Hq + 2 * Hkv)])
+    x = torch.randn(M, K).to(torch.bfloat16)
+    cs = rope_table(LLAMA31_8B, max_pos=512)
+    pos = torch.arange(M, dtype=torch.int32)
+    slots = torch.randperm(6 * 64)[:M].to(torch.int32)
+    q_ref = torch.zeros(M, Hq * 128, dtype=torch.bfloat16)
+    kr = torch.zeros(6, Hkv, 64, 128, dtype=torch.bfloat16)
+    vr = torch.zeros_like(kr)
+    ops.qkv_rope_gemm(Wt, x, pos, slots, cs, Hq, Hkv, q_ref, kr, vr)  # CPU reference path
+    qd = torch.zeros_like(q_ref).to(DEV)
+    kd, vd = torch.zeros_like(kr).to(DEV), torch.zeros_like(vr).to(DEV)
+    ops.qkv_rope_gemm(Wt.to(DEV), x.to(DEV), pos.to(DEV), slots.to(DEV), cs.to(DEV), Hq, Hkv, qd,
+                      kd, vd)
+    assert _rel(qd.cpu(), q_ref) < 1e-2 and _rel(kd.cpu(), kr) < 1e-2 and _rel(vd.cpu(), vr) < 1e-2
+    assert ops.tiled_split_fault() == 0
+
+
 # ------------------------------------------------------------ stochastic sampler
 @pytest.mark.parametrize("V", [128256, 32000, 1003])
 def test_sample_kernel_matches_reference(V):
