@@ -973,7 +973,7 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
 // m-tile of 192 / 320 rows: at these M the tiles are bound by the per-CU LDS-DMA fill
 // rate, so the bytes staged per useful output decide, and 128-row tiles would stream
 // every weight column 2-3 times (25 % padding) while 256x256 pads up to 44 %.
-static int pick_tile(int M, int N) {
+static int pick_tile(int M, int N, int K) {
   if (M <= 64) return N % 128 == 0 ? 4 : 0;
   // (one-m-tile 384 / 448-row tiles for 321-448 rows measured 1.1-1.3x SLOWER than the
   // 128x128 split-K / phased 256x256 picks below and were removed:
@@ -981,7 +981,11 @@ static int pick_tile(int M, int N) {
   // (257-320 rows: the one-m-tile 320x128 pays on the wide gate_up only; o_proj at 288 rows
   // took 64 us with it and 39 with 128x128 split-K, cold weights:
   // profiles/r5_prefill_gemm_cold_vs_hipblaslt.jsonl)
-  if (N % 128 == 0 && ((M > 128 && M <= 192) || (M > 256 && M <= 320 && N >= 16384)))
+  // (129-192 rows, N <= 4096 with K <= 4096 -- o_proj: 32 one-m-tile tiles take split-K 4 at
+  // most, 128 blocks; 128 x 128 split-K 4 fills the 256 CUs: 30.8 vs 37.7 us for llama3.1-8B
+  // o_proj at 192 rows, cold weights, profiles/r6_prefill_gemm_sweep_cold.jsonl)
+  const bool short_k = N <= 4096 && K <= 4096;
+  if (N % 128 == 0 && ((M > 128 && M <= 192 && !short_k) || (M > 256 && M <= 320 && N >= 16384)))
     return M <= 192 ? 7 : 6;
   // qkv-width projections (4096 < N <= 8192) in the 384-row bucket (8 peers x ~44-token
   // prompts): 192 x 128 tiles, split-K 2 by launch()'s rule -- llama3.1-8B qkv+RoPE 49.2 vs
@@ -1063,7 +1067,7 @@ static int prefill_dispatch(const void* Wt, const void* X, int ldx, int M, int K
                          hipStream_t st) {
   using namespace pgemm;
   if (M <= 0 || K % BK) return (int)hipErrorInvalidValue;
-  int tile = g_prefill_tile ? g_prefill_tile : pick_tile(M, N);
+  int tile = g_prefill_tile ? g_prefill_tile : pick_tile(M, N, K);
   const int bn = (tile == 3 || tile == 4 || tile >= 6) ? 128 : 256;
   if (!tile || N % bn) return (int)hipErrorInvalidValue;
   const int up_off = (epi == EPI_SILU) ? N / 32 : 0;

@@ -921,6 +921,23 @@ def test_tiled_qkv_rope_and_argmax(M, tiled_cfg):
     assert (ids.cpu().long() == ref).float().mean() > 0.98  # bf16 near-ties may differ
 
 
+def test_tiled_oproj_192_rows_heuristic():
+    """o_proj shape (N = K = 4096) in the 192-row bucket: the heuristic's 128 x 128 split-K 4
+    pick (prefill_gemm.h pick_tile), residual epilogue against fp32."""
+    from p2p_llm_chat_go_amd.ops.gemm import tiled_config
+
+    tiled_config(2, 0, 0)
+    torch.manual_seed(2)
+    M, N, K = 192, 4096, 4096
+    W = (torch.randn(N, K) * 0.02).to(torch.bfloat16)
+    x = torch.randn(M, K).to(torch.bfloat16)
+    h = torch.randn(M, N).to(torch.bfloat16)
+    hd = h.to(DEV)
+    ops.skinny_gemm(ops.tile_weight(W).to(DEV), x.to(DEV), ops.EPI_RESID, out=hd)
+    assert _rel(hd.cpu(), h.float() + x.float() @ W.float().t()) < 1e-2
+    assert ops.tiled_split_fault() == 0
+
+
 def test_tiled_qkv_rope_384_rows_heuristic():
     """The 384-row bucket at qkv width (32 + 2 x 8 heads: N = 6144) takes 192 x 128 tiles with
     split-K 2 by the heuristic (prefill_gemm.h pick_tile): q, K and V against the fp32 path."""
