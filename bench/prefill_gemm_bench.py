@@ -37,7 +37,7 @@ def main():
                 ("v2_128x256", (2, 2, 1)), ("v2_128x128", (2, 3, 1)),
                 ("v2_128x128_s2", (2, 3, 2)), ("v2_128x128_s4", (2, 3, 4)),
                 ("v2_320x128", (2, 6, 1)), ("v2_320x128_s2", (2, 6, 2)), ("v2_192x128", (2, 7, 1)),
-                ("v2_192x128_s2", (2, 7, 2)), ("v2_256x256_s3", (2, 1, 3, 0)),
+                ("v2_192x128_s2", (2, 7, 2)), ("v2_192x256", (2, 8, 1)), ("v2_192x256_s2", (2, 8, 2)), ("v2_192x256_auto", (2, 8, 0)), ("v2_256x256_s3", (2, 1, 3, 0)),
                 ("v2_256x256_s5", (2, 1, 5, 0)), ("v2_128x256_s2", (2, 2, 2)),
                 ("v2_128x256_s3", (2, 2, 3)), ("v2_128x128_s2", (2, 3, 2))]
     L = __import__("p2p_llm_chat_go_amd.ops._lib", fromlist=["lib"]).lib()

@@ -963,6 +963,7 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
     case 5: return launch<64, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 6: return launch<320, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
     case 7: return launch<192, 128, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
+    case 8: return launch<192, 256, EPI, NORM>(Wt, X, ldx, M, K, N, up_off, out, ldo, eps, ea, st);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -973,6 +974,7 @@ int launch_tile(int tile, const void* Wt, const void* X, int ldx, int M, int K, 
 // m-tile of 192 / 320 rows: at these M the tiles are bound by the per-CU LDS-DMA fill
 // rate, so the bytes staged per useful output decide, and 128-row tiles would stream
 // every weight column 2-3 times (25 % padding) while 256x256 pads up to 44 %.
+static int g_tile8 = 1;  // the 192 x 256 gate_up pick below (A/B switch: p2p_prefill_tile8)
 static int pick_tile(int M, int N, int K) {
   if (M <= 64) return N % 128 == 0 ? 4 : 0;
   // (one-m-tile 384 / 448-row tiles for 321-448 rows measured 1.1-1.3x SLOWER than the
@@ -993,6 +995,11 @@ static int pick_tile(int M, int N, int K) {
   // (profiles/r6_prefill_gemm_384_cold.jsonl); o_proj / down (N = 4096) and gate_up measured
   // best on their picks below
   if (N % 128 == 0 && M > 320 && M <= 384 && N > 4096 && N <= 8192) return 7;
+  // SwiGLU-width projections (N >= 16384: gate_up) in the 384-row bucket: 192 x 256 tiles (2 x
+  // N/256, no padding rows) instead of the phased 256 x 256 (384 -> 512 rows): 2-8 us faster
+  // per launch in every round of an order-balanced A/B (bench/tile_ab.py,
+  // profiles/r6_tile_ab_gate_up_384.jsonl)
+  if (g_tile8 && N % 256 == 0 && M > 320 && M <= 384 && N >= 16384) return 8;
   const int cand[3][3] = {{1, 256, 256}, {2, 128, 256}, {3, 128, 128}};
   int best = 0;
   for (auto& c : cand) {
@@ -1068,7 +1075,7 @@ static int prefill_dispatch(const void* Wt, const void* X, int ldx, int M, int K
   using namespace pgemm;
   if (M <= 0 || K % BK) return (int)hipErrorInvalidValue;
   int tile = g_prefill_tile ? g_prefill_tile : pick_tile(M, N, K);
-  const int bn = (tile == 3 || tile == 4 || tile >= 6) ? 128 : 256;
+  const int bn = (tile == 3 || tile == 4 || tile == 6 || tile == 7) ? 128 : 256;
   if (!tile || N % bn) return (int)hipErrorInvalidValue;
   const int up_off = (epi == EPI_SILU) ? N / 32 : 0;
   // normed projections from 128 rows: rstd by row_rstd_kernel, GEMM without in-loop sums

@@ -198,7 +198,7 @@ int launch_tiled(const void* Wt, const void* X, int ldx, int M, int K, int n_til
 static int g_tiled_version = 2;  // 2 = LDS-DMA 8-wave kernel (prefill_gemm.h), 1 = register-staged
 
 // Benchmarks / A-B tests: version 1|2, tile 0 (heuristic) or 1..7 (256x256, 128x256, 128x128,
-// 64x128, 64x256, 320x128, 192x128),
+// 64x128, 64x256, 320x128, 192x128, 192x256),
 // splitk 0 (heuristic), 1 (off) or a forced K-slice count.
 // 256x256 prefill tiles: 1 = phased pipeline (default), 0 = the 2-stage kernel (A/B).
 P2P_API void p2p_prefill_phased(int on) { pgemm::g_phased = on ? 1 : 0; }
@@ -207,6 +207,8 @@ P2P_API void p2p_prefill_phased(int on) { pgemm::g_phased = on ? 1 : 0; }
 // one block per CU (default), 2 = deep variant always.
 // Precomputed per-row rstd for normed prefill GEMMs (A/B): 1 = on (default), 0 = in-loop sums.
 P2P_API void p2p_prefill_pre_rstd(int on) { pgemm::g_pre_rstd = on ? 1 : 0; }
+// 192 x 256 tiles for SwiGLU-width projections in the 384-row bucket (A/B): 1 = on (default)
+P2P_API void p2p_prefill_tile8(int on) { pgemm::g_tile8 = on ? 1 : 0; }
 
 P2P_API void p2p_prefill_deep(int mode) { pgemm::g_deep = (mode >= 0 && mode <= 2) ? mode : 1; }
 
@@ -249,7 +251,7 @@ P2P_API int p2p_tiled_split_fault() {
 
 P2P_API void p2p_tiled_gemm_config(int version, int tile, int splitk) {
   if (version == 1 || version == 2) g_tiled_version = version;
-  g_prefill_tile = (tile >= 0 && tile <= 7) ? tile : 0;
+  g_prefill_tile = (tile >= 0 && tile <= 8) ? tile : 0;
   pgemm::g_splitk = splitk >= 0 ? splitk : 0;
 }
 

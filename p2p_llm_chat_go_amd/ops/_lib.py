@@ -216,7 +216,8 @@ def lib():
         if fn is not None:
             fn.argtypes = []
             fn.restype = c_int
-        for name in ("p2p_prefill_phased", "p2p_prefill_deep", "p2p_prefill_pre_rstd"):
+        for name in ("p2p_prefill_phased", "p2p_prefill_deep", "p2p_prefill_pre_rstd",
+                     "p2p_prefill_tile8"):
             fn = getattr(L, name, None)
             if fn is not None:
                 fn.argtypes = [c_int]

@@ -733,7 +733,7 @@ def test_moe_route_grouped_combine(R, E, K, e_lo, e_local):
 # per CU with splitk | 8 take the parallel reduction unless the 4th field is 0
 TILED_CFGS = [(2, 0, 0), (2, 1, 1), (2, 2, 1), (2, 3, 1), (2, 3, 4), (2, 3, 4, 0), (2, 1, 3),
               (2, 4, 1), (2, 4, 2), (2, 4, 4), (2, 4, 4, 0), (2, 4, 3), (2, 5, 2), (2, 6, 1),
-              (2, 6, 4), (2, 7, 1), (2, 7, 2), (1, 0, 0)]
+              (2, 6, 4), (2, 7, 1), (2, 7, 2), (2, 8, 1), (2, 8, 2), (1, 0, 0)]
 
 
 @pytest.fixture(params=TILED_CFGS, ids=lambda c: "v%d_t%d_s%d" % c[:3] + ("_serial" if len(c) > 3 else ""))
@@ -919,6 +919,22 @@ def test_tiled_qkv_rope_and_argmax(M, tiled_cfg):
     ids = torch.zeros(M, dtype=torch.int32, device=DEV)
     ops.argmax_finalize(keys, ids)
     assert (ids.cpu().long() == ref).float().mean() > 0.98  # bf16 near-ties may differ
+
+
+def test_tiled_gate_up_384_rows_heuristic():
+    """SwiGLU width (N >= 16384) in the 384-row bucket: the heuristic's 192 x 256 tiles
+    (prefill_gemm.h pick_tile), normed SwiGLU epilogue against fp32."""
+    from p2p_llm_chat_go_amd.ops.gemm import tiled_config
+
+    tiled_config(2, 0, 0)
+    torch.manual_seed(4)
+    M, N, K = 384, 16384, 512
+    W = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    x = (torch.randn(M, K) * torch.linspace(0.3, 2.0, M)[:, None]).to(torch.bfloat16)
+    a = (x.float() @ W.float().t()) * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    act = ops.skinny_gemm(ops.tile_weight(W).to(DEV), x.to(DEV), ops.EPI_SILU, norm=True)
+    assert _rel(act.cpu(), torch.nn.functional.silu(a[:, :N // 2]) * a[:, N // 2:]) < 1e-2
+    assert ops.tiled_split_fault() == 0
 
 
 def test_tiled_oproj_192_rows_heuristic():
